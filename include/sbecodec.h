@@ -1,0 +1,183 @@
+/*
+ * sbecodec.h — C ABI of the MI355X-native batch SBE record codec.
+ *
+ * This is the drop-in boundary for the wire codec of reverb-sys/aeron-cluster-client-cpp
+ * (reference snapshot mounted at /root/reference; all file:line citations are relative to it).
+ * Every entry point is plain C: pointers, sizes and integers only.  Device pointers are HIP
+ * device (or host-pinned, device-visible) pointers; `stream` is a hipStream_t passed as void*
+ * (NULL = the default stream).  Nothing here allocates, synchronises or copies on the host:
+ * every call is an asynchronous launch on `stream` and returns after argument validation.
+ *
+ * Entry point                     replaces (reference)
+ * ------------------------------  ------------------------------------------------------------
+ * sbe_encode_topic_batch()        SBEEncoder::encode_topic_message   src/sbe_encoder.cpp:131-167
+ *                                  (decl include/aeron_cluster/sbe_messages.hpp:158-164), its live
+ *                                  twin SessionManager::Impl::create_topic_message
+ *                                  src/session_manager.cpp:1050-1115 and the correct-length encoder
+ *                                  inside ClusterClient::publish_topic src/cluster_client.cpp:1809-1864;
+ *                                  output records are what ClusterClient::offer_ingress
+ *                                  (include/aeron_cluster/cluster_client.hpp:409,
+ *                                  src/cluster_client_offer.cpp:11-20) receives one by one.
+ * sbe_decode_batch(PARSE_MESSAGE) MessageParser::parse_message      src/sbe_encoder.cpp:513-551
+ *                                  (+ parse_topic_message :724-831, decode_acknowledgment_with_sbe
+ *                                  :833-954, decode_topic_message_with_sbe :957-1143,
+ *                                  parse_session_event :618-647) → ParseResult
+ *                                  include/aeron_cluster/sbe_messages.hpp:306-412
+ * sbe_decode_batch(ON_EGRESS)     decode_ack  src/ack_decoder.cpp:29-105 (AckInfo
+ *                                  include/aeron_cluster/ack_decoder.hpp:9-15) and
+ *                                  MessageHandler::on_egress include/aeron_cluster/message_handler.hpp:35-68
+ */
+#ifndef SBECODEC_H
+#define SBECODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBECODEC_ABI_VERSION 1
+
+/* ---- return codes of every entry point ---- */
+#define SBE_OK 0
+#define SBE_EINVAL (-1)    /* bad argument (null pointer, n too large, bad mode) */
+#define SBE_EHIP (-2)      /* a HIP launch failed (hipGetLastError != hipSuccess) */
+#define SBE_ENOSPC (-3)    /* workspace too small */
+#define SBE_ENODEV (-4)    /* no gfx950 device visible */
+
+/* ---- wire constants (include/model/MessageHeader.h:95-490, TopicMessage.h:114-118,
+ *      Acknowledgment.h:114-118, include/aeron_cluster/config.hpp:169-199) ---- */
+#define SBE_HEADER_LEN 8u
+#define SBE_TM_BLOCK_LEN 16u
+#define SBE_TM_TEMPLATE_ID 1u
+#define SBE_ACK_TEMPLATE_ID 2u
+#define SBE_TOPIC_SCHEMA_ID 1u
+#define SBE_CLUSTER_SCHEMA_ID 111u
+#define SBE_SESSION_EVENT_TEMPLATE_ID 2u
+#define SBE_TM_FIELDS 5u           /* topic, messageType, uuid, payload, headers */
+#define SBE_TM_WIRE_OVERHEAD 34u   /* 8 header + 16 block + 5 x u16 length */
+#define SBE_TM_REF_OVERHEAD 26u    /* reference encode_topic_message emits 8 B less */
+#define SBE_VAR_MAX_LEN 65534u     /* TopicMessage.h:1396-1428 (E109 above this) */
+
+/* ===================================== encode ===================================== */
+
+/* encode flags */
+#define SBE_ENC_REF_TRUNCATE8 0x1u /* emit exactly what SBEEncoder::encode_topic_message returns:
+                                      buffer.resize(encodedLength()) keeps only the first
+                                      26+Σlen bytes of the wire record (src/sbe_encoder.cpp:163-164) */
+
+/* per-record encode status */
+#define SBE_ENC_OK 0u
+#define SBE_ENC_E109_TOPIC 1u        /* "topicLength too long for length type [E109]" */
+#define SBE_ENC_E109_MESSAGE_TYPE 2u /* "messageTypeLength too long for length type [E109]" */
+#define SBE_ENC_E109_UUID 3u         /* "uuidLength too long for length type [E109]" */
+#define SBE_ENC_E109_PAYLOAD 4u      /* "payloadLength too long for length type [E109]" */
+#define SBE_ENC_E109_HEADERS 5u      /* "headersLength too long for length type [E109]" */
+#define SBE_ENC_OVERFLOW 6u          /* record does not fit in out_capacity (nothing written) */
+
+/* A batch of TopicMessages in struct-of-arrays form.  Field order per record is the wire order
+ * topic, messageType, uuid, payload, headers (TopicMessage.h:515-1231).
+ *   arena      string bytes.
+ *   str_off    [n][5] byte offsets into arena, or NULL: "packed" — the strings of record 0..n-1
+ *              lie back to back in arena in record-major, field-minor order from arena[0].
+ *   str_len    [n][5] lengths (> 65534 → E109, the record emits no bytes).
+ *   timestamp  [n]; 0 is replaced by ts_default (the reference substitutes the wall clock for 0,
+ *              src/sbe_encoder.cpp:134-138; the caller passes that clock value). */
+typedef struct sbe_tm_batch {
+    const uint8_t* arena;
+    const uint32_t* str_off;
+    const uint32_t* str_len;
+    const uint64_t* timestamp;
+} sbe_tm_batch;
+
+/* Bytes of device workspace sbe_encode_topic_batch needs for n records (look-back tile state). */
+size_t sbe_encode_workspace_size(uint64_t n);
+
+/* Zero a workspace once after allocating it (hipMemsetAsync on `stream`).  Every completed
+ * sbe_encode_topic_batch leaves its workspace zeroed again, so calls need no per-call reset.
+ * A workspace serves one stream at a time; re-initialise it after a failed launch. */
+int sbe_encode_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
+
+/* Upper bound of the encoded stream for a batch whose strings total `string_bytes`. */
+uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t flags);
+
+/* Encode n TopicMessages into one packed byte stream.
+ *   out        device buffer of out_capacity bytes; record i is out[out_off[i] .. out_off[i+1]).
+ *   out_off    [n+1] u64 device array (written).
+ *   status     [n] u8 device array (written) or NULL.
+ *   workspace  device memory of >= sbe_encode_workspace_size(n) bytes, zeroed by
+ *              sbe_encode_workspace_init before its first use.
+ *   alignment  out 16 B, out_off 8 B (arena, str_off, str_len, timestamp: natural alignment).
+ * Records are independent; a failing record (E109, overflow) emits 0 bytes and the batch goes on. */
+int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
+                           uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
+/* ===================================== decode ===================================== */
+
+#define SBE_DEC_PARSE_MESSAGE 0u /* MessageParser::parse_message semantics → ParseResult */
+#define SBE_DEC_ON_EGRESS 1u     /* MessageHandler::on_egress semantics (decode_ack first) */
+
+/* per-record decode status.  Parse mode (0..31): */
+#define SBE_ST_TM 0u                 /* TopicMessage: views topic,type,uuid,payload,headers */
+#define SBE_ST_ACK 1u                /* Acknowledgment (printable-run heuristic): views 0..2 */
+#define SBE_ST_SESSION_EVENT 2u      /* SessionEvent: view 3 = detail (u32-prefixed) */
+#define SBE_ST_ERR_NULL_EMPTY 16u    /* "Null or empty data" */
+#define SBE_ST_ERR_HEADER 17u        /* "Failed to decode message header" */
+#define SBE_ST_ERR_UNKNOWN_TYPE 18u  /* "Unknown message type: template=T, schema=S" (hdr kept) */
+#define SBE_ST_ERR_SESSION_EVENT 19u /* "Failed to decode SessionEvent" */
+#define SBE_ST_ERR_SESSION_SHORT 20u /* "Session message too short to contain embedded message" */
+#define SBE_ST_ERR_EMBEDDED_SHORT 21u /* "Embedded message too short" */
+#define SBE_ST_ERR_EMBEDDED_TEMPLATE 22u /* "Unknown embedded message template_id: <param>" */
+#define SBE_ST_ERR_EMBEDDED_SCHEMA 23u   /* "Unknown embedded message schema_id: <param>" */
+#define SBE_ST_ERR_DIRECT_TEMPLATE 24u   /* "Unknown direct message template_id: <param>" */
+#define SBE_ST_ERR_TM_E100 25u       /* "SBE TopicMessage decoding failed: buffer too short [E100]" */
+#define SBE_ST_ERR_ACK_SHORT 26u     /* "Buffer too short for Acknowledgment message. Need at least
+                                         16 bytes, got <param>" */
+/* On-egress mode (32..): */
+#define SBE_ST_EG_ACK_SIMPLE 32u     /* decode_ack simple 16-B control ack; ts = timestamp_nanos */
+#define SBE_ST_EG_ACK 33u            /* decode_ack full ack; views messageId,topic,correlationId */
+#define SBE_ST_EG_TM 34u             /* topic-message callback; views topic,type,uuid,payload,headers */
+#define SBE_ST_EG_NONE 35u           /* on_egress returns without a callback */
+#define SBE_ST_EG_THROW_E100 36u     /* on_egress throws std::runtime_error("buffer too short [E100]") */
+
+/* per-record decode flags */
+#define SBE_FL_ID_DEFAULT 0x1u      /* ack: message_id = "ack_" + decimal(ts) */
+#define SBE_FL_PAYLOAD_DEFAULT 0x2u /* ack: payload = "SUCCESS" */
+#define SBE_FL_HEADERS_E100 0x4u    /* TM: headers read hit E100 and was swallowed (headers = "") */
+#define SBE_FL_SEQ_KEY 0x8u         /* TM: payload contains "_sequence_number" (jsoncpp lookup,
+                                       src/sbe_encoder.cpp:1031-1125, not evaluated: parity unpinned) */
+#define SBE_FL_WRAPPED 0x10u        /* record was a schema-111 session message (embedded decode) */
+
+/* Decoded records, struct of arrays, all device arrays of n (or n*4 / n*5) elements.
+ *   hdr      [n][4] block_length, template_id, schema_id, version as ParseResult reports them.
+ *   ts       [n] ParseResult.timestamp / AckInfo.timestamp_nanos.
+ *   view_off [n][5], view_len [n][5]: byte ranges relative to the record's first byte.
+ *            For statuses with a parameter, view_off[i*5] holds it. */
+typedef struct sbe_decoded {
+    uint8_t* status;
+    uint8_t* flags;
+    uint16_t* hdr;
+    uint64_t* ts;
+    uint32_t* view_off;
+    uint32_t* view_len;
+} sbe_decoded;
+
+/* Decode n records; record i is in[rec_off[i] .. rec_off[i+1]) (rec_off: [n+1] device u64).
+ * Record boundaries come from the transport (Aeron fragments, src/cluster_client.cpp:541-546):
+ * the SBE header carries no total length.  Alignment: in 16 B, rec_off/hdr/ts 8 B, views 4 B. */
+int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     const sbe_decoded* out, void* stream);
+
+/* ===================================== misc ===================================== */
+int sbe_abi_version(void);
+/* 1 if a gfx950 device is visible to HIP, 0 if not, <0 on HIP error. */
+int sbe_device_ready(void);
+/* Name of the last HIP error seen by this library (thread-local), "" if none. */
+const char* sbe_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SBECODEC_H */

@@ -1,0 +1,418 @@
+/*
+ * sbe_oracle.c — TEST INFRASTRUCTURE ONLY (see sbe_oracle.h).
+ *
+ * Plain-C restatement of the reference wire codec.  Every function cites the reference lines it
+ * restates (paths relative to /root/reference).  Bounds are checked BEFORE any read (the
+ * reference's getXAsString builds the string before its E100 check, TopicMessage.h:539-541;
+ * that read is discarded on the throw, so checking first changes no output).
+ */
+#include "sbe_oracle.h"
+
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline uint32_t rd32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static inline uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+static inline void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+static inline void wr64(uint8_t* p, uint64_t v) {
+    for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+/* include/aeron_cluster/protocol.hpp:37-42 */
+uint64_t orc_to_nanos_auto(uint64_t ts) { return ts < 100000000000000ULL ? ts * 1000000ULL : ts; }
+
+/* ------------------------------------------------------------------------------------------
+ * Encode.  SBEEncoder::encode_topic_message, src/sbe_encoder.cpp:131-167:
+ *   computeLength() checks each field in wire order and throws E109 above 65534
+ *   (TopicMessage.h:1382-1434); wrapAndApplyHeader writes {blockLength 16, templateId 1,
+ *   schemaId 1, version 1} (TopicMessage.h:221-238); timestamp @+0, sequenceNumber(0) @+8
+ *   (:362-374, :425-437); putX writes u16 LE length then the bytes (:515-529 ...);
+ *   buffer.resize(encodedLength()) with encodedLength = position - m_offset and m_offset = 8
+ *   (:281-284), i.e. the wire record minus its last 8 bytes.
+ * ------------------------------------------------------------------------------------------ */
+uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len[5], uint64_t ts,
+                        uint32_t flags, uint8_t* out, uint8_t* status) {
+    for (int f = 0; f < 5; ++f) {
+        if (len[f] > SBE_VAR_MAX_LEN) { /* TopicMessage.h:1396-1428 */
+            if (status) *status = (uint8_t)(SBE_ENC_E109_TOPIC + f);
+            return 0;
+        }
+    }
+    uint64_t total = SBE_TM_WIRE_OVERHEAD;
+    for (int f = 0; f < 5; ++f) total += len[f];
+    uint64_t emit = (flags & SBE_ENC_REF_TRUNCATE8) ? total - 8 : total;
+    /* build the wire record, then keep the first `emit` bytes */
+    uint8_t head[24];
+    wr16(head + 0, SBE_TM_BLOCK_LEN);
+    wr16(head + 2, SBE_TM_TEMPLATE_ID);
+    wr16(head + 4, SBE_TOPIC_SCHEMA_ID);
+    wr16(head + 6, 1); /* schema version, TopicMessage.h:117 */
+    wr64(head + 8, ts);
+    wr64(head + 16, 0);
+    uint64_t pos = 0;
+#define PUT(src, n)                                        \
+    do {                                                   \
+        uint64_t n_ = (n);                                 \
+        uint64_t k_ = pos + n_ <= emit ? n_ : emit - pos;  \
+        if (pos < emit && k_) memcpy(out + pos, (src), k_); \
+        pos += n_;                                         \
+    } while (0)
+    PUT(head, 24);
+    for (int f = 0; f < 5; ++f) {
+        uint8_t l2[2];
+        wr16(l2, (uint16_t)len[f]);
+        PUT(l2, 2);
+        if (len[f]) PUT(s[f], len[f]);
+    }
+#undef PUT
+    if (status) *status = SBE_ENC_OK;
+    return emit;
+}
+
+int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                     const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
+                     uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads) {
+    const uint64_t ovh = (flags & SBE_ENC_REF_TRUNCATE8) ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+    /* pass 1: record sizes (0 for E109) and, in packed mode, string offsets */
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t* L = str_len + 5 * i;
+        uint64_t sum = 0;
+        int bad = 0;
+        for (int f = 0; f < 5; ++f) {
+            sum += L[f];
+            if (L[f] > SBE_VAR_MAX_LEN) bad = 1;
+        }
+        out_off[i] = acc;
+        acc += bad ? 0 : ovh + sum;
+    }
+    out_off[n] = acc;
+    if (nthreads < 1) nthreads = 1;
+    if (str_off) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const uint8_t* s[5];
+            for (int f = 0; f < 5; ++f) s[f] = arena + str_off[5 * i + f];
+            uint64_t ts = timestamp[i] ? timestamp[i] : ts_default;
+            uint8_t st;
+            orc_encode_one(s, str_len + 5 * i, ts, flags, out + out_off[i], &st);
+            if (status) status[i] = st;
+        }
+    } else {
+        /* packed: string bytes of record i start at Σ_{j<i} Σlen_j (E109 records included).
+         * Split into nthreads contiguous chunks; each chunk first sums its predecessors'
+         * string bytes. */
+        int nt = nthreads;
+        uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+#endif
+        for (int t = 0; t < nt; ++t) {
+            uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk < n ? lo + chunk : n;
+            if (lo >= hi) continue;
+            /* string bytes before record lo = out_off-free recomputation over lengths */
+            uint64_t ib = 0;
+            for (uint64_t j = 0; j < lo; ++j)
+                for (int f = 0; f < 5; ++f) ib += str_len[5 * j + f];
+            for (uint64_t i = lo; i < hi; ++i) {
+                const uint32_t* L = str_len + 5 * i;
+                const uint8_t* s[5];
+                uint64_t o = ib;
+                for (int f = 0; f < 5; ++f) {
+                    s[f] = arena + o;
+                    o += L[f];
+                }
+                uint64_t ts = timestamp[i] ? timestamp[i] : ts_default;
+                uint8_t st;
+                orc_encode_one(s, L, ts, flags, out + out_off[i], &st);
+                if (status) status[i] = st;
+                ib = o;
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Decode.  Descriptor conventions: see include/sbecodec.h (views relative to record start).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    uint8_t status, flags;
+    uint16_t hdr[4]; /* block_length, template_id, schema_id, version */
+    uint64_t ts;
+    uint32_t off[5], len[5];
+} desc_t;
+
+static void set_view(desc_t* d, int k, uint64_t off, uint64_t len) {
+    d->off[k] = (uint32_t)off;
+    d->len[k] = (uint32_t)len;
+}
+
+static void fail(desc_t* d, uint8_t st, uint32_t param) {
+    memset(d, 0, sizeof(*d));
+    d->status = st;
+    d->off[0] = param;
+}
+
+static void set_hdr(desc_t* d, const uint8_t* p) {
+    d->hdr[0] = rd16(p + 0);
+    d->hdr[1] = rd16(p + 2);
+    d->hdr[2] = rd16(p + 4);
+    d->hdr[3] = rd16(p + 6);
+}
+
+/* Does [p, p+n) contain "_sequence_number"?  Marks the jsoncpp-dependent case
+ * (src/sbe_encoder.cpp:1031-1125), whose sequence_number is not evaluated (parity unpinned). */
+static int has_seq_key(const uint8_t* p, uint64_t n) {
+    static const char key[] = "_sequence_number";
+    const uint64_t k = sizeof(key) - 1;
+    if (n < k) return 0;
+    for (uint64_t i = 0; i + k <= n; ++i)
+        if (p[i] == '_' && memcmp(p + i, key, k) == 0) return 1;
+    return 0;
+}
+
+/* MessageParser::decode_topic_message_with_sbe, src/sbe_encoder.cpp:957-1143.
+ * rec = embedded record at byte `base` of the original record. */
+static void dec_tm_parse(const uint8_t* rec, uint64_t len, uint64_t base, desc_t* d) {
+    /* MessageHeader::wrap(buf,0,0,len) cannot throw here: len >= 8 by dispatch (:521-526, :772) */
+    const uint16_t blk = rd16(rec + 0), ver = rd16(rec + 6);
+    /* template/schema are 1/1 by dispatch (:792, :814), so :976-983 never fails */
+    /* wrapForDecode(buf, 8, blk, ver, len): sbeCheckPosition(8 + blk) (TopicMessage.h:240-254) */
+    uint64_t pos = 8u + blk;
+    if (pos > len) { fail(d, SBE_ST_ERR_TM_E100, 0); return; }
+    desc_t r;
+    memset(&r, 0, sizeof(r));
+    /* getTopicAsString, getMessageTypeAsString, getUuidAsString, getPayloadAsString (:1006-1009):
+     * sbePosition(pos+2) then sbePosition(pos+2+L), each throws E100 past len (:529-543) */
+    for (int f = 0; f < 4; ++f) {
+        if (pos + 2 > len) { fail(d, SBE_ST_ERR_TM_E100, 0); return; }
+        uint64_t L = rd16(rec + pos);
+        if (pos + 2 + L > len) { fail(d, SBE_ST_ERR_TM_E100, 0); return; }
+        set_view(&r, f, base + pos + 2, L);
+        pos += 2 + L;
+    }
+    r.status = SBE_ST_TM;
+    r.hdr[0] = blk;  /* block_length = acting_block_length (:1025) */
+    r.hdr[1] = 1;    /* template_id (:1022) */
+    r.hdr[2] = 1;    /* schema_id (:1023) */
+    r.hdr[3] = ver;  /* version = acting_version (:1024) */
+    r.ts = rd64(rec + 8); /* in bounds: success implies len >= 16 + blk */
+    if (base) r.flags |= SBE_FL_WRAPPED;
+    if (has_seq_key(rec + (r.off[3] - base), r.len[3])) r.flags |= SBE_FL_SEQ_KEY;
+    /* headers in their own try: E100 → headers = "" and success stays (:1127-1135) */
+    if (pos + 2 > len || pos + 2 + (uint64_t)rd16(rec + pos) > len) {
+        r.flags |= SBE_FL_HEADERS_E100;
+    } else {
+        uint64_t L = rd16(rec + pos);
+        set_view(&r, 4, base + pos + 2, L);
+    }
+    *d = r;
+}
+
+/* MessageParser::decode_acknowledgment_with_sbe, src/sbe_encoder.cpp:833-954 */
+static void dec_ack_heuristic(const uint8_t* rec, uint64_t len, uint64_t base, desc_t* d) {
+    /* len < 8 ("Buffer too short for SBE header", :842-845) is unreachable: every caller has
+     * already required 8 bytes (:521-526, :772).  template/schema are 2/1 by dispatch. */
+    if (len < 16) { fail(d, SBE_ST_ERR_ACK_SHORT, (uint32_t)len); return; } /* :868-874 */
+    desc_t r;
+    memset(&r, 0, sizeof(r));
+    set_hdr(&r, rec); /* :916-920 */
+    r.status = SBE_ST_ACK;
+    r.ts = rd64(rec + 8); /* :880 */
+    if (base) r.flags |= SBE_FL_WRAPPED;
+    /* maximal runs of bytes in [32,126] over [16,len); runs of >= 3 kept; first three
+     * become message_id, payload, headers (:890-933) */
+    int nruns = 0;
+    uint64_t run_start = 0, run_len = 0;
+    for (uint64_t i = 16; i < len && nruns < 3; ++i) {
+        uint8_t c = rec[i];
+        if (c >= 32 && c <= 126) {
+            if (run_len == 0) run_start = i;
+            ++run_len;
+        } else {
+            if (run_len >= 3) set_view(&r, nruns++, base + run_start, run_len);
+            run_len = 0;
+        }
+    }
+    if (nruns < 3 && run_len >= 3) set_view(&r, nruns++, base + run_start, run_len);
+    if (nruns < 1) r.flags |= SBE_FL_ID_DEFAULT;      /* "ack_" + to_string(ts) (:936-938) */
+    if (nruns < 2) r.flags |= SBE_FL_PAYLOAD_DEFAULT; /* "SUCCESS" (:939-941) */
+    *d = r;
+}
+
+/* MessageParser::parse_session_event + SBEDecoder::decode_session_event,
+ * src/sbe_encoder.cpp:618-647, :183-238, :285-318 */
+static void dec_session_event(const uint8_t* rec, uint64_t len, desc_t* d) {
+    if (len < 8 + 32) { fail(d, SBE_ST_ERR_SESSION_EVENT, 0); return; } /* :185-187 */
+    desc_t r;
+    memset(&r, 0, sizeof(r));
+    r.status = SBE_ST_SESSION_EVENT;
+    set_hdr(&r, rec); /* :639-644 */
+    /* detail: u32-prefixed string at 40 if it fits (extract_variable_string :285-318) */
+    uint64_t rem = len - 40;
+    if (rem >= 4) {
+        uint64_t L = rd32(rec + 40);
+        if (!(L > rem - 4 || L > 10u * 1024u * 1024u) && L > 0) set_view(&r, 3, 44, L);
+    }
+    *d = r;
+}
+
+/* MessageParser::parse_topic_message, src/sbe_encoder.cpp:724-831 */
+static void dec_topic_dispatch(const uint8_t* rec, uint64_t len, desc_t* d) {
+    const uint16_t blk = rd16(rec + 0), tmpl = rd16(rec + 2), schema = rd16(rec + 4);
+    if (schema == SBE_CLUSTER_SCHEMA_ID) {
+        uint64_t shs = 8u + blk; /* :756 */
+        if (len <= shs) { fail(d, SBE_ST_ERR_SESSION_SHORT, 0); return; }
+        const uint8_t* emb = rec + shs;
+        uint64_t elen = len - shs;
+        if (elen < 8) { fail(d, SBE_ST_ERR_EMBEDDED_SHORT, 0); return; }
+        uint16_t etmpl = rd16(emb + 2), eschema = rd16(emb + 4);
+        if (eschema == 1) {
+            if (etmpl == 1) { dec_tm_parse(emb, elen, shs, d); return; }
+            if (etmpl == 2) { dec_ack_heuristic(emb, elen, shs, d); return; }
+            fail(d, SBE_ST_ERR_EMBEDDED_TEMPLATE, etmpl);
+            return;
+        }
+        fail(d, SBE_ST_ERR_EMBEDDED_SCHEMA, eschema);
+        return;
+    }
+    /* schema == 1 here (parse_message only dispatches schema 1 or 111 to this function) */
+    if (tmpl == 1) { dec_tm_parse(rec, len, 0, d); return; }
+    if (tmpl == 2) { dec_ack_heuristic(rec, len, 0, d); return; }
+    fail(d, SBE_ST_ERR_DIRECT_TEMPLATE, tmpl); /* :820-823 */
+}
+
+/* MessageParser::parse_message, src/sbe_encoder.cpp:513-551, with the ParseResult predicates
+ * of include/aeron_cluster/sbe_messages.hpp:332-377 (message_type is still empty here, so the
+ * string clauses of is_topic_message never fire). */
+static void dec_parse_message(const uint8_t* rec, uint64_t len, desc_t* d) {
+    if (!rec || len == 0) { fail(d, SBE_ST_ERR_NULL_EMPTY, 0); return; }
+    if (len < 8) { fail(d, SBE_ST_ERR_HEADER, 0); return; } /* :174-181, :523-526 */
+    const uint16_t tmpl = rd16(rec + 2), schema = rd16(rec + 4);
+    if (tmpl == 2 && schema == SBE_CLUSTER_SCHEMA_ID) { dec_session_event(rec, len, d); return; }
+    int is_topic = (tmpl == 1 && schema == 1) || (schema == SBE_CLUSTER_SCHEMA_ID && tmpl == 1) ||
+                   (schema == 1 && tmpl == 2);
+    if (is_topic) { dec_topic_dispatch(rec, len, d); return; }
+    /* is_acknowledgment() (2/1) is covered by the third is_topic clause: never reached */
+    fail(d, SBE_ST_ERR_UNKNOWN_TYPE, 0); /* :546-549, header fields kept */
+    set_hdr(d, rec);
+}
+
+/* decode_ack, src/ack_decoder.cpp:29-105.  Returns 1 and fills d on success. */
+static int dec_ack_full(const uint8_t* rec, uint64_t len, desc_t* d) {
+    if (len < 8) return 0;
+    const uint16_t blk = rd16(rec + 0), tmpl = rd16(rec + 2), schema = rd16(rec + 4);
+    if (schema != 1 || tmpl != 2) return 0; /* :40-42 */
+    desc_t r;
+    memset(&r, 0, sizeof(r));
+    set_hdr(&r, rec);
+    if (len == 16 && blk == 8) { /* simple control ack :46-52 */
+        r.status = SBE_ST_EG_ACK_SIMPLE;
+        r.ts = orc_to_nanos_auto(rd64(rec + 8));
+        *d = r;
+        return 1;
+    }
+    /* Acknowledgment::wrapForDecode(data, 8, blk, ver, len - 8): the "len-8 bug" (:67) */
+    const uint64_t lim = len - 8;
+    uint64_t pos = 8u + blk;
+    if (pos > lim) return 0;
+    /* getXLength() peeks the u16 at the position (in bounds: pos <= len-8); getX() is called
+     * only for a non-zero length and then advances past 2+L with E100 checks (:71-96,
+     * Acknowledgment.h:410-450); a zero length leaves the position where it was. */
+    for (int f = 0; f < 3; ++f) {
+        uint64_t L = rd16(rec + pos);
+        if (L > 0) {
+            if (pos + 2 + L > lim) return 0; /* E100 → catch(...) → nullopt (:99-101) */
+            set_view(&r, f, pos + 2, L);
+            pos += 2 + L;
+        }
+    }
+    r.status = SBE_ST_EG_ACK;
+    r.ts = orc_to_nanos_auto(rd64(rec + 8)); /* len >= 16 + blk here */
+    *d = r;
+    return 1;
+}
+
+/* MessageHandler::on_egress, include/aeron_cluster/message_handler.hpp:35-68 */
+static void dec_on_egress(const uint8_t* rec, uint64_t len, desc_t* d) {
+    memset(d, 0, sizeof(*d));
+    if (!rec || len < 8) { d->status = SBE_ST_EG_NONE; return; }
+    if (dec_ack_full(rec, len, d)) return;
+    const uint16_t blk = rd16(rec + 0), tmpl = rd16(rec + 2), schema = rd16(rec + 4);
+    set_hdr(d, rec);
+    if (!(tmpl == 1 && schema == 1)) { d->status = SBE_ST_EG_NONE; return; } /* :74-79 */
+    /* TopicMessage::wrapForDecode(data, 8, blk, ver, len - 8) — no try/catch: E100 escapes */
+    const uint64_t lim = len - 8;
+    uint64_t pos = 8u + blk;
+    if (pos > lim) { d->status = SBE_ST_EG_THROW_E100; return; }
+    /* read_var_string: xLength() peek; getter only if len > 0 (:81-89) */
+    for (int f = 0; f < 5; ++f) {
+        uint64_t L = rd16(rec + pos);
+        if (L > 0) {
+            if (pos + 2 + L > lim) {
+                memset(d->off, 0, sizeof d->off);
+                memset(d->len, 0, sizeof d->len);
+                d->status = SBE_ST_EG_THROW_E100;
+                return;
+            }
+            set_view(d, f, pos + 2, L);
+            pos += 2 + L;
+        }
+    }
+    if (d->len[0] == 0) { /* empty topic → return (:63) */
+        memset(d->off, 0, sizeof d->off);
+        memset(d->len, 0, sizeof d->len);
+        d->status = SBE_ST_EG_NONE;
+        return;
+    }
+    d->status = SBE_ST_EG_TM;
+}
+
+static void decode_into(const uint8_t* rec, uint64_t len, uint32_t mode, desc_t* d) {
+    if (mode == SBE_DEC_ON_EGRESS)
+        dec_on_egress(rec, len, d);
+    else
+        dec_parse_message(rec, len, d);
+}
+
+void orc_decode_one(const uint8_t* rec, uint64_t len, uint32_t mode, uint8_t* status,
+                    uint8_t* flags, uint16_t hdr[4], uint64_t* ts, uint32_t view_off[5],
+                    uint32_t view_len[5]) {
+    desc_t d;
+    decode_into(rec, len, mode, &d);
+    *status = d.status;
+    *flags = d.flags;
+    memcpy(hdr, d.hdr, sizeof d.hdr);
+    *ts = d.ts;
+    memcpy(view_off, d.off, sizeof d.off);
+    memcpy(view_len, d.len, sizeof d.len);
+}
+
+int orc_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     uint8_t* status, uint8_t* flags, uint16_t* hdr, uint64_t* ts,
+                     uint32_t* view_off, uint32_t* view_len, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        desc_t d;
+        uint64_t a = rec_off[i], b = rec_off[i + 1];
+        decode_into(b > a ? in + a : NULL, b - a, mode, &d);
+        status[i] = d.status;
+        flags[i] = d.flags;
+        memcpy(hdr + 4 * i, d.hdr, sizeof d.hdr);
+        ts[i] = d.ts;
+        memcpy(view_off + 5 * i, d.off, sizeof d.off);
+        memcpy(view_len + 5 * i, d.len, sizeof d.len);
+    }
+    return 0;
+}

@@ -1,0 +1,55 @@
+/*
+ * sbe_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C) of the reference codec semantics, used as the parity checker by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  Never linked into, loaded
+ * by or called from the product library (libsbecodec.so) or its host mirror.
+ *
+ * Pinned by: tests/golden/ fixtures produced by oracle/_ref (the reference's own SBE-generated
+ * flyweights, compiled from the model headers under /root/reference/include by oracle/Makefile) and the
+ * reference probe observations recorded in SURVEY.md Appendix B.  See DESIGN.md §Oracle.
+ *
+ * The batch entry points produce exactly the device output layout of include/sbecodec.h.
+ */
+#ifndef SBE_ORACLE_H
+#define SBE_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/sbecodec.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One TopicMessage, SBEEncoder::encode_topic_message (src/sbe_encoder.cpp:131-167).
+ * s[f]/len[f] field f of topic,messageType,uuid,payload,headers.  Writes the record to out
+ * (capacity >= 34 + Σlen) and returns its byte count; returns 0 and sets *status on E109. */
+uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len[5], uint64_t ts,
+                        uint32_t flags, uint8_t* out, uint8_t* status);
+
+/* Batch encode with the exact semantics/outputs of sbe_encode_topic_batch (no capacity limit:
+ * out must hold sbe_encode_output_bound bytes).  nthreads > 1 uses OpenMP (two passes). */
+int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                     const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
+                     uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads);
+
+/* One record, MessageParser::parse_message (mode 0) or MessageHandler::on_egress (mode 1).
+ * Writes the descriptor fields of record slot 0 of the given arrays. */
+void orc_decode_one(const uint8_t* rec, uint64_t len, uint32_t mode, uint8_t* status,
+                    uint8_t* flags, uint16_t hdr[4], uint64_t* ts, uint32_t view_off[5],
+                    uint32_t view_len[5]);
+
+/* Batch decode: same outputs as sbe_decode_batch (host arrays). */
+int orc_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     uint8_t* status, uint8_t* flags, uint16_t* hdr, uint64_t* ts,
+                     uint32_t* view_off, uint32_t* view_len, int nthreads);
+
+/* protocol.hpp:37-42 */
+uint64_t orc_to_nanos_auto(uint64_t ts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

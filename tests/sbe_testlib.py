@@ -1,0 +1,524 @@
+"""Test-side helpers: oracle bindings (ctypes over oracle/liboracle.so), seeded record generators,
+and the ParseResult / AckInfo / on_egress materialisers that turn device descriptors back into
+the reference's result objects (include/aeron_cluster/sbe_messages.hpp:306-328,
+include/aeron_cluster/ack_decoder.hpp:9-15, include/aeron_cluster/message_handler.hpp:35-68).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use the oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "aeron-cluster-client-cpp_amd")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_LIB = os.path.join(ORACLE_DIR, "_ref", "libsbe_ref_fw.so")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+# status / flag constants (include/sbecodec.h)
+ENC_REF_TRUNCATE8 = 1
+DEC_PARSE, DEC_EGRESS = 0, 1
+ST_TM, ST_ACK, ST_SESSION_EVENT = 0, 1, 2
+ST_ERR_NULL_EMPTY, ST_ERR_HEADER, ST_ERR_UNKNOWN_TYPE = 16, 17, 18
+ST_ERR_SESSION_EVENT, ST_ERR_SESSION_SHORT, ST_ERR_EMBEDDED_SHORT = 19, 20, 21
+ST_ERR_EMBEDDED_TEMPLATE, ST_ERR_EMBEDDED_SCHEMA, ST_ERR_DIRECT_TEMPLATE = 22, 23, 24
+ST_ERR_TM_E100, ST_ERR_ACK_SHORT = 25, 26
+ST_EG_ACK_SIMPLE, ST_EG_ACK, ST_EG_TM, ST_EG_NONE, ST_EG_THROW_E100 = 32, 33, 34, 35, 36
+FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED = 1, 2, 4, 8, 16
+
+U64 = np.uint64
+
+
+# ------------------------------------------------------------------------------------------
+# oracle
+# ------------------------------------------------------------------------------------------
+def build_oracle():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True, stdout=subprocess.DEVNULL)
+
+
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_LIB):
+            build_oracle()
+        L = ctypes.CDLL(ORACLE_LIB)
+        vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        L.orc_encode_batch.argtypes = [vp, vp, vp, vp, u64, u64, u32, vp, vp, vp, i]
+        L.orc_decode_batch.argtypes = [vp, vp, u64, u32, vp, vp, vp, vp, vp, vp, i]
+        L.orc_to_nanos_auto.restype = u64
+        L.orc_to_nanos_auto.argtypes = [u64]
+        _oracle = L
+    return _oracle
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def oracle_encode(arena, str_len, ts, str_off=None, flags=0, ts_default=0, nthreads=1):
+    """arena uint8[], str_len uint32[n,5], ts uint64[n] → (out bytes, out_off uint64[n+1], status)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    str_len = np.ascontiguousarray(str_len, dtype=np.uint32).reshape(-1, 5)
+    ts = np.ascontiguousarray(ts, dtype=np.uint64)
+    n = ts.size
+    if str_off is not None:
+        str_off = np.ascontiguousarray(str_off, dtype=np.uint32).reshape(-1, 5)
+    cap = int(str_len.sum(dtype=np.uint64)) + 34 * n + 16
+    out = np.zeros(cap, dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    oracle().orc_encode_batch(_p(arena if arena.size else np.zeros(1, np.uint8)), _p(str_off), _p(str_len),
+                              _p(ts), n, ts_default, flags, _p(out), _p(out_off), _p(status), nthreads)
+    return out[: int(out_off[n])], out_off, status[:n]
+
+
+def oracle_decode(data, rec_off, mode=DEC_PARSE, nthreads=1):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = rec_off.size - 1
+    m = max(n, 1)
+    d = dict(status=np.zeros(m, np.uint8), flags=np.zeros(m, np.uint8), hdr=np.zeros((m, 4), np.uint16),
+             ts=np.zeros(m, np.uint64), view_off=np.zeros((m, 5), np.uint32), view_len=np.zeros((m, 5), np.uint32))
+    buf = data if data.size else np.zeros(1, np.uint8)
+    oracle().orc_decode_batch(_p(buf), _p(rec_off), n, mode, _p(d["status"]), _p(d["flags"]), _p(d["hdr"]),
+                              _p(d["ts"]), _p(d["view_off"]), _p(d["view_len"]), nthreads)
+    return {k: v[:n] for k, v in d.items()}
+
+
+# ------------------------------------------------------------------------------------------
+# reference flyweight harness (oracle/_ref, only where /root/reference was present to build it)
+# ------------------------------------------------------------------------------------------
+_ref = None
+
+
+def ref_available():
+    return os.path.exists(REF_LIB)
+
+
+def ref():
+    global _ref
+    if _ref is None:
+        L = ctypes.CDLL(REF_LIB)
+        vp, u64, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.ref_tm_encode.argtypes = [vp, vp, u64, i, vp, u64, vp]
+        L.ref_tm_decode_parse.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        L.ref_ack_decode.argtypes = [vp, u64, vp, vp, vp]
+        L.ref_egress_tm.argtypes = [vp, u64, vp, vp]
+        _ref = L
+    return _ref
+
+
+def ref_encode(fields, ts, wire):
+    bufs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in fields]
+    ptrs = (ctypes.c_void_p * 5)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint32 * 5)(*[len(f) for f in fields])
+    cap = 34 + sum(len(f) for f in fields) + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_uint64(0)
+    rc = ref().ref_tm_encode(ptrs, lens, ts, 1 if wire else 0, out, cap, ctypes.byref(n))
+    return rc, out.raw[: n.value]
+
+
+def _rec_buf(rec: bytes):
+    # the reference reads only inside the record when it succeeds, but its getXAsString builds
+    # the string before the bounds check (TopicMessage.h:539-541): pad the harness input so
+    # those discarded reads stay inside our allocation.
+    return ctypes.create_string_buffer(bytes(rec) + b"\0" * 65600, len(rec) + 65600)
+
+
+def ref_tm_decode(rec: bytes):
+    b = _rec_buf(rec)
+    ts, seq = ctypes.c_uint64(), ctypes.c_uint64()
+    flen = (ctypes.c_uint32 * 5)()
+    fbuf = ctypes.create_string_buffer(len(rec) * 5 + 16)
+    hok = ctypes.c_int(0)
+    rc = ref().ref_tm_decode_parse(b, len(rec), ctypes.byref(ts), ctypes.byref(seq), flen, fbuf, ctypes.byref(hok))
+    return rc, ts.value, _split(fbuf.raw, flen, 5), hok.value
+
+
+def ref_ack_decode(rec: bytes):
+    b = _rec_buf(rec)
+    ts = ctypes.c_uint64()
+    flen = (ctypes.c_uint32 * 3)()
+    fbuf = ctypes.create_string_buffer(len(rec) * 3 + 16)
+    rc = ref().ref_ack_decode(b, len(rec), ctypes.byref(ts), flen, fbuf)
+    return rc, ts.value, _split(fbuf.raw, flen, 3)
+
+
+def ref_egress_tm(rec: bytes):
+    b = _rec_buf(rec)
+    flen = (ctypes.c_uint32 * 5)()
+    fbuf = ctypes.create_string_buffer(len(rec) * 5 + 16)
+    rc = ref().ref_egress_tm(b, len(rec), flen, fbuf)
+    return rc, _split(fbuf.raw, flen, 5)
+
+
+def _split(raw, flen, k):
+    out, at = [], 0
+    for i in range(k):
+        out.append(raw[at: at + flen[i]])
+        at += flen[i]
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# materialisers: descriptor → reference result objects
+# ------------------------------------------------------------------------------------------
+def _i64(u):
+    u = int(u) & (2**64 - 1)
+    return u - 2**64 if u >= 2**63 else u
+
+
+def _view(rec, d, k):
+    o, n = int(d["view_off"][k]), int(d["view_len"][k])
+    return bytes(rec[o: o + n])
+
+
+def materialize_parse(rec: bytes, d) -> dict:
+    """ParseResult (sbe_messages.hpp:306-328) from one record's descriptor d (dict of scalars/rows)."""
+    r = dict(success=False, error_message=b"", message_type=b"", message_id=b"", payload=b"", headers=b"",
+             timestamp=0, sequence_number=0, template_id=0, schema_id=0, version=0, block_length=0,
+             correlation_id=0, session_id=0, leader_member_id=0, event_code=0, leadership_term_id=0)
+    st, fl = int(d["status"]), int(d["flags"])
+    hdr = [int(x) for x in d["hdr"]]
+    param = int(d["view_off"][0])
+
+    def take_hdr():
+        r.update(block_length=hdr[0], template_id=hdr[1], schema_id=hdr[2], version=hdr[3])
+
+    if st == ST_TM:
+        r.update(success=True, message_type=_view(rec, d, 1), message_id=_view(rec, d, 2),
+                 payload=_view(rec, d, 3), headers=_view(rec, d, 4), timestamp=_i64(d["ts"]))
+        take_hdr()
+    elif st == ST_ACK:
+        ts = int(d["ts"])
+        r.update(success=True, message_type=b"Acknowledgment", timestamp=_i64(ts),
+                 message_id=(b"ack_" + str(ts).encode()) if fl & FL_ID_DEFAULT else _view(rec, d, 0),
+                 payload=b"SUCCESS" if fl & FL_PAYLOAD_DEFAULT else _view(rec, d, 1),
+                 headers=_view(rec, d, 2))
+        take_hdr()
+    elif st == ST_SESSION_EVENT:
+        q = lambda o, f: struct.unpack_from(f, rec, o)[0]  # noqa: E731
+        r.update(success=True, message_type=b"SessionEvent", correlation_id=q(8, "<q"), session_id=q(16, "<q"),
+                 leadership_term_id=q(24, "<q"), leader_member_id=q(32, "<i"), event_code=q(36, "<i"),
+                 payload=_view(rec, d, 3), timestamp=0)
+        take_hdr()
+    else:
+        msg = {
+            ST_ERR_NULL_EMPTY: b"Null or empty data",
+            ST_ERR_HEADER: b"Failed to decode message header",
+            ST_ERR_UNKNOWN_TYPE: b"Unknown message type: template=%d, schema=%d" % (hdr[1], hdr[2]),
+            ST_ERR_SESSION_EVENT: b"Failed to decode SessionEvent",
+            ST_ERR_SESSION_SHORT: b"Session message too short to contain embedded message",
+            ST_ERR_EMBEDDED_SHORT: b"Embedded message too short",
+            ST_ERR_EMBEDDED_TEMPLATE: b"Unknown embedded message template_id: %d" % param,
+            ST_ERR_EMBEDDED_SCHEMA: b"Unknown embedded message schema_id: %d" % param,
+            ST_ERR_DIRECT_TEMPLATE: b"Unknown direct message template_id: %d" % param,
+            ST_ERR_TM_E100: b"SBE TopicMessage decoding failed: buffer too short [E100]",
+            ST_ERR_ACK_SHORT: b"Buffer too short for Acknowledgment message. Need at least 16 bytes, got %d" % param,
+        }[st]
+        r["error_message"] = msg
+        if st == ST_ERR_UNKNOWN_TYPE:
+            take_hdr()
+    return r
+
+
+def materialize_egress(rec: bytes, d):
+    """Outcome of MessageHandler::on_egress: ('ack', AckInfo dict) | ('tm', 5 fields) | ('none',) |
+    ('throw', b'buffer too short [E100]')."""
+    st = int(d["status"])
+    if st == ST_EG_ACK_SIMPLE:
+        return ("ack", dict(timestamp_nanos=int(d["ts"]), message_id=b"", topic=b"", correlation_id=b"",
+                            simple_control_ack=True))
+    if st == ST_EG_ACK:
+        return ("ack", dict(timestamp_nanos=int(d["ts"]), message_id=_view(rec, d, 0), topic=_view(rec, d, 1),
+                            correlation_id=_view(rec, d, 2), simple_control_ack=False))
+    if st == ST_EG_TM:
+        return ("tm", tuple(_view(rec, d, k) for k in range(5)))
+    if st == ST_EG_THROW_E100:
+        return ("throw", b"buffer too short [E100]")
+    assert st == ST_EG_NONE, st
+    return ("none",)
+
+
+def row(dec, i):
+    return {k: v[i] for k, v in dec.items()}
+
+
+# ------------------------------------------------------------------------------------------
+# wire builders (tests construct records the way the server / reference would)
+# ------------------------------------------------------------------------------------------
+def hdr_bytes(blk, tmpl, schema, ver):
+    return struct.pack("<HHHH", blk, tmpl, schema, ver)
+
+
+def tm_wire(fields, ts, blk=16, ver=1, seq=0):
+    b = hdr_bytes(blk, 1, 1, ver) + struct.pack("<QQ", ts & (2**64 - 1), seq)
+    for f in fields:
+        b += struct.pack("<H", len(f)) + bytes(f)
+    return b
+
+
+def ack_wire(msg_id, topic, corr, ts, blk=8, ver=1):
+    b = hdr_bytes(blk, 2, 1, ver) + struct.pack("<Q", ts)
+    for f in (msg_id, topic, corr):
+        b += struct.pack("<H", len(f)) + bytes(f)
+    return b
+
+
+def simple_ack(ts, ver=1):
+    return hdr_bytes(8, 2, 1, ver) + struct.pack("<Q", ts)
+
+
+def session_wrap(rec, term=7, session=9, blk=24):
+    return hdr_bytes(blk, 1, 111, 8) + struct.pack("<qqq", term, session, 0) + b"\0" * max(0, blk - 24) + rec
+
+
+def session_event(corr, sess, term, leader, code, detail=b"", blk=32):
+    b = hdr_bytes(blk, 2, 111, 8) + struct.pack("<qqqii", corr, sess, term, leader, code)
+    if detail is not None:
+        b += struct.pack("<I", len(detail)) + detail
+    return b
+
+
+def pack_records(recs):
+    off = np.zeros(len(recs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in recs], dtype=np.uint64) if recs else []
+    data = np.frombuffer(b"".join(bytes(r) for r in recs), dtype=np.uint8).copy() if recs else np.zeros(0, np.uint8)
+    return data, off
+
+
+# ------------------------------------------------------------------------------------------
+# seeded synthetic workloads; splitmix64 so every component sees the same bytes
+# ------------------------------------------------------------------------------------------
+def splitmix64(seed: int, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = (U64(seed) + U64(0x9E3779B97F4A7C15) * (np.arange(1, n + 1, dtype=U64)))
+        z = x
+        z = (z ^ (z >> U64(30))) * U64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> U64(27))) * U64(0x94D049BB133111EB)
+        return z ^ (z >> U64(31))
+
+
+def _digits(v: np.ndarray, width: int) -> np.ndarray:
+    """uint64[n] → uint8[n,width] zero-padded decimal of v mod 10**width."""
+    v = v.copy()
+    out = np.empty((v.size, width), dtype=np.uint8)
+    for k in range(width - 1, -1, -1):
+        out[:, k] = (v % U64(10)).astype(np.uint8) + ord("0")
+        v //= U64(10)
+    return out
+
+
+# payload template (143 B) and headers template (32 B): fixed-256 Order records
+_PAYLOAD_T = (b'{"side":"BUY","symbol":"BTC-USD","qty":"#########","price":"#########.##",'
+              b'"client_order_id":"cid_#################","type":"LIMIT","tif":"GTC"}')
+_HEADERS_T = b'{"messageType":"CREATE_ORDER"}  '
+
+
+def fixed256_orders(n: int, seed: int = 0x5EED0002):
+    """topic "orders", type "CREATE_ORDER", uuid msg_<19d>_<5d>,
+    payload 143 B, headers 32 B: Σlen = 222, wire record 256 B.  Packed SoA."""
+    assert len(_PAYLOAD_T) == 143 and len(_HEADERS_T) == 32, (len(_PAYLOAD_T), len(_HEADERS_T))
+    r = splitmix64(seed, 4 * n).reshape(n, 4)
+    ts = (U64(1_760_000_000_000_000_000) + np.arange(n, dtype=U64))
+    uuid = np.empty((n, 29), np.uint8)
+    uuid[:, :4] = np.frombuffer(b"msg_", np.uint8)
+    uuid[:, 4:23] = _digits(ts, 19)
+    uuid[:, 23] = ord("_")
+    uuid[:, 24:29] = _digits(r[:, 0], 5)
+    pay = np.tile(np.frombuffer(_PAYLOAD_T, np.uint8), (n, 1))
+    hol = [i for i, c in enumerate(_PAYLOAD_T) if c == ord("#")]
+    qty, price, cid = hol[:9], hol[9:20], hol[20:]
+    pay[:, qty] = _digits(r[:, 1], 9)
+    pay[:, price] = _digits(r[:, 2], 11)
+    pay[:, cid] = _digits(r[:, 3], 17)
+    rec = np.concatenate([np.tile(np.frombuffer(b"orders", np.uint8), (n, 1)),
+                          np.tile(np.frombuffer(b"CREATE_ORDER", np.uint8), (n, 1)),
+                          uuid, pay, np.tile(np.frombuffer(_HEADERS_T, np.uint8), (n, 1))], axis=1)
+    str_len = np.tile(np.array([6, 12, 29, 143, 32], np.uint32), (n, 1))
+    return rec.reshape(-1), str_len, ts
+
+
+_TOPICS = [b"orders", b"order_request_topic", b"order_notification_topic"]
+_TYPES = [b"CREATE_ORDER", b"UPDATE_ORDER"]
+
+
+def var_orders(n: int, seed: int = 0x5EED0004):
+    """SURVEY §8(d) config 4 (variable length): topic ∈ 3 names, type ∈ 2, uuid 29 B, payload
+    uniform [32,480] with a 3–10 B symbol, headers uniform [16,64].  Packed SoA."""
+    r = splitmix64(seed, 6 * n).reshape(n, 6)
+    ti = (r[:, 0] % U64(3)).astype(np.int64)
+    yi = (r[:, 1] % U64(2)).astype(np.int64)
+    plen = (U64(32) + r[:, 2] % U64(449)).astype(np.int64)
+    hlen = (U64(16) + r[:, 3] % U64(49)).astype(np.int64)
+    slen = (U64(3) + r[:, 4] % U64(8)).astype(np.int64)
+    tlen = np.array([len(t) for t in _TOPICS])[ti]
+    ylen = np.array([len(t) for t in _TYPES])[yi]
+    str_len = np.stack([tlen, ylen, np.full(n, 29), plen, hlen], axis=1).astype(np.uint32)
+    ts = (U64(1_760_000_000_000_000_000) + np.arange(n, dtype=U64))
+    tot = str_len.astype(np.int64).sum(1)
+    starts = np.zeros(n + 1, np.int64)
+    starts[1:] = np.cumsum(tot)
+    arena = np.empty(int(starts[-1]), np.uint8)
+    # fill with printable filler derived from the random stream, then lay the fixed pieces
+    fill = splitmix64(seed ^ 0xABCDEF, (arena.size + 7) // 8).view(np.uint8)[: arena.size]
+    arena[:] = (fill % 94) + 32
+    arena[arena == ord('_')] = ord('-')  # keep "_sequence_number" out of synthetic payloads
+    base = starts[:-1]
+    for k, t in enumerate(_TOPICS):
+        idx = base[ti == k]
+        arena[idx[:, None] + np.arange(len(t))] = np.frombuffer(t, np.uint8)
+    tb = base + tlen
+    for k, t in enumerate(_TYPES):
+        idx = tb[yi == k]
+        arena[idx[:, None] + np.arange(len(t))] = np.frombuffer(t, np.uint8)
+    ub = tb + ylen
+    arena[ub[:, None] + np.arange(4)] = np.frombuffer(b"msg_", np.uint8)
+    arena[ub[:, None] + 4 + np.arange(19)] = _digits(ts, 19)
+    arena[ub + 23] = ord("-")
+    arena[ub[:, None] + 24 + np.arange(5)] = _digits(r[:, 5], 5)
+    pb = ub + 29
+    arena[pb[:, None] + np.arange(10)] = np.frombuffer(b'{"symbol":', np.uint8)
+    return arena, str_len, ts
+
+
+def mixed_records(n: int, seed: int = 0x5EED0003):
+    """69 % TM-256, 15 % Ack-73 (exact), 15 % Ack-81 (+8 B slack),
+    1 % simple 16-B ack, randomly interleaved; returns (data, rec_off)."""
+    arena, str_len, ts = fixed256_orders(n, seed)
+    recs_tm = arena.reshape(n, 222)
+    kind = (splitmix64(seed ^ 0x77, n) % U64(100)).astype(np.int64)
+    kind = np.where(kind < 69, 0, np.where(kind < 84, 1, np.where(kind < 99, 2, 3)))
+    sizes = np.array([256, 73, 81, 16])[kind]
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(sizes)
+    data = np.zeros(int(off[-1]), np.uint8)
+    ts_ms = U64(1_760_000_000_000) + np.arange(n, dtype=U64)
+    tsb = ts.view(np.uint8).reshape(n, 8)
+    tsm = ts_ms.view(np.uint8).reshape(n, 8)
+    # TopicMessage
+    i = np.nonzero(kind == 0)[0]
+    b = off[i]
+    data[b[:, None] + np.arange(8)] = np.frombuffer(hdr_bytes(16, 1, 1, 1), np.uint8)
+    data[b[:, None] + 8 + np.arange(8)] = tsb[i]
+    pos = 24
+    col = 0
+    for L in (6, 12, 29, 143, 32):
+        data[b[:, None] + pos + np.arange(2)] = np.frombuffer(struct.pack("<H", L), np.uint8)
+        data[b[:, None] + pos + 2 + np.arange(L)] = recs_tm[i, col: col + L]
+        pos += 2 + L
+        col += L
+    # full acks (exact and +8 slack): messageId = uuid (29), topic "orders", corr 16 digits
+    for k in (1, 2):
+        i = np.nonzero(kind == k)[0]
+        b = off[i]
+        data[b[:, None] + np.arange(8)] = np.frombuffer(hdr_bytes(8, 2, 1, 1), np.uint8)
+        data[b[:, None] + 8 + np.arange(8)] = tsm[i]
+        data[b[:, None] + 16 + np.arange(2)] = np.frombuffer(struct.pack("<H", 29), np.uint8)
+        data[b[:, None] + 18 + np.arange(29)] = recs_tm[i, 18:47]
+        data[b[:, None] + 47 + np.arange(2)] = np.frombuffer(struct.pack("<H", 6), np.uint8)
+        data[b[:, None] + 49 + np.arange(6)] = np.frombuffer(b"orders", np.uint8)
+        data[b[:, None] + 55 + np.arange(2)] = np.frombuffer(struct.pack("<H", 16), np.uint8)
+        data[b[:, None] + 57 + np.arange(16)] = recs_tm[i, 18 + 4: 18 + 20]
+    i = np.nonzero(kind == 3)[0]
+    b = off[i]
+    data[b[:, None] + np.arange(8)] = np.frombuffer(hdr_bytes(8, 2, 1, 1), np.uint8)
+    data[b[:, None] + 8 + np.arange(8)] = tsm[i]
+    return data, off.astype(np.uint64)
+
+
+# ------------------------------------------------------------------------------------------
+# edge-case records (decode): every status of both modes, ragged lengths, all prefixes
+# ------------------------------------------------------------------------------------------
+def edge_records():
+    """[(name, bytes)] covering the reference's branches."""
+    f5 = [b"orders", b"CREATE_ORDER", b"msg_1", b'{"a":1}', b'{"h":2}']
+    tm = tm_wire(f5, 0x1122334455667788)
+    ack = ack_wire(b"msg_42", b"orders", b"corr-1", 1_700_000_000_000)
+    out = [
+        ("tm_wire", tm),
+        ("tm_ref_trunc", tm[:-8]),
+        ("tm_slack8", tm + b"\0" * 8),
+        ("tm_slack3", tm + b"\0" * 3),
+        ("tm_slack8_empty_type", tm_wire([b"t", b"", b"u", b"p", b"h"], 4) + b"\0" * 8),
+        ("tm_slack8_blk0", tm_wire(f5, 5, blk=0) + b"\0" * 8),
+        ("tm_cut_in_payload", tm[:50]),
+        ("tm_blk8", tm_wire(f5, 5, blk=8)),
+        ("tm_blk0", tm_wire(f5, 5, blk=0)),
+        ("tm_blk40", tm_wire(f5, 5, blk=40)),
+        ("tm_blk_huge", tm_wire(f5, 5, blk=60000)),
+        ("tm_all_empty", tm_wire([b""] * 5, 9)),
+        ("tm_empty_topic", tm_wire([b"", b"T", b"u", b"p", b"h"], 9)),
+        ("tm_empty_headers", tm_wire(f5[:4] + [b""], 9)),
+        ("tm_seq_key", tm_wire(f5[:3] + [b'{"_sequence_number":17}', b"{}"], 3)),
+        ("tm_seq_key_nested", tm_wire(f5[:3] + [b'{"message":{"_sequence_number":"4"}}', b"{}"], 3)),
+        ("tm_ver7", tm_wire(f5, 1, ver=7)),
+        ("tm_nonprintable", tm_wire([b"\x00\x01", b"\xff" * 3, b"\x7f", b"\x80abc", b"\n"], 2**64 - 1)),
+        ("wrapped_tm", session_wrap(tm)),
+        ("wrapped_tm_blk32", session_wrap(tm, blk=32)),
+        ("wrapped_ack", session_wrap(ack)),
+        ("wrapped_simple_ack", session_wrap(simple_ack(1000))),
+        ("wrapped_short_ack", session_wrap(simple_ack(1000)[:12])),
+        ("wrapped_only_header", session_wrap(b"")),
+        ("wrapped_emb_short", session_wrap(b"\x01\x02\x03")),
+        ("wrapped_emb_tmpl9", session_wrap(hdr_bytes(16, 9, 1, 1) + b"x" * 20)),
+        ("wrapped_emb_schema5", session_wrap(hdr_bytes(16, 1, 5, 1) + b"x" * 20)),
+        ("wrapped_tm_trunc", session_wrap(tm[:-8])),
+        ("wrapped_tm_cut", session_wrap(tm[:40])),
+        ("unknown_tmpl9", hdr_bytes(16, 9, 1, 1) + b"\0" * 30),
+        ("unknown_schema7", hdr_bytes(16, 1, 7, 1) + b"\0" * 30),
+        ("unknown_111_tmpl5", hdr_bytes(16, 5, 111, 8) + b"\0" * 30),
+        ("simple_ack_ms", simple_ack(1_000_000_000_000)),
+        ("simple_ack_ns", simple_ack(1_760_000_000_123_456_789)),
+        ("simple_ack_blk16", hdr_bytes(16, 2, 1, 1) + struct.pack("<Q", 12345)),
+        ("ack_exact", ack),
+        ("ack_slack8", ack + b"\0" * 8),
+        ("ack_slack7", ack + b"\0" * 7),
+        ("ack_zero_msgid", ack_wire(b"", b"orders", b"corr-1", 77) + b"\0" * 8),
+        ("ack_zero_topic", ack_wire(b"m1", b"", b"corr-1", 77) + b"\0" * 8),
+        ("ack_glue", ack_wire(b"A" * 0x41, b"orders", b"B" * 0x2041, 123) + b"\0" * 8),
+        ("ack_no_runs", hdr_bytes(8, 2, 1, 1) + struct.pack("<Q", 5) + bytes([1, 2, 0, 200, 31, 127, 10])),
+        ("ack_runs_2char", hdr_bytes(8, 2, 1, 1) + struct.pack("<Q", 5) + b"ab\0cd\0xyz"),
+        ("ack_4runs", hdr_bytes(8, 2, 1, 1) + struct.pack("<Q", 6) + b"one\0two\0three\0four"),
+        ("ack_blk0", ack_wire(b"id", b"t", b"c", 8, blk=0) + b"\0" * 8),
+        ("ack_blk40", ack_wire(b"id", b"t", b"c", 8, blk=40) + b"\0" * 60),
+        ("ack_len8", hdr_bytes(8, 2, 1, 1)),
+        ("ack_len15", hdr_bytes(8, 2, 1, 1) + b"1234567"),
+        ("session_event_min", session_event(1, 2, 3, 4, 0, detail=None)),
+        ("session_event_detail", session_event(-1, 2**40, 3, 1, 2, detail=b"redirect:host:1234")),
+        ("session_event_detail_empty", session_event(1, 2, 3, 4, 1, detail=b"")),
+        ("session_event_detail_long", session_event(1, 2, 3, 4, 1, detail=b"abc")[:-1]),
+        ("session_event_short", session_event(1, 2, 3, 4, 0, detail=None)[:39]),
+        ("session_event_3b_tail", session_event(1, 2, 3, 4, 0, detail=None) + b"\x01\x00\x00"),
+        ("empty", b""),
+    ]
+    for k in range(1, 8):
+        out.append((f"len{k}", tm[:k]))
+    for k in range(0, len(tm) + 1, 3):
+        out.append((f"tm_prefix{k}", tm[:k]))
+    w = session_wrap(tm)
+    for k in range(30, len(w) + 1, 5):
+        out.append((f"wrapped_prefix{k}", w[:k]))
+    for k in range(8, len(ack) + 9):
+        out.append((f"ack_prefix{k}", (ack + b"\0" * 8)[:k]))
+    rng = np.random.default_rng(1234)
+    for k in range(40):
+        hdrs = [(16, 1, 1, 1), (8, 2, 1, 1), (24, 1, 111, 8), (32, 2, 111, 8), (0, 1, 1, 0), (200, 1, 1, 1)]
+        h = hdrs[k % len(hdrs)]
+        body = rng.integers(0, 256, size=int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+        if k % 3 == 0:  # mostly-printable bodies with small length prefixes
+            body = bytes((b % 6) if i % 9 == 0 else (32 + b % 95) for i, b in enumerate(body))
+        out.append((f"random{k}", hdr_bytes(*h) + body))
+    return out

@@ -1,0 +1,168 @@
+"""GPU parity: the HIP codec (through the C ABI) against the oracle, bit-exact.
+
+Sizes keep the oracle to seconds; full-size configurations are checked through size-independent
+properties (round trip, offsets monotone, byte checksums) in test_gpu_scale.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+import sbe_testlib as T
+
+pytestmark = pytest.mark.gpu
+
+
+def to_dev(a, dtype):
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view({torch.uint8: np.uint8, torch.int32: np.int32, torch.int64: np.int64}[dtype])
+                            ).to("cuda")
+
+
+def gpu_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
+    a = to_dev(arena if arena.size else np.zeros(16, np.uint8), torch.uint8)
+    L = to_dev(np.asarray(str_len, np.uint32).reshape(-1, 5), torch.int32)
+    t = to_dev(np.asarray(ts, np.uint64), torch.int64)
+    o = None if str_off is None else to_dev(np.asarray(str_off, np.uint32).reshape(-1, 5), torch.int32)
+    enc = codec.encode_topic_batch(a, L, t, str_off=o, flags=flags, ts_default=ts_default)
+    torch.cuda.synchronize()
+    assert codec.workspace_error(enc.workspace) == 0
+    off = enc.out_off.cpu().numpy().view(np.uint64)
+    n = ts.size
+    out = enc.out[: int(off[n])].cpu().numpy()
+    return out, off, enc.status.cpu().numpy()
+
+
+def gpu_decode(codec, data, rec_off, mode):
+    d = to_dev(data if data.size else np.zeros(16, np.uint8), torch.uint8)
+    r = to_dev(np.asarray(rec_off, np.uint64), torch.int64)
+    dec = codec.decode_batch(d, r, mode=mode)
+    torch.cuda.synchronize()
+    return dec.numpy()
+
+
+def assert_same_decode(got, exp):
+    for k in exp:
+        g, e = got[k], exp[k]
+        if not np.array_equal(g, e):
+            bad = np.nonzero((g != e).reshape(len(e), -1).any(1))[0]
+            raise AssertionError(f"{k} differs at records {bad[:10]}: got {g[bad[:3]]} expected {e[bad[:3]]}")
+
+
+def check_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
+    go, goff, gst = gpu_encode(codec, arena, str_len, ts, str_off, flags, ts_default)
+    eo, eoff, est = T.oracle_encode(arena, str_len, ts, str_off, flags, ts_default)
+    np.testing.assert_array_equal(goff, eoff)
+    np.testing.assert_array_equal(gst, est)
+    if not np.array_equal(go, eo):
+        i = int(np.nonzero(go != eo)[0][0])
+        rec = int(np.searchsorted(eoff, i, side="right") - 1)
+        raise AssertionError(f"output byte {i} (record {rec}) differs: {go[i]} != {eo[i]}")
+    return go, goff
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 64 * 37 + 5])
+def test_encode_fixed256(codec, n, flags):
+    arena, L, ts = T.fixed256_orders(n)
+    check_encode(codec, arena, L, ts, flags=flags)
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+def test_encode_var(codec, flags):
+    arena, L, ts = T.var_orders(20000)
+    check_encode(codec, arena, L, ts, flags=flags)
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+def test_encode_gather_mode(codec, flags):
+    # explicit per-field offsets into a shuffled arena, ragged alignment
+    arena, L, ts = T.var_orders(5000, seed=99)
+    n = ts.size
+    starts = np.zeros(n * 5 + 1, np.int64)
+    starts[1:] = np.cumsum(L.reshape(-1).astype(np.int64))
+    perm = np.random.default_rng(3).permutation(n * 5)
+    pieces = [arena[starts[k]: starts[k + 1]] for k in range(n * 5)]
+    new = np.zeros(len(arena) + 3 * n * 5 + 7, np.uint8)
+    off = np.zeros(n * 5, np.uint32)
+    at = 7
+    for k in perm:
+        off[k] = at
+        new[at: at + len(pieces[k])] = pieces[k]
+        at += len(pieces[k]) + (k % 3)
+    check_encode(codec, new, L, ts, str_off=off, flags=flags)
+
+
+def test_encode_edges(codec):
+    rng = np.random.default_rng(7)
+    lens = [[0, 0, 0, 0, 0], [1, 0, 0, 0, 0], [0, 0, 0, 0, 1], [6, 12, 29, 0, 0],
+            [65534, 0, 1, 2, 3], [65535, 0, 0, 0, 0], [0, 65535, 0, 0, 0], [0, 0, 65535, 0, 0],
+            [0, 0, 0, 65535, 0], [0, 0, 0, 0, 65535], [70000, 70000, 0, 0, 1],
+            [3, 3, 3, 65534, 65534], [65534] * 5, [5, 6, 7, 8, 9]]
+    for _ in range(200):
+        lens.append(list(rng.integers(0, 40, 5)))
+    L = np.array(lens, np.uint32)
+    n = len(L)
+    arena = rng.integers(0, 256, int(L.sum(dtype=np.int64)), dtype=np.uint8)
+    ts = rng.integers(0, 2**63, n, dtype=np.uint64)
+    ts[::7] = 0  # 0 → ts_default (the reference substitutes its clock, src/sbe_encoder.cpp:134-138)
+    for flags in (0, T.ENC_REF_TRUNCATE8):
+        check_encode(codec, arena, L, ts, flags=flags, ts_default=1_760_000_000_123)
+
+
+def test_encode_empty_batch(codec):
+    out, off, st = gpu_encode(codec, np.zeros(0, np.uint8), np.zeros((0, 5), np.uint32), np.zeros(0, np.uint64))
+    assert off.tolist() == [0] and out.size == 0
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_edges(codec, mode):
+    recs = [r for _, r in T.edge_records()]
+    data, off = T.pack_records(recs)
+    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_edges_every_alignment(codec, mode):
+    # the same records behind 0..15 bytes of lead-in, so each one starts at every offset mod 16
+    recs = [r for _, r in T.edge_records()]
+    for lead in range(16):
+        allr = [b"\0" * lead] + recs
+        data, off = T.pack_records(allr)
+        assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_mixed(codec, mode):
+    data, off = T.mixed_records(50000)
+    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_large_records(codec, mode):
+    # records far larger than the 16 KiB LDS window (global-memory read path)
+    rng = np.random.default_rng(11)
+    recs = []
+    for k in range(200):
+        f = [rng.integers(32, 127, int(rng.integers(0, 9000)), dtype=np.uint8).tobytes() for _ in range(5)]
+        r = T.tm_wire(f, k)
+        recs.append(r if k % 4 else r + b"\0" * 8)
+        recs.append(T.ack_wire(f[0][:500], f[1][:300], f[2][:70], k) + b"\0" * (k % 9))
+    data, off = T.pack_records(recs)
+    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+def test_roundtrip_materialized(codec, flags):
+    # encode on the GPU, decode on the GPU, rebuild ParseResults: fields come back byte-identical
+    arena, L, ts = T.var_orders(3000, seed=5)
+    out, off, st = gpu_encode(codec, arena, L, ts, flags=flags)
+    dec = gpu_decode(codec, out, off, T.DEC_PARSE)
+    starts = np.concatenate([[0], np.cumsum(L.reshape(-1).astype(np.int64))])
+    for i in range(ts.size):
+        rec = bytes(out[off[i]: off[i + 1]])
+        pr = T.materialize_parse(rec, T.row(dec, i))
+        f = [bytes(arena[starts[5 * i + k]: starts[5 * i + k + 1]]) for k in range(5)]
+        assert pr["success"] and pr["message_type"] == f[1] and pr["message_id"] == f[2] and pr["payload"] == f[3]
+        assert pr["timestamp"] == int(ts[i]) and pr["block_length"] == 16
+        # wire form keeps headers; the reference-truncated form loses them to E100
+        assert pr["headers"] == (b"" if flags else f[4])
