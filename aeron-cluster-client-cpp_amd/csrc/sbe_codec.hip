@@ -6,12 +6,12 @@
 //
 //  encode  (SBEEncoder::encode_topic_message, src/sbe_encoder.cpp:131-167)
 //    1. lane loads its record's 5 lengths + timestamp, wave-scans output (and, packed, input) sizes
-//    2. tile base offsets by single-pass decoupled look-back over per-tile 8-byte status words
-//       (flag | value in one word → no payload hand-off; tile ids from an atomic ticket, so every
-//       tile waited on is already running: no dispatch-order assumption)
-//    3. each lane composes its wire record (header, ts, seq=0, u16 len + bytes ×5) as aligned
-//       dwords into an XOR-swizzled LDS window; record edges use byte writes
-//    4. the wave stores the window with global_store_dwordx4 (edge chunks byte-wise)
+//    2. tile/block byte counts (K1) and their exclusive scan (K2) give every tile its offsets
+//    3. K3, one wave per 64-record tile, per output window: the window's input strings (packed
+//       mode) are staged into LDS with global_load_dwordx4; each lane writes its record into an
+//       XOR-swizzled LDS output window (string interiors as aligned dwords: one LDS read, one
+//       v_alignbyte, one ds_write_b32; literals and string edges as bytes); the wave then stores
+//       the window with global_store_dwordx4
 //  decode  (MessageParser::parse_message :513-551 / MessageHandler::on_egress
 //           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105)
 //    1. the wave stages its tile's contiguous bytes into the same swizzled LDS window with
@@ -31,9 +31,6 @@ constexpr int kWave = 64;
 constexpr int kTile = 64;                 // records per workgroup (one per lane)
 constexpr uint32_t kWin = 16384;          // LDS window bytes (encode output / decode input)
 constexpr uint32_t kWinDw = kWin / 4;
-constexpr uint64_t kFlagAgg = 1ull << 62; // look-back status word: [63:62] flag, [61:0] value
-constexpr uint64_t kFlagInc = 2ull << 62;
-constexpr uint64_t kValMask = (1ull << 62) - 1;
 
 // ------------------------------------------------------------------------------------------
 // LDS window.  Dword i of the window lives at i ^ ((i >> 6) & 31): lanes that write dword j of
@@ -97,30 +94,33 @@ __device__ __forceinline__ uint32_t byte_mask_bits(uint32_t nbytes) {
     return nbytes >= 4 ? 0xffffffffu : ((1u << (8u * nbytes)) - 1u);
 }
 
-// ------------------------------------------------------------------------------------------
-// Encode
-// ------------------------------------------------------------------------------------------
-// Encode workspace: a 64-byte header, then two parities of per-tile look-back status words.
-// Zeroed once by sbe_encode_workspace_init; each call zeroes the parity the previous call used
-// and the last tile through the look-back flips `parity`, so calls need no reset in between.
-struct EncWorkspace {
-    uint32_t ticket;   // tile tickets drawn in the running call
-    uint32_t done;     // tiles past their look-back
-    uint32_t parity;   // status array used by the next call
-    uint32_t err;      // bit 0: a look-back spin gave up (never expected)
-    uint64_t used[2];  // tiles written in each status array by its last call
-    uint64_t pad[4];
-};
-static_assert(sizeof(EncWorkspace) == 64, "workspace header is 64 bytes");
-constexpr uint32_t kMaxSpins = 1u << 22;
+// Global-memory accesses through address_space(1) pointers: integer address arithmetic would
+// otherwise degrade them to flat_* instructions, which also count on lgkmcnt and make every LDS
+// read wait for outstanding memory loads.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+__device__ __forceinline__ uint32_t gload32(uintptr_t addr) { return *reinterpret_cast<g_u32*>(addr); }
+__device__ __forceinline__ uint4 gload128(uintptr_t addr) {
+    const u32x4 v = *reinterpret_cast<g_u32x4*>(addr);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
-template <typename T>
-__device__ __forceinline__ T atomic_read(T* p) {
-    return __hip_atomic_fetch_or(p, (T)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void publish(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// ------------------------------------------------------------------------------------------
+// Encode: three launches, no inter-workgroup hand-off inside any of them.
+//   K1 sbe_enc_sums   per 64-record tile and per 256-record block: output / packed-input bytes
+//   K2 sbe_enc_scan   one workgroup: exclusive scan of the block sums (in place)
+//   K3 sbe_enc_pack   one wave per tile: record offsets, LDS-staged input, per-lane record
+//                     composition into an LDS output window, coalesced 16-byte stores
+// ------------------------------------------------------------------------------------------
+#ifndef SBE_ENC_RPT
+#define SBE_ENC_RPT 32
+#endif
+constexpr int kBlk = 256;                             // records per K1/K2 block
+constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
+constexpr int kLpr = kWave / kRpt;                    // lanes per record in K3
+constexpr int kTilesPerBlk = kBlk / kRpt;
+static_assert(kWave % kRpt == 0 && kBlk % kRpt == 0, "tile shape");
 
 struct EncArgs {
     const uint8_t* arena;
@@ -133,268 +133,467 @@ struct EncArgs {
     uint64_t cap;
     uint64_t* out_off;
     uint8_t* status;
-    EncWorkspace* ws;
-    uint64_t* st;        // 2 parities x {out, in} x cap_tiles status words
-    uint64_t cap_tiles;
+    uint64_t* tsum;  // [tiles][2]   output / input bytes per tile
+    uint64_t* bsum;  // [blocks][2]  per block; K2 turns it into exclusive prefixes
 };
 
-// Per-lane dword composer.  Bytes are appended in stream order; whole dwords are flushed to the
-// LDS window when they fall inside [wb, we) and are masked to the record's own bytes [rs, re).
-struct Composer {
-    uint64_t q;     // absolute position of the first pending byte's dword (4-aligned)
-    uint64_t acc;   // pending bytes, little-endian
-    uint32_t nacc;  // pending byte count incl. (rs & 3) leading don't-care bytes for the 1st dword
-    uint64_t rs, re, wb, we;
-    uint32_t* win;
-
-    __device__ __forceinline__ void flush(uint32_t v) {
-        if (q >= wb && q < we) {
-            const uint32_t i = (uint32_t)((q - wb) >> 2);
-            if (q >= rs && q + 4 <= re) {
-                win[swz(i)] = v;
-            } else {
-                uint8_t* b = reinterpret_cast<uint8_t*>(win + swz(i));
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k)
-                    if (q + k >= rs && q + k < re) b[k] = (uint8_t)(v >> (8 * k));
-            }
-        }
-        q += 4;
-    }
-    // append nb (1..4) bytes held in the low bytes of v (bytes above nb must be zero)
-    __device__ __forceinline__ void append(uint32_t v, uint32_t nb) {
-        acc |= (uint64_t)v << (8u * nacc);
-        nacc += nb;
-        if (nacc >= 4) {
-            flush((uint32_t)acc);
-            acc >>= 32;
-            nacc -= 4;
-        }
-    }
-    __device__ __forceinline__ void finish() {
-        if (nacc) flush((uint32_t)acc);
-    }
-    // position of the next byte to be appended
-    __device__ __forceinline__ uint64_t pos() const { return q + nacc; }
-    // jump to absolute position p (> current), discarding pending bytes: valid only when every
-    // dword holding the skipped bytes lies before the window (p + 4 <= wb)
-    __device__ __forceinline__ void skip_to(uint64_t p) {
-        q = p & ~3ull;
-        nacc = (uint32_t)(p & 3u);
-        acc = 0;
-    }
-    // append L bytes of global memory starting at src
-    __device__ __forceinline__ void append_bytes(const uint8_t* src, uint32_t L) {
-        if (L == 0) return;
-        const uint64_t p0 = pos();
-        if (p0 + L + 4 <= wb) { skip_to(p0 + L); return; }
-        const uintptr_t a = reinterpret_cast<uintptr_t>(src);
-        const uint32_t sh = (uint32_t)(a & 3u);
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(a - sh);
-        uint32_t nb = 4u - sh;
-        if (nb > L) nb = L;
-        append((w[0] >> (8u * sh)) & byte_mask_bits(nb), nb);
-        uint32_t rem = L - nb;
-        ++w;
-        while (rem >= 4) {
-            if (q >= we) return;  // past the window: nothing more to write for this record
-            append(w[0], 4);
-            ++w;
-            rem -= 4;
-        }
-        if (rem) append(w[0] & byte_mask_bits(rem), rem);
-    }
-};
-
-template <bool kPacked, bool kTrunc>
-__global__ __launch_bounds__(kWave) void sbe_encode_kernel(EncArgs a) {
-    __shared__ uint32_t win[kWinDw];
-    const int lane = threadIdx.x;
-
-    // ---- tile ticket (dynamic tile order = start order: look-back never waits on an unstarted tile)
-    uint32_t tile = 0, par = 0;
-    uint64_t used_other = 0;
-    if (lane == 0) {
-        tile = atomicAdd(&a.ws->ticket, 1u);
-        par = atomic_read(&a.ws->parity) & 1u;
-        used_other = atomic_read(&a.ws->used[par ^ 1u]);
-    }
-    tile = __builtin_amdgcn_readfirstlane(__shfl(tile, 0, kWave));
-    par = __builtin_amdgcn_readfirstlane(__shfl(par, 0, kWave));
-    used_other = uniform64(__shfl(used_other, 0, kWave));
-    const uint64_t r = (uint64_t)tile * kTile + lane;
-    const bool valid = r < a.n;
-    const uint64_t ntiles = (a.n + kTile - 1) / kTile;
-    uint64_t* const st_out = a.st + (uint64_t)par * 2 * a.cap_tiles;
-    uint64_t* const st_in = st_out + a.cap_tiles;
-    uint64_t* const other_out = a.st + (uint64_t)(par ^ 1u) * 2 * a.cap_tiles;
-    uint64_t* const other_in = other_out + a.cap_tiles;
-    // zero the other parity's words used by the previous call (that call has completed)
-    for (uint64_t t = tile + (uint64_t)lane * ntiles; t < used_other; t += (uint64_t)kWave * ntiles) {
-        other_out[t] = 0;
-        other_in[t] = 0;
-    }
-
-    // ---- record sizes
-    uint32_t L[5] = {0, 0, 0, 0, 0};
+// Sizes of record r: output bytes (0 on E109) and packed-input bytes (its strings, always).
+template <bool kTrunc>
+__device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t (&L)[5], uint32_t& out_b,
+                                          uint32_t& in_b, uint8_t& st) {
     uint32_t sum = 0;
-    uint8_t st = SBE_ENC_OK;
-    uint64_t ts = 0;
-    if (valid) {
+    st = SBE_ENC_OK;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) L[f] = 0;
+    if (r < a.n) {
 #pragma unroll
         for (int f = 0; f < 5; ++f) {
             L[f] = a.str_len[5 * r + f];
             sum += L[f];
         }
 #pragma unroll
-        for (int f = 4; f >= 0; --f)
+        for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
             if (L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
-        ts = a.timestamp[r];
-        if (ts == 0) ts = a.ts_default;
     }
     const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
-    const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + sum : 0u;
-    const uint32_t rec_in = (kPacked && valid) ? sum : 0u;  // E109 records keep their arena bytes
-    const uint32_t inc_out = wave_incl_scan(rec_out, lane);
-    const uint32_t inc_in = kPacked ? wave_incl_scan(rec_in, lane) : 0u;
-    const uint64_t agg_out = __shfl(inc_out, kWave - 1, kWave);
-    const uint64_t agg_in = kPacked ? (uint64_t)__shfl(inc_in, kWave - 1, kWave) : 0ull;
+    out_b = (r < a.n && st == SBE_ENC_OK) ? ovh + sum : 0u;
+    in_b = r < a.n ? sum : 0u;
+}
 
-    // ---- decoupled look-back.  Each status word is a self-contained 8-B granule (flag | value),
-    // published with an agent-scope store and polled with agent-scope atomic RMW reads, which are
-    // performed at the device coherence point (per-XCD L2s are not coherent with each other).
-    // This call's words live in array `par`; the other array was zeroed above for the next call.
-    uint64_t base_out = 0, base_in = 0;
-    if (tile == 0) {
-        if (lane == 0) {
-            publish(st_out, kFlagInc | agg_out);
-            publish(st_in, kFlagInc | agg_in);
-        }
-    } else {
-        if (lane == 0) {
-            publish(st_out + tile, kFlagAgg | agg_out);
-            publish(st_in + tile, kFlagAgg | agg_in);
-        }
-        int64_t pred = (int64_t)tile - 1;
-        uint32_t spins = 0;
-        for (;;) {
-            const int64_t idx = pred - lane;
-            uint64_t so = kFlagInc, si = kFlagInc;  // before tile 0: inclusive zero
-            if (idx >= 0) {
-                so = atomic_read(st_out + idx);
-                si = atomic_read(st_in + idx);
-            }
-            const uint64_t fo = so >> 62, fi = si >> 62;
-            const bool ready = fo != 0 && fo == fi;
-            const uint64_t incm = __ballot(ready && fo == 2);
-            const uint64_t notready = __ballot(!ready);
-            const int k = incm ? __builtin_ctzll(incm) : 64;  // nearest inclusive predecessor
-            const uint64_t need = k >= 63 ? ~0ull : ((2ull << k) - 1ull);
-            if ((notready & need) && ++spins < kMaxSpins) {
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            if (notready & need) {  // bounded spin: record the failure instead of hanging
-                if (lane == 0) atomicOr(&a.ws->err, 1u);
-            }
-            const bool take = lane <= k;
-            base_out += wave_sum64(take ? (so & kValMask) : 0ull);
-            base_in += wave_sum64(take ? (si & kValMask) : 0ull);
-            if (k < 64 || (notready & need)) break;
-            pred -= kWave;
-        }
-        base_out = uniform64(base_out);
-        base_in = uniform64(base_in);
-        if (lane == 0) {
-            publish(st_out + tile, kFlagInc | (base_out + agg_out));
-            publish(st_in + tile, kFlagInc | (base_in + agg_in));
-        }
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint64_t t = __shfl_up(v, d, kWave);
+        if (lane >= d) v += t;
     }
-    // the last tile through the look-back hands the workspace to the next call
+    return v;
+}
+
+template <bool kPacked, bool kTrunc>
+__global__ __launch_bounds__(kBlk) void sbe_enc_sums(EncArgs a) {
+    __shared__ uint64_t red[2][kBlk / kWave];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const uint64_t r = (uint64_t)blockIdx.x * kBlk + threadIdx.x;
+    uint32_t L[5], ob, ib;
+    uint8_t st;
+    rec_sizes<kTrunc>(a, r, L, ob, ib, st);
+    if (!kPacked) ib = 0;
+    // per pack tile (kRpt records = kRpt consecutive lanes): segmented sums via shuffles
+    uint32_t to = ob, ti = ib;
+#pragma unroll
+    for (int d = 1; d < kRpt; d <<= 1) {
+        to += __shfl_xor(to, d, kWave);
+        ti += __shfl_xor(ti, d, kWave);
+    }
+    const uint64_t tile = r / kRpt;
+    if ((lane & (kRpt - 1)) == 0 && r < a.n) {
+        a.tsum[2 * tile] = to;
+        a.tsum[2 * tile + 1] = ti;
+    }
+    const uint64_t so = wave_sum64(ob), si = kPacked ? wave_sum64(ib) : 0ull;
     if (lane == 0) {
-        const uint32_t done = atomicAdd(&a.ws->done, 1u);
-        if (done == ntiles - 1) {
-            __hip_atomic_store(&a.ws->used[par], ntiles, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ws->used[par ^ 1u], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ws->parity, par ^ 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ws->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ws->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        red[0][w] = so;
+        red[1][w] = si;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t bo = 0, bi = 0;
+        for (int j = 0; j < kBlk / kWave; ++j) {
+            bo += red[0][j];
+            bi += red[1][j];
+        }
+        a.bsum[2 * blockIdx.x] = bo;
+        a.bsum[2 * blockIdx.x + 1] = bi;
+    }
+}
+
+// exclusive scan of nb (out, in) pairs in place; one workgroup of 1024 threads
+constexpr int kScanThreads = 1024, kScanPer = 4;
+__global__ __launch_bounds__(kScanThreads) void sbe_enc_scan(uint64_t* bsum, uint64_t nb) {
+    __shared__ uint64_t wt[2][kScanThreads / kWave];
+    __shared__ uint64_t carry[2];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    if (tid == 0) carry[0] = carry[1] = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < nb; base += (uint64_t)kScanThreads * kScanPer) {
+        uint64_t vo[kScanPer], vi[kScanPer], so = 0, si = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const uint64_t i = base + (uint64_t)tid * kScanPer + k;
+            vo[k] = i < nb ? bsum[2 * i] : 0;
+            vi[k] = i < nb ? bsum[2 * i + 1] : 0;
+            so += vo[k];
+            si += vi[k];
+        }
+        const uint64_t io = wave_incl_scan64(so, lane), ii = wave_incl_scan64(si, lane);
+        if (lane == kWave - 1) {
+            wt[0][w] = io;
+            wt[1][w] = ii;
+        }
+        __syncthreads();
+        uint64_t po = carry[0], pi = carry[1];
+        for (int j = 0; j < w; ++j) {
+            po += wt[0][j];
+            pi += wt[1][j];
+        }
+        po += io - so;
+        pi += ii - si;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const uint64_t i = base + (uint64_t)tid * kScanPer + k;
+            if (i < nb) {
+                bsum[2 * i] = po;
+                bsum[2 * i + 1] = pi;
+            }
+            po += vo[k];
+            pi += vi[k];
+        }
+        __syncthreads();
+        if (tid == kScanThreads - 1) {
+            carry[0] = po;
+            carry[1] = pi;
+        }
+        __syncthreads();
+    }
+}
+
+#ifndef SBE_ENC_WIN
+#define SBE_ENC_WIN 8192
+#endif
+constexpr int32_t kEW = SBE_ENC_WIN;            // output window bytes per pass
+constexpr int32_t kEWIn = SBE_ENC_WIN + 256;    // staged input bytes per pass
+
+__device__ __forceinline__ uint32_t swz_byte(int32_t pos) { return swz((uint32_t)pos >> 2) * 4u + ((uint32_t)pos & 3u); }
+
+// Byte-addressed stream of source dwords: the staged LDS input window or global memory.
+struct LdsSrc {
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t dw(int32_t i) const { return lds_dw(w, (uint32_t)i); }
+};
+struct GlbSrc {
+    uintptr_t base;  // 4-aligned absolute address of dword 0
+    __device__ __forceinline__ uint32_t dw(int32_t i) const { return gload32(base + 4 * (int64_t)i); }
+};
+
+// Write string bytes [o, o+L) of the output window (window-relative; clipped to [lo, hi)) from a
+// source whose byte 0 is stream byte `sb` of S.  Interior dwords: one source read, one
+// v_alignbyte, one ds_write_b32; the (<= 3 + 3) edge bytes are written one by one.
+template <typename Src>
+__device__ __forceinline__ void put_string(uint32_t* wout, int32_t o, int32_t L, int32_t lo, int32_t hi,
+                                           const Src& S, int32_t sb) {
+    int32_t a = o > lo ? o : lo;
+    const int32_t e = (o + L) < hi ? (o + L) : hi;
+    if (a >= e) return;
+    uint8_t* wb8 = reinterpret_cast<uint8_t*>(wout);
+    // head bytes up to the next aligned dword
+    const int32_t ah = (a + 3) & ~3;
+    for (; a < e && a < ah; ++a) {
+        const int32_t b = sb + (a - o);
+        wb8[swz_byte(a)] = (uint8_t)(S.dw(b >> 2) >> (8 * (b & 3)));
+    }
+    const int32_t ee = e & ~3;
+    if (a < ee) {
+        const int32_t b = sb + (a - o);
+        const uint32_t sh = (uint32_t)(b & 3);
+        int32_t i = b >> 2;
+        uint32_t prev = S.dw(i);
+        for (; a < ee; a += 4) {
+            const uint32_t next = sh ? S.dw(i + 1) : 0u;
+            wout[swz((uint32_t)a >> 2)] = __builtin_amdgcn_alignbyte(next, prev, sh);
+            prev = next;
+            ++i;
+            if (!sh) prev = S.dw(i);
         }
     }
+    for (; a < e; ++a) {
+        const int32_t b = sb + (a - o);
+        wb8[swz_byte(a)] = (uint8_t)(S.dw(b >> 2) >> (8 * (b & 3)));
+    }
+}
 
-    // ---- per-record offsets / status
-    const uint64_t rs = base_out + inc_out - rec_out;
-    const uint64_t re = rs + rec_out;
-    if (valid) {
-        if (st == SBE_ENC_OK && re > a.cap) st = SBE_ENC_OVERFLOW;
-        a.out_off[r] = rs;
-        if (r == a.n - 1) a.out_off[a.n] = re;
+__device__ __noinline__ void put_string_global(uint32_t* wout, int32_t o, int32_t L, int32_t lo, int32_t hi,
+                                              uintptr_t sa) {
+    const uintptr_t b4 = sa & ~(uintptr_t)3;
+    put_string(wout, o, L, lo, hi, GlbSrc{b4}, (int32_t)(sa - b4));
+}
+
+// literal bytes [o, o+n) (n <= 8) held little-endian in v, clipped to [lo, hi)
+__device__ __forceinline__ void put_lit(uint32_t* wout, int32_t o, int32_t n, uint64_t v, int32_t lo, int32_t hi) {
+    uint8_t* wb8 = reinterpret_cast<uint8_t*>(wout);
+    if ((o & 3) == 0 && n == 8 && o >= lo && o + 8 <= hi) {
+        wout[swz((uint32_t)o >> 2)] = (uint32_t)v;
+        wout[swz((uint32_t)(o + 4) >> 2)] = (uint32_t)(v >> 32);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (k < n && o + k >= lo && o + k < hi) wb8[swz_byte(o + k)] = (uint8_t)(v >> (8 * k));
+}
+
+// ---- K3: persistent, software-pipelined pack kernel ---------------------------------------
+// One wave per workgroup loops over tiles t = blockIdx.x, += gridDim.x.  While it composes tile
+// t it already holds tile t+G's staged-input loads in flight (registers) and tile t+2G's lengths,
+// so the two dependent HBM round trips of a tile hide behind the previous tile's work.  Each
+// record is composed by kLpr lanes (one contiguous part each) into an XOR-swizzled LDS output
+// window, which the wave then stores with global_store_dwordx4 (1 KiB per instruction).
+constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging registers per lane
+
+struct TileIn {  // raw per-lane loads of one tile
+    uint32_t L[5];
+    uint64_t ts;
+    uint64_t po, pi;  // one preceding tile sum of the block (lane-indexed)
+    uint64_t bo, bi;  // block prefix
+};
+
+struct TileSt {  // prepared per-lane state of one tile
+    uint64_t rs, re, ps, pe;  // record range, this lane's part of it
+    uint64_t ts;
+    uint32_t L[5], rec_out;
+    uint64_t in0;             // packed: record's first string byte, relative to in_tile
+    uint64_t T0, T1;          // tile output range (clipped to capacity)
+    uintptr_t in_tile;        // packed: absolute address of the tile's first input byte
+    uint32_t agg_in;
+    uintptr_t gsrc[5];        // gather mode: absolute string addresses
+};
+
+template <bool kPacked>
+__device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane) {
+    TileIn x;
+    const uint64_t r = tile * kRpt + lane / kLpr;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) x.L[f] = r < a.n ? a.str_len[5 * r + f] : 0u;
+    x.ts = r < a.n ? a.timestamp[r] : 0ull;
+    const uint64_t blk = tile / kTilesPerBlk, tib = tile - blk * kTilesPerBlk;
+    x.po = x.pi = 0;
+    if ((uint64_t)lane < tib) {
+        x.po = a.tsum[2 * (blk * kTilesPerBlk + lane)];
+        if (kPacked) x.pi = a.tsum[2 * (blk * kTilesPerBlk + lane) + 1];
+    }
+    x.bo = a.bsum[2 * blk];
+    x.bi = kPacked ? a.bsum[2 * blk + 1] : 0ull;
+    return x;
+}
+
+template <bool kPacked, bool kTrunc>
+__device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane) {
+    TileSt S;
+    const int q = lane % kLpr, lead = lane - q;
+    const uint64_t r = tile * kRpt + lane / kLpr;
+    const bool valid = r < a.n;
+    uint32_t sum = 0;
+    uint8_t st = SBE_ENC_OK;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+        S.L[f] = x.L[f];
+        sum += x.L[f];
+    }
+#pragma unroll
+    for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
+        if (x.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
+    const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+    const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + sum : 0u;
+    const uint32_t rec_in = (kPacked && valid) ? sum : 0u;
+    const uint64_t base_out = uniform64(x.bo + wave_sum64(x.po));
+    const uint64_t base_in = kPacked ? uniform64(x.bi + wave_sum64(x.pi)) : 0ull;
+    const uint32_t lo_out = q == 0 ? rec_out : 0u, lo_in = q == 0 ? rec_in : 0u;
+    const uint32_t inc_out = wave_incl_scan(lo_out, lane);
+    const uint32_t inc_in = kPacked ? wave_incl_scan(lo_in, lane) : 0u;
+    const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
+    S.agg_in = kPacked ? __builtin_amdgcn_readfirstlane(__shfl(inc_in, kWave - 1, kWave)) : 0u;
+    const uint32_t ex_out = __shfl(inc_out - lo_out, lead, kWave);
+    S.in0 = kPacked ? (uint64_t)__shfl(inc_in - lo_in, lead, kWave) : 0ull;
+    S.rec_out = rec_out;
+    S.rs = base_out + ex_out;
+    S.re = S.rs + rec_out;
+    S.ts = x.ts ? x.ts : a.ts_default;
+    if (valid && q == 0) {
+        if (st == SBE_ENC_OK && S.re > a.cap) st = SBE_ENC_OVERFLOW;
+        a.out_off[r] = S.rs;
+        if (r == a.n - 1) a.out_off[a.n] = S.re;
         if (a.status) a.status[r] = st;
     }
-
-    // ---- source addresses of the five strings
-    const uint8_t* src[5];
-    if (kPacked) {
-        uint64_t o = base_in + inc_in - rec_in;
+    const uint64_t ps = q == 0 ? S.rs : ((S.rs + (uint64_t)q * rec_out / kLpr + 3) & ~3ull);
+    const uint64_t pe = q == kLpr - 1 ? S.re : ((S.rs + (uint64_t)(q + 1) * rec_out / kLpr + 3) & ~3ull);
+    const uint64_t hi_rec = S.re < a.cap ? S.re : a.cap;
+    S.ps = ps < S.re ? ps : S.re;
+    S.pe = pe < hi_rec ? pe : hi_rec;
+    S.T0 = base_out;
+    S.T1 = (base_out + agg_out) < a.cap ? (base_out + agg_out) : a.cap;
+    S.in_tile = reinterpret_cast<uintptr_t>(a.arena) + base_in;
+    if (!kPacked) {
 #pragma unroll
-        for (int f = 0; f < 5; ++f) {
-            src[f] = a.arena + o;
-            o += L[f];
-        }
-    } else {
-#pragma unroll
-        for (int f = 0; f < 5; ++f) src[f] = valid ? a.arena + a.str_off[5 * r + f] : a.arena;
+        for (int f = 0; f < 5; ++f)
+            S.gsrc[f] = reinterpret_cast<uintptr_t>(a.arena) + (valid ? a.str_off[5 * r + f] : 0u);
     }
+    return S;
+}
 
-    // ---- compose windows and store them
-    const uint64_t T0 = base_out;
-    const uint64_t T1 = (base_out + agg_out) < a.cap ? (base_out + agg_out) : a.cap;
-    const uint64_t hi_rec = re < a.cap ? re : a.cap;
-    for (uint64_t wb = T0 & ~15ull; wb < T1; wb += kWin) {
-        const uint64_t we = wb + kWin;
-        if (rec_out && rs < we && hi_rec > wb && rs < hi_rec) {
-            Composer c;
-            c.q = rs & ~3ull;
-            c.acc = 0;
-            c.nacc = (uint32_t)(rs & 3u);
-            c.rs = rs;
-            c.re = hi_rec;
-            c.wb = wb;
-            c.we = we;
-            c.win = win;
-            // header {blockLength 16, templateId 1, schemaId 1, version 1}, ts, sequenceNumber 0
-            c.append(SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16), 4);
-            c.append(SBE_TOPIC_SCHEMA_ID | (1u << 16), 4);
-            c.append((uint32_t)ts, 4);
-            c.append((uint32_t)(ts >> 32), 4);
-            c.append(0u, 4);
-            c.append(0u, 4);
+// one output window covers the tile: the pipelined path
+__device__ __forceinline__ bool single_window(const TileSt& S) { return S.T1 - (S.T0 & ~15ull) <= (uint64_t)kEW; }
+
+// Staged input range for output window [wb, ...): from the first string byte at/after max(wb,T0)
+// (input offset >= p - 34 within the record holding it) for kEWIn bytes, clipped to the tile.
+__device__ __forceinline__ void stage_range(const TileSt& S, uint64_t wb, int lane, uintptr_t& swb,
+                                            int32_t& nbytes) {
+    const uint64_t g = wb > S.T0 ? wb : S.T0;
+    const int q = lane % kLpr;
+    const uint64_t mine = __ballot(q == 0 && S.rec_out && S.rs <= g && g < S.re);
+    const int ra = mine ? __builtin_ctzll(mine) : 0;
+    const uint64_t ra_rs = uniform64(__shfl(S.rs, ra, kWave));
+    const uint64_t ra_in = uniform64(__shfl(S.in0, ra, kWave));
+    const uint64_t p = g - ra_rs;
+    const uintptr_t first = S.in_tile + ra_in + (p > 34 ? p - 34 : 0);
+    swb = first & ~(uintptr_t)15;
+    const uintptr_t lim = (S.in_tile + S.agg_in + 15) & ~(uintptr_t)15;
+    const uintptr_t swe = swb + kEWIn < lim ? swb + kEWIn : (lim > swb ? lim : swb);
+    nbytes = (int32_t)(swe - swb);
+}
+
+__device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int lane, uint4 (&I)[kStageRegs]) {
 #pragma unroll
-            for (int f = 0; f < 5; ++f) {
-                if (c.q >= we) break;
-                c.append(L[f] & 0xffffu, 2);
-                c.append_bytes(src[f], L[f]);
-            }
-            if (c.q < we) c.finish();
-        }
-        __syncthreads();
-        // store [max(wb,T0), min(we,T1)) : 16-B chunks, partial edge chunks byte-wise
-        const uint64_t lo = wb > T0 ? wb : T0;
-        const uint64_t hi = we < T1 ? we : T1;
-        const uint32_t nch = (uint32_t)((hi - wb + 15) >> 4);
-        for (uint32_t ch = lane; ch < nch; ch += kWave) {
-            const uint64_t g = wb + 16ull * ch;
-            const uint4 v = lds_read_chunk(win, ch);
-            if (g >= lo && g + 16 <= hi) {
-                *reinterpret_cast<uint4*>(a.out + g) = v;
+    for (int k = 0; k < kStageRegs; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        I[k] = (int32_t)(16 * ch) < nbytes ? gload128(swb + 16u * ch) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void stage_write(uint32_t* win_in, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
+#pragma unroll
+    for (int k = 0; k < kStageRegs; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        if ((int32_t)(16 * ch) < nbytes) lds_write_chunk(win_in, ch, I[k]);
+    }
+}
+
+// compose this lane's part of its record for output window [wb, we)
+template <bool kPacked>
+__device__ __forceinline__ void compose(uint32_t* wout, const uint32_t* win_in, const TileSt& S, uint64_t wb,
+                                        uint64_t we, uintptr_t swb, int32_t win_bytes) {
+    if (!(S.rec_out && S.ps < S.pe && S.ps < we && S.pe > wb)) return;
+    const int32_t R0 = (int32_t)((int64_t)S.rs - (int64_t)wb);
+    const int32_t pl = (int32_t)((int64_t)S.ps - (int64_t)wb);
+    const int32_t lo = pl > 0 ? pl : 0;
+    const int32_t hr = (int32_t)((int64_t)S.pe - (int64_t)wb);
+    const int32_t hi = hr < (int32_t)(we - wb) ? hr : (int32_t)(we - wb);
+    // header {16,1,1,1}, timestamp, sequenceNumber 0 (TopicMessage.h:221-238, :362-437)
+    put_lit(wout, R0, 8, (uint64_t)(SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16)) |
+                             ((uint64_t)(SBE_TOPIC_SCHEMA_ID | (1u << 16)) << 32), lo, hi);
+    put_lit(wout, R0 + 8, 8, S.ts, lo, hi);
+    put_lit(wout, R0 + 16, 8, 0ull, lo, hi);
+    int32_t o = R0 + 24;
+    uint64_t sin = S.in0;
+#pragma nounroll
+    for (int f = 0; f < 5; ++f) {
+        const uint32_t Lu = f == 0 ? S.L[0] : f == 1 ? S.L[1] : f == 2 ? S.L[2] : f == 3 ? S.L[3] : S.L[4];
+        put_lit(wout, o, 2, Lu & 0xffffu, lo, hi);  // u16 length, then the bytes (:515-529)
+        o += 2;
+        const int32_t Lf = (int32_t)Lu;
+        if (Lf && o < hi && o + Lf > lo) {
+            uintptr_t sa;
+            if (kPacked) {
+                sa = S.in_tile + sin;
             } else {
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (uint32_t k = 0; k < 16; ++k)
-                    if (g + k >= lo && g + k < hi) a.out[g + k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+                sa = f == 0 ? S.gsrc[0] : f == 1 ? S.gsrc[1] : f == 2 ? S.gsrc[2] : f == 3 ? S.gsrc[3] : S.gsrc[4];
+            }
+            if (kPacked && sa >= swb && sa + Lf <= swb + (uint32_t)win_bytes) {
+                put_string(wout, o, Lf, lo, hi, LdsSrc{win_in}, (int32_t)(sa - swb));
+            } else {
+                put_string_global(wout, o, Lf, lo, hi, sa);
             }
         }
+        o += Lf;
+        sin += (uint32_t)Lf;
+    }
+}
+
+__device__ __forceinline__ void store_window(uint8_t* out, const uint32_t* wout, uint64_t T0, uint64_t wb, uint64_t we,
+                                             int lane) {
+    const uint64_t lo = wb > T0 ? wb : T0;
+    const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
+    for (uint32_t ch = lane; ch < nch; ch += kWave) {
+        const uint64_t g = wb + 16ull * ch;
+        const uint4 v = lds_read_chunk(wout, ch);
+        if (g >= lo && g + 16 <= we) {
+            *reinterpret_cast<uint4*>(out + g) = v;
+        } else {
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k)
+                if (g + k >= lo && g + k < we) out[g + k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
+template <bool kPacked, bool kTrunc>
+__global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
+    __shared__ uint32_t wout[kEW / 4];
+    __shared__ uint32_t win_in[kPacked ? kEWIn / 4 : 4];
+    const int lane = threadIdx.x;
+    const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
+    const uint64_t G = gridDim.x;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+
+    TileIn x = tile_load<kPacked>(a, t, lane);
+    TileSt S = tile_prepare<kPacked, kTrunc>(a, x, t, lane);
+    uint4 I[kStageRegs];
+    uintptr_t swb = 0;
+    int32_t nb = 0;
+    bool fast = kPacked && single_window(S);
+    if (fast) {
+        stage_range(S, S.T0 & ~15ull, lane, swb, nb);
+        stage_issue(swb, nb, lane, I);
+    }
+    uint64_t tn = t + G;
+    if (tn < ntiles) x = tile_load<kPacked>(a, tn, lane);
+
+    for (;;) {
+        // current tile's staged input: registers → LDS
+        const uintptr_t cur_swb = swb;
+        const int32_t cur_nb = nb;
+        const bool cur_fast = fast;
+        if (cur_fast) stage_write(win_in, cur_nb, lane, I);
         __syncthreads();
+        // next tile: prepare it and put its input loads in flight; prefetch the one after
+        const bool have_next = tn < ntiles;
+        TileSt Sn;
+        if (have_next) {
+            Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane);
+            fast = kPacked && single_window(Sn);
+            if (fast) {
+                stage_range(Sn, Sn.T0 & ~15ull, lane, swb, nb);
+                stage_issue(swb, nb, lane, I);
+            }
+            const uint64_t t2 = tn + G;
+            if (t2 < ntiles) x = tile_load<kPacked>(a, t2, lane);
+        }
+        // current tile: compose + store, one window (fast) or window by window
+        if (cur_fast) {
+            const uint64_t wb = S.T0 & ~15ull;
+            compose<kPacked>(wout, win_in, S, wb, S.T1, cur_swb, cur_nb);
+            __syncthreads();
+            store_window(a.out, wout, S.T0, wb, S.T1, lane);
+            __syncthreads();
+        } else {
+            for (uint64_t wb = S.T0 & ~15ull; wb < S.T1; wb += kEW) {
+                const uint64_t we = wb + kEW < S.T1 ? wb + kEW : S.T1;
+                uintptr_t sw = 0;
+                int32_t nbw = 0;
+                if (kPacked) {
+                    stage_range(S, wb, lane, sw, nbw);
+                    const uint32_t nch = (uint32_t)(nbw >> 4);
+                    for (uint32_t ch = lane; ch < nch; ch += kWave) lds_write_chunk(win_in, ch, gload128(sw + 16u * ch));
+                    __syncthreads();
+                }
+                compose<kPacked>(wout, win_in, S, wb, we, sw, nbw);
+                __syncthreads();
+                store_window(a.out, wout, S.T0, wb, we, lane);
+                __syncthreads();
+            }
+        }
+        if (!have_next) break;
+        S = Sn;
+        tn += G;
     }
 }
 
@@ -423,7 +622,7 @@ struct RecReader {
     // dword of the stream at aligned absolute position qa
     __device__ __forceinline__ uint32_t dw(uint64_t qa) const {
         if (qa >= wb && qa < we) return lds_dw(win, (uint32_t)((qa - wb) >> 2));
-        return *reinterpret_cast<const uint32_t*>(in + qa);
+        return gload32(reinterpret_cast<uintptr_t>(in) + qa);
     }
     // up to 4 bytes at record offset p (the caller guarantees p+nb <= record length)
     __device__ __forceinline__ uint32_t bytes(uint64_t p, uint32_t nb) const {
@@ -698,7 +897,7 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
     const uint64_t we = (wb + kWin) < end ? wb + kWin : end;
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
     for (uint32_t ch = lane; ch < nch; ch += kWave)
-        lds_write_chunk(win, ch, *reinterpret_cast<const uint4*>(a.in + wb + 16ull * ch));
+        lds_write_chunk(win, ch, gload128(reinterpret_cast<uintptr_t>(a.in) + wb + 16ull * ch));
     __syncthreads();
 
     if (!valid) return;
@@ -731,6 +930,26 @@ int record_hip(hipError_t e) {
 
 constexpr uint64_t kMaxTiles = 0xffffffffull;
 
+// Persistent grid of the pack kernel: every workgroup resident at once (occupancy x CUs).
+uint64_t pack_grid(const void* kernel, uint64_t tiles) {
+    static thread_local const void* cached_k = nullptr;
+    static thread_local int cached_dev = -1;
+    static thread_local uint64_t cached = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (kernel != cached_k || dev != cached_dev) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWave, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        cached = (uint64_t)per_cu * (uint64_t)cus;
+        cached_k = kernel;
+        cached_dev = dev;
+    }
+    return tiles < cached ? tiles : cached;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -755,8 +974,9 @@ int sbe_device_ready(void) {
 }
 
 size_t sbe_encode_workspace_size(uint64_t n) {
-    const uint64_t tiles = (n + kTile - 1) / kTile;
-    return (size_t)(sizeof(EncWorkspace) + 32 * (tiles ? tiles : 1));
+    const uint64_t blocks = (n + kBlk - 1) / kBlk;
+    const uint64_t tiles = blocks * kTilesPerBlk;
+    return (size_t)(16 * (tiles + blocks) + 16);
 }
 
 uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t flags) {
@@ -778,22 +998,28 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
     if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
     if (!in->str_len || !in->timestamp || !in->arena || !out) return SBE_EINVAL;
     if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
-    const uint64_t tiles = (n + kTile - 1) / kTile;
+    const uint64_t blocks = (n + kBlk - 1) / kBlk;
+    const uint64_t tiles = (n + kRpt - 1) / kRpt;
     if (tiles > kMaxTiles) return SBE_EINVAL;
     if (!workspace || workspace_bytes < sbe_encode_workspace_size(n)) return SBE_ENOSPC;
-    if (reinterpret_cast<uintptr_t>(workspace) & 63u) return SBE_EINVAL;
-    uint8_t* ws = static_cast<uint8_t*>(workspace);
-    const uint64_t cap_tiles = (workspace_bytes - sizeof(EncWorkspace)) / 32;
-    EncArgs a{in->arena, in->str_off, in->str_len, in->timestamp, n, ts_default, out, out_capacity, out_off,
-              status, reinterpret_cast<EncWorkspace*>(ws), reinterpret_cast<uint64_t*>(ws + sizeof(EncWorkspace)),
-              cap_tiles};
-    const dim3 grid((uint32_t)tiles), block(kWave);
+    if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
+    uint64_t* ws = static_cast<uint64_t*>(workspace);
+    EncArgs a{in->arena, in->str_off, in->str_len, in->timestamp, n,  ts_default,
+              out,       out_capacity, out_off,   status,        ws, ws + 2 * blocks * kTilesPerBlk};
     const bool packed = in->str_off == nullptr;
     const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
-    if (packed && !trunc) hipLaunchKernelGGL((sbe_encode_kernel<true, false>), grid, block, 0, s, a);
-    else if (packed && trunc) hipLaunchKernelGGL((sbe_encode_kernel<true, true>), grid, block, 0, s, a);
-    else if (!packed && !trunc) hipLaunchKernelGGL((sbe_encode_kernel<false, false>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((sbe_encode_kernel<false, true>), grid, block, 0, s, a);
+#define SBE_ENC_LAUNCH(P, T)                                                                          \
+    do {                                                                                              \
+        const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<P, T>), tiles);   \
+        hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)blocks), dim3(kBlk), 0, s, a);        \
+        hipLaunchKernelGGL(sbe_enc_scan, dim3(1), dim3(kScanThreads), 0, s, a.bsum, blocks);          \
+        hipLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, a);        \
+    } while (0)
+    if (packed && !trunc) SBE_ENC_LAUNCH(true, false);
+    else if (packed && trunc) SBE_ENC_LAUNCH(true, true);
+    else if (!packed && !trunc) SBE_ENC_LAUNCH(false, false);
+    else SBE_ENC_LAUNCH(false, true);
+#undef SBE_ENC_LAUNCH
     return record_hip(hipGetLastError());
 }
 

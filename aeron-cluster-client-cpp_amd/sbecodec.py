@@ -19,7 +19,7 @@ from dataclasses import dataclass
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsbecodec.so")
+LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
 ABI_VERSION = 1
@@ -126,15 +126,10 @@ def workspace_size(n: int) -> int:
 
 
 def alloc_workspace(n: int, device, stream=None) -> torch.Tensor:
-    """Workspace for encoding up to n records, zeroed once (the kernel keeps it zeroed)."""
+    """Workspace for encoding up to n records, zeroed and registered once."""
     ws = torch.empty(max(workspace_size(n), 16), dtype=torch.uint8, device=device)
     _check(lib().sbe_encode_workspace_init(_ptr(ws), ws.numel(), _stream(stream)), "sbe_encode_workspace_init")
     return ws
-
-
-def workspace_error(ws: torch.Tensor) -> int:
-    """Error bits the encode kernel left in its workspace header (0 = none); synchronises."""
-    return int(ws[12:16].cpu().numpy().view("<u4")[0])
 
 
 @dataclass

@@ -173,7 +173,7 @@ def main():
         enc_gbs = n * ENC_BYTES / (enc_ms * 1e-3) / 1e9
         dec_gbs = n * DEC_BYTES / (dec_ms * 1e-3) / 1e9
         if enc_ms >= dec_ms:
-            dom = dict(kernel="sbe_encode_kernel<packed,wire>", bytes_per_record=ENC_BYTES, ms=enc_ms, gbs=enc_gbs)
+            dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, ms=enc_ms, gbs=enc_gbs)
         else:
             dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES, ms=dec_ms, gbs=dec_gbs)
         cpu = None

@@ -94,9 +94,8 @@ typedef struct sbe_tm_batch {
 /* Bytes of device workspace sbe_encode_topic_batch needs for n records (look-back tile state). */
 size_t sbe_encode_workspace_size(uint64_t n);
 
-/* Zero a workspace once after allocating it (hipMemsetAsync on `stream`).  Every completed
- * sbe_encode_topic_batch leaves its workspace zeroed again, so calls need no per-call reset.
- * A workspace serves one stream at a time; re-initialise it after a failed launch. */
+/* Optional: zero a workspace (hipMemsetAsync on `stream`).  The encoder needs no particular
+ * workspace contents; a workspace serves one stream at a time. */
 int sbe_encode_workspace_init(void* workspace, size_t workspace_bytes, void* stream);
 
 /* Upper bound of the encoded stream for a batch whose strings total `string_bytes`. */
@@ -106,8 +105,7 @@ uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t fla
  *   out        device buffer of out_capacity bytes; record i is out[out_off[i] .. out_off[i+1]).
  *   out_off    [n+1] u64 device array (written).
  *   status     [n] u8 device array (written) or NULL.
- *   workspace  device memory of >= sbe_encode_workspace_size(n) bytes, zeroed by
- *              sbe_encode_workspace_init before its first use.
+ *   workspace  device memory of >= sbe_encode_workspace_size(n) bytes, 16-B aligned.
  *   alignment  out 16 B, out_off 8 B (arena, str_off, str_len, timestamp: natural alignment).
  * Records are independent; a failing record (E109, overflow) emits 0 bytes and the batch goes on. */
 int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,

@@ -25,7 +25,6 @@ def gpu_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
     o = None if str_off is None else to_dev(np.asarray(str_off, np.uint32).reshape(-1, 5), torch.int32)
     enc = codec.encode_topic_batch(a, L, t, str_off=o, flags=flags, ts_default=ts_default)
     torch.cuda.synchronize()
-    assert codec.workspace_error(enc.workspace) == 0
     off = enc.out_off.cpu().numpy().view(np.uint64)
     n = ts.size
     out = enc.out[: int(off[n])].cpu().numpy()
