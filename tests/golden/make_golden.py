@@ -1,0 +1,116 @@
+"""Generate the golden fixtures under tests/golden/ (run in the container where /root/reference
+is present and oracle/_ref/libsbe_ref_fw.so has been built by `make -C oracle`).
+
+Every expected value in encode_ref.json / decode_tm_ref.json / ack_ref.json / egress_tm_ref.json
+is produced by the reference's own SBE-generated flyweights (include/model/*.h compiled unmodified,
+driven in the reference's call order by oracle/ref_flyweights.cpp).  survey_probes.json holds the
+outputs of the reference functions themselves as recorded in SURVEY.md Appendix B (probe runs of
+the compiled reference in the survey container); those expectations are transcribed, not computed.
+
+Inputs only are derived from tests/sbe_testlib.py generators and tests/sbe_testlib.edge_records().
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import sbe_testlib as T  # noqa: E402
+
+
+def hx(b):
+    return bytes(b).hex()
+
+
+def blob(b):
+    """Bytes up to 1 KiB inline as hex; larger ones as length + sha256 + head/tail (the test
+    regenerates the input from the committed generators and compares digests)."""
+    import hashlib
+    b = bytes(b)
+    if len(b) <= 1024:
+        return hx(b)
+    return {"len": len(b), "sha256": hashlib.sha256(b).hexdigest(), "head": hx(b[:64]), "tail": hx(b[-64:])}
+
+
+def field_spec(f):
+    """Large uniform fields are stored as {fill, len}; others as hex."""
+    b = bytes(f)
+    if len(b) > 512 and len(set(b)) == 1:
+        return {"fill": b[0], "len": len(b)}
+    return hx(b)
+
+
+def encode_cases():
+    cases = []
+    # SURVEY Appendix B probe input
+    cases.append(([b"orders", b"CREATE_ORDER", b"msg_1", b'{"a":1}', b'{"h":2}'], 0x1122334455667788))
+    arena, L, ts = T.fixed256_orders(3)
+    at = 0
+    for i in range(3):
+        f = []
+        for k in range(5):
+            f.append(bytes(arena[at: at + L[i, k]]))
+            at += int(L[i, k])
+        cases.append((f, int(ts[i])))
+    arena, L, ts = T.var_orders(8, seed=77)
+    at = 0
+    for i in range(8):
+        f = []
+        for k in range(5):
+            f.append(bytes(arena[at: at + L[i, k]]))
+            at += int(L[i, k])
+        cases.append((f, int(ts[i])))
+    cases.append(([b""] * 5, 1))
+    cases.append(([b"t", b"", b"", b"", b""], 2**64 - 1))
+    cases.append(([b"orders", b"CREATE_ORDER", b"id", b"{}", b""], 5))
+    cases.append(([b"\x00\xff", b"\n\r", b"\x80", b"", b"\x7f" * 5], 12345))
+    big = b"\x41" * 65534
+    cases.append(([big, b"x", b"", b"", b""], 7))
+    for k in range(5):
+        f = [b"a", b"b", b"c", b"d", b"e"]
+        f[k] = b"\x5a" * 65535
+        cases.append((f, 9))
+    return cases
+
+
+def main():
+    if not T.ref_available():
+        sys.exit("oracle/_ref/libsbe_ref_fw.so is missing: run `make -C oracle` with /root/reference present")
+    out = []
+    for fields, ts in encode_cases():
+        rc_t, ref_t = T.ref_encode(fields, ts, wire=False)
+        rc_w, ref_w = T.ref_encode(fields, ts, wire=True)
+        assert rc_t == rc_w
+        out.append({"fields": [field_spec(f) for f in fields], "ts": str(ts), "status": rc_t,
+                    "ref_truncated": blob(ref_t), "wire": blob(ref_w)})
+    json.dump({"source": "reference flyweights via oracle/_ref (SBEEncoder::encode_topic_message call order, "
+                         "src/sbe_encoder.cpp:141-164; wire length per src/cluster_client.cpp:1857)",
+               "cases": out}, open(os.path.join(HERE, "encode_ref.json"), "w"), indent=1)
+
+    recs = T.edge_records()
+    tm, ack, eg = [], [], []
+    for name, r in recs:
+        if len(r) >= 8 and r[2:6] == b"\x01\x00\x01\x00":  # template 1, schema 1
+            rc, ts, f, hok = T.ref_tm_decode(r)
+            tm.append({"name": name, "rec": blob(r), "e100": rc, "ts": str(ts) if rc == 0 else None,
+                       "fields": [blob(x) for x in f] if rc == 0 else None, "headers_ok": hok if rc == 0 else None})
+            rc, f = T.ref_egress_tm(r)
+            eg.append({"name": name, "rec": blob(r), "throws": rc, "fields": [blob(x) for x in f] if rc == 0 else None})
+        if len(r) >= 16 and r[2:6] == b"\x02\x00\x01\x00":  # template 2, schema 1, full-ack branch
+            if len(r) == 16 and r[0:2] == b"\x08\x00":
+                continue  # simple control ack branch never reaches the flyweights
+            rc, ts, f = T.ref_ack_decode(r)
+            ack.append({"name": name, "rec": blob(r), "fails": rc, "ts": str(ts) if rc == 0 else None,
+                        "fields": [blob(x) for x in f] if rc == 0 else None})
+    src = "reference flyweights via oracle/_ref"
+    json.dump({"source": src + " (decode_topic_message_with_sbe flyweight sequence, src/sbe_encoder.cpp:966-1135)",
+               "cases": tm}, open(os.path.join(HERE, "decode_tm_ref.json"), "w"), indent=1)
+    json.dump({"source": src + " (decode_ack full-ack flyweight sequence, src/ack_decoder.cpp:55-101)",
+               "cases": ack}, open(os.path.join(HERE, "ack_ref.json"), "w"), indent=1)
+    json.dump({"source": src + " (MessageHandler::on_egress TopicMessage sequence, message_handler.hpp:47-60)",
+               "cases": eg}, open(os.path.join(HERE, "egress_tm_ref.json"), "w"), indent=1)
+    print(f"encode {len(out)}, tm {len(tm)}, ack {len(ack)}, egress {len(eg)}")
+
+
+if __name__ == "__main__":
+    main()
