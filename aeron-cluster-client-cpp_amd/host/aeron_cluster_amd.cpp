@@ -1,0 +1,391 @@
+// aeron_cluster_amd.cpp — host side of the reference codec surface over the C ABI.
+// Host memory in, host memory out (the reference's API contract): each call stages its batch in
+// pinned buffers, copies it to HBM on a private stream, launches the HIP kernels through
+// include/sbecodec.h and copies the results back.  Results are materialised on the host from the
+// device descriptors (views into the caller's own bytes), never recomputed here.
+#include "aeron_cluster_amd.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+
+#include "sbecodec.h"
+
+namespace aeron_cluster {
+namespace {
+
+[[noreturn]] void fail(const char* what) {
+    throw std::runtime_error(std::string("sbecodec: ") + what + " (" + sbe_last_error() + ")");
+}
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("sbecodec: ") + what + ": " + hipGetErrorString(e));
+}
+
+// Growable device / pinned host buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void need(size_t n) {
+        if (n <= cap) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t c = n < 4096 ? 4096 : n + n / 4;
+        hip_check(hipMalloc(&p, c), "hipMalloc");
+        cap = c;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void need(size_t n) {
+        if (n <= cap) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t c = n < 4096 ? 4096 : n + n / 4;
+        hip_check(hipHostMalloc(&p, c, hipHostMallocDefault), "hipHostMalloc");
+        cap = c;
+    }
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// Per-thread device context (the reference's codec functions are reentrant statics).
+struct Ctx {
+    hipStream_t stream = nullptr;
+    DevBuf d_arena, d_len, d_ts, d_out, d_off, d_st, d_ws, d_in, d_roff, d_dec;
+    HostBuf h_arena, h_len, h_ts, h_out, h_off, h_st, h_in, h_roff, h_dec;
+    Ctx() {
+        if (sbe_device_ready() != 1) fail("no gfx950 device visible");
+        hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    ~Ctx() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+Ctx& ctx() {
+    thread_local Ctx c;
+    return c;
+}
+
+inline int64_t rdi64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    return (int64_t)v;
+}
+inline int32_t rdi32(const uint8_t* p) { return (int32_t)((uint32_t)p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)); }
+
+// device descriptors of n records, in one allocation
+struct Desc {
+    std::vector<uint8_t> status, flags;
+    std::vector<uint16_t> hdr;
+    std::vector<uint64_t> ts;
+    std::vector<uint32_t> off, len;
+};
+
+Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
+    Ctx& c = ctx();
+    Desc d;
+    if (n == 0) return d;
+    const uint64_t base = rec_off[0], total = rec_off[n] - base;
+    // records rebased to 0 so the device stream starts 16-B aligned
+    c.h_in.need(total + 16);
+    std::memcpy(c.h_in.p, data + base, total);
+    c.h_roff.need((n + 1) * 8);
+    uint64_t* ro = static_cast<uint64_t*>(c.h_roff.p);
+    for (size_t i = 0; i <= n; ++i) ro[i] = rec_off[i] - base;
+    c.d_in.need(total + 16);
+    c.d_roff.need((n + 1) * 8);
+    // descriptor SoA: status n, flags n, hdr 8n, ts 8n, off 20n, len 20n (each 16-B aligned)
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_st = 0, o_fl = al(n), o_hdr = o_fl + al(n), o_ts = o_hdr + al(8 * n), o_off = o_ts + al(8 * n),
+                 o_len = o_off + al(20 * n), dbytes = o_len + al(20 * n);
+    c.d_dec.need(dbytes);
+    c.h_dec.need(dbytes);
+    hip_check(hipMemcpyAsync(c.d_in.p, c.h_in.p, total, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_roff.p, c.h_roff.p, (n + 1) * 8, hipMemcpyHostToDevice, c.stream), "H2D");
+    uint8_t* db = static_cast<uint8_t*>(c.d_dec.p);
+    sbe_decoded out{db + o_st, db + o_fl, reinterpret_cast<uint16_t*>(db + o_hdr), reinterpret_cast<uint64_t*>(db + o_ts),
+                    reinterpret_cast<uint32_t*>(db + o_off), reinterpret_cast<uint32_t*>(db + o_len)};
+    if (sbe_decode_batch(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, mode, &out, c.stream) != SBE_OK)
+        fail("sbe_decode_batch");
+    hip_check(hipMemcpyAsync(c.h_dec.p, c.d_dec.p, dbytes, hipMemcpyDeviceToHost, c.stream), "D2H");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    const uint8_t* hb = static_cast<const uint8_t*>(c.h_dec.p);
+    d.status.assign(hb + o_st, hb + o_st + n);
+    d.flags.assign(hb + o_fl, hb + o_fl + n);
+    d.hdr.assign(reinterpret_cast<const uint16_t*>(hb + o_hdr), reinterpret_cast<const uint16_t*>(hb + o_hdr) + 4 * n);
+    d.ts.assign(reinterpret_cast<const uint64_t*>(hb + o_ts), reinterpret_cast<const uint64_t*>(hb + o_ts) + n);
+    d.off.assign(reinterpret_cast<const uint32_t*>(hb + o_off), reinterpret_cast<const uint32_t*>(hb + o_off) + 5 * n);
+    d.len.assign(reinterpret_cast<const uint32_t*>(hb + o_len), reinterpret_cast<const uint32_t*>(hb + o_len) + 5 * n);
+    return d;
+}
+
+ParseResult materialize(const uint8_t* rec, const Desc& d, size_t i) {
+    ParseResult r;
+    const uint8_t st = d.status[i], fl = d.flags[i];
+    const uint16_t* h = &d.hdr[4 * i];
+    auto view = [&](int k) {
+        return std::string(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]);
+    };
+    auto take_hdr = [&] {
+        r.block_length = h[0];
+        r.template_id = h[1];
+        r.schema_id = h[2];
+        r.version = h[3];
+    };
+    const uint32_t param = d.off[5 * i];
+    switch (st) {
+        case SBE_ST_TM:  // src/sbe_encoder.cpp:1021-1135
+            r.success = true;
+            r.message_type = view(1);
+            r.message_id = view(2);
+            r.payload = view(3);
+            r.headers = view(4);
+            r.timestamp = (int64_t)d.ts[i];
+            r.sequence_key_present = (fl & SBE_FL_SEQ_KEY) != 0;
+            take_hdr();
+            break;
+        case SBE_ST_ACK:  // src/sbe_encoder.cpp:916-941
+            r.success = true;
+            r.message_type = "Acknowledgment";
+            r.timestamp = (int64_t)d.ts[i];
+            r.message_id = (fl & SBE_FL_ID_DEFAULT) ? "ack_" + std::to_string(d.ts[i]) : view(0);
+            r.payload = (fl & SBE_FL_PAYLOAD_DEFAULT) ? std::string("SUCCESS") : view(1);
+            r.headers = view(2);
+            take_hdr();
+            break;
+        case SBE_ST_SESSION_EVENT:  // src/sbe_encoder.cpp:629-644 (SessionEvent layout sbe_messages.hpp:39-50)
+            r.success = true;
+            r.message_type = "SessionEvent";
+            r.correlation_id = rdi64(rec + 8);
+            r.session_id = rdi64(rec + 16);
+            r.leadership_term_id = rdi64(rec + 24);
+            r.leader_member_id = rdi32(rec + 32);
+            r.event_code = rdi32(rec + 36);
+            r.payload = view(3);
+            r.timestamp = 0;
+            take_hdr();
+            break;
+        case SBE_ST_ERR_NULL_EMPTY: r.error_message = "Null or empty data"; break;
+        case SBE_ST_ERR_HEADER: r.error_message = "Failed to decode message header"; break;
+        case SBE_ST_ERR_UNKNOWN_TYPE:
+            take_hdr();
+            r.error_message = "Unknown message type: template=" + std::to_string(r.template_id) +
+                              ", schema=" + std::to_string(r.schema_id);
+            break;
+        case SBE_ST_ERR_SESSION_EVENT: r.error_message = "Failed to decode SessionEvent"; break;
+        case SBE_ST_ERR_SESSION_SHORT: r.error_message = "Session message too short to contain embedded message"; break;
+        case SBE_ST_ERR_EMBEDDED_SHORT: r.error_message = "Embedded message too short"; break;
+        case SBE_ST_ERR_EMBEDDED_TEMPLATE:
+            r.error_message = "Unknown embedded message template_id: " + std::to_string(param);
+            break;
+        case SBE_ST_ERR_EMBEDDED_SCHEMA:
+            r.error_message = "Unknown embedded message schema_id: " + std::to_string(param);
+            break;
+        case SBE_ST_ERR_DIRECT_TEMPLATE:
+            r.error_message = "Unknown direct message template_id: " + std::to_string(param);
+            break;
+        case SBE_ST_ERR_TM_E100: r.error_message = "SBE TopicMessage decoding failed: buffer too short [E100]"; break;
+        case SBE_ST_ERR_ACK_SHORT:
+            r.error_message = "Buffer too short for Acknowledgment message. Need at least 16 bytes, got " +
+                              std::to_string(param);
+            break;
+        default: throw std::runtime_error("sbecodec: unexpected parse status");
+    }
+    return r;
+}
+
+const char* kE109[5] = {"topicLength too long for length type [E109]", "messageTypeLength too long for length type [E109]",
+                        "uuidLength too long for length type [E109]", "payloadLength too long for length type [E109]",
+                        "headersLength too long for length type [E109]"};
+
+}  // namespace
+
+bool ParseResult::is_topic_message() const {
+    if (template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID && schema_id == SBEConstants::TOPIC_SCHEMA_ID) return true;
+    if (schema_id == SBEConstants::CLUSTER_SCHEMA_ID && template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID) return true;
+    if (schema_id == SBEConstants::TOPIC_SCHEMA_ID && template_id == SBEConstants::SESSION_EVENT_TEMPLATE_ID) return true;
+    if (!message_type.empty() &&
+        (message_type.find("ORDER") != std::string::npos || message_type.find("TopicMessage") != std::string::npos ||
+         message_type.find("CREATE_ORDER") != std::string::npos || message_type.find("UPDATE_ORDER") != std::string::npos))
+        return true;
+    return false;
+}
+
+bool gpu_codec_available() { return sbe_device_ready() == 1; }
+
+EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) {
+    Ctx& c = ctx();
+    EncodedBatch b;
+    const size_t n = msgs.size();
+    b.offsets.assign(n + 1, 0);
+    b.status.assign(n, 0);
+    if (n == 0) return b;
+    size_t arena = 0;
+    for (const auto& m : msgs) arena += m.topic.size() + m.message_type.size() + m.uuid.size() + m.payload.size() + m.headers.size();
+    c.h_arena.need(arena + 16);
+    c.h_len.need(n * 20);
+    c.h_ts.need(n * 8);
+    uint8_t* ap = static_cast<uint8_t*>(c.h_arena.p);
+    uint32_t* lp = static_cast<uint32_t*>(c.h_len.p);
+    uint64_t* tp = static_cast<uint64_t*>(c.h_ts.p);
+    size_t at = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const std::string_view f[5] = {msgs[i].topic, msgs[i].message_type, msgs[i].uuid, msgs[i].payload, msgs[i].headers};
+        for (int k = 0; k < 5; ++k) {
+            std::memcpy(ap + at, f[k].data(), f[k].size());
+            at += f[k].size();
+            lp[5 * i + k] = (uint32_t)f[k].size();
+        }
+        tp[i] = (uint64_t)msgs[i].timestamp;
+    }
+    // timestamp 0 → the clock the reference reads (src/sbe_encoder.cpp:134-138)
+    const uint64_t now_ms = (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+                                std::chrono::system_clock::now().time_since_epoch())
+                                .count();
+    const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8 : 0u;
+    const uint64_t cap = sbe_encode_output_bound(n, arena, flags) + 16;
+    c.d_arena.need(arena + 16);
+    c.d_len.need(n * 20);
+    c.d_ts.need(n * 8);
+    c.d_out.need(cap);
+    c.d_off.need((n + 1) * 8);
+    c.d_st.need(n);
+    const size_t wsb = sbe_encode_workspace_size(n);
+    c.d_ws.need(wsb);
+    hip_check(hipMemcpyAsync(c.d_arena.p, ap, arena, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_len.p, lp, n * 20, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_ts.p, tp, n * 8, hipMemcpyHostToDevice, c.stream), "H2D");
+    sbe_tm_batch in{static_cast<uint8_t*>(c.d_arena.p), nullptr, static_cast<uint32_t*>(c.d_len.p),
+                    static_cast<uint64_t*>(c.d_ts.p)};
+    if (sbe_encode_topic_batch(&in, n, now_ms, flags, static_cast<uint8_t*>(c.d_out.p), cap,
+                               static_cast<uint64_t*>(c.d_off.p), static_cast<uint8_t*>(c.d_st.p), c.d_ws.p, c.d_ws.cap,
+                               c.stream) != SBE_OK)
+        fail("sbe_encode_topic_batch");
+    hip_check(hipMemcpyAsync(b.offsets.data(), c.d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
+    hip_check(hipMemcpyAsync(b.status.data(), c.d_st.p, n, hipMemcpyDeviceToHost, c.stream), "D2H");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    b.bytes.resize(b.offsets[n]);
+    if (b.offsets[n]) {
+        hip_check(hipMemcpyAsync(b.bytes.data(), c.d_out.p, b.offsets[n], hipMemcpyDeviceToHost, c.stream), "D2H");
+        hip_check(hipStreamSynchronize(c.stream), "sync");
+    }
+    return b;
+}
+
+std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
+                                                           const std::string& uuid, const std::string& payload,
+                                                           const std::string& headers, std::int64_t timestamp) {
+    TopicMessageFields f{topic, message_type, uuid, payload, headers, timestamp};
+    EncodedBatch b = encode_topic_batch({f}, EncodeLength::Reference);
+    const uint8_t st = b.status[0];
+    if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
+    if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
+    return b.bytes;
+}
+
+ParseResult MessageParser::parse_message(const std::uint8_t* data, std::size_t length) {
+    if (!data || length == 0) {  // src/sbe_encoder.cpp:516-519 (no device round trip needed)
+        ParseResult r;
+        r.error_message = "Null or empty data";
+        return r;
+    }
+    const uint64_t off[2] = {0, length};
+    Desc d = run_decode(data, off, 1, SBE_DEC_PARSE_MESSAGE);
+    return materialize(data, d, 0);
+}
+
+std::vector<ParseResult> MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
+    Desc d = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
+    std::vector<ParseResult> out;
+    out.reserve(n);
+    for (size_t i = 0; i < n; ++i) out.push_back(materialize(data + rec_off[i], d, i));
+    return out;
+}
+
+namespace {
+std::optional<AckInfo> ack_from(const uint8_t* rec, const Desc& d, size_t i) {
+    const uint8_t st = d.status[i];
+    if (st != SBE_ST_EG_ACK_SIMPLE && st != SBE_ST_EG_ACK) return std::nullopt;
+    AckInfo a;
+    a.timestamp_nanos = d.ts[i];
+    a.simple_control_ack = st == SBE_ST_EG_ACK_SIMPLE;
+    if (st == SBE_ST_EG_ACK) {
+        auto v = [&](int k) { return std::string(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]); };
+        a.message_id = v(0);
+        a.topic = v(1);
+        a.correlation_id = v(2);
+    }
+    return a;
+}
+}  // namespace
+
+std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len) {
+    if (!data || len < 8) return std::nullopt;  // src/ack_decoder.cpp:30
+    const uint64_t off[2] = {0, len};
+    Desc d = run_decode(data, off, 1, SBE_DEC_ON_EGRESS);
+    return ack_from(data, d, 0);
+}
+
+MessageHandler::MessageHandler() = default;
+MessageHandler::~MessageHandler() = default;
+
+void MessageHandler::handleMessage(const ParseResult& result) {
+    // src/message_handler.cpp:10-16
+    if (result.success)
+        std::printf("[MessageHandler] Handled message: %s\n", result.message_type.c_str());
+    else
+        std::printf("[MessageHandler] Failed to handle message: %s\n", result.error_message.c_str());
+}
+
+void MessageHandler::on_egress(const std::uint8_t* data, std::size_t len) {
+    if (len < 8) return;
+    const uint64_t off[2] = {0, len};
+    on_egress_batch(data, off, 1);
+}
+
+void MessageHandler::on_egress_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
+    Desc d = run_decode(data, rec_off, n, SBE_DEC_ON_EGRESS);
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t* rec = data + rec_off[i];
+        switch (d.status[i]) {
+            case SBE_ST_EG_ACK_SIMPLE:
+            case SBE_ST_EG_ACK:
+                if (ack_cb_) ack_cb_(*ack_from(rec, d, i));
+                break;
+            case SBE_ST_EG_TM:
+                if (tm_cb_) {
+                    auto v = [&](int k) {
+                        return std::string_view(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]);
+                    };
+                    tm_cb_(v(0), v(1), v(2), v(3), v(4));
+                }
+                break;
+            case SBE_ST_EG_THROW_E100: throw std::runtime_error("buffer too short [E100]");
+            default: break;  // SBE_ST_EG_NONE
+        }
+    }
+}
+
+std::size_t offer_batch(const EncodedBatch& batch, const OfferFn& offer) {
+    const size_t n = batch.offsets.empty() ? 0 : batch.offsets.size() - 1;
+    for (size_t i = 0; i < n; ++i) {
+        if (batch.offsets[i + 1] == batch.offsets[i]) continue;  // failed record (status != 0)
+        if (!offer(batch.bytes.data() + batch.offsets[i], batch.offsets[i + 1] - batch.offsets[i])) return i;
+    }
+    return n;
+}
+
+}  // namespace aeron_cluster

@@ -1,0 +1,152 @@
+// aeron_cluster_amd.hpp — C++17 host mirror of the reference's codec surface, backed by the
+// MI355X kernels behind include/sbecodec.h.
+//
+// Same names, argument meaning and error behaviour as the reference (paths relative to it):
+//   SBEEncoder::encode_topic_message   include/aeron_cluster/sbe_messages.hpp:158-164,
+//                                      src/sbe_encoder.cpp:131-167 (E109 → std::runtime_error)
+//   MessageParser::parse_message       include/aeron_cluster/sbe_messages.hpp:422, src/sbe_encoder.cpp:513-551
+//   ParseResult                        include/aeron_cluster/sbe_messages.hpp:306-412
+//   decode_ack / AckInfo               include/aeron_cluster/ack_decoder.hpp:9-19, src/ack_decoder.cpp:29-105
+//   MessageHandler::on_egress          include/aeron_cluster/message_handler.hpp:35-89 (E100 escapes
+//                                      as std::runtime_error("buffer too short [E100]"))
+//   ClusterClient::offer_ingress       include/aeron_cluster/cluster_client.hpp:409 — the sink the
+//                                      encoded records are handed to (OfferFn below)
+// plus batched overloads, which are the point of the GPU path: one launch per batch.
+//
+// Everything computes on the GPU.  There is no CPU codec here: without a gfx950 device every
+// entry point throws std::runtime_error("sbecodec: ...").
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <optional>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace aeron_cluster {
+
+// include/aeron_cluster/config.hpp:169-199
+namespace SBEConstants {
+constexpr std::uint16_t CLUSTER_SCHEMA_ID = 111;
+constexpr std::uint16_t TOPIC_SCHEMA_ID = 1;
+constexpr std::uint16_t SESSION_EVENT_TEMPLATE_ID = 2;
+constexpr std::uint16_t TOPIC_MESSAGE_TEMPLATE_ID = 1;
+constexpr std::uint16_t ACKNOWLEDGMENT_TEMPLATE_ID = 2;
+}  // namespace SBEConstants
+
+// include/aeron_cluster/sbe_messages.hpp:306-328 (fields), :332-377 (predicates)
+struct ParseResult {
+    bool success = false;
+    std::string error_message;
+    std::string message_type;
+    std::string message_id;
+    std::string payload;
+    std::string headers;
+    std::int64_t timestamp = 0;
+    std::uint64_t sequence_number = 0;
+    std::uint16_t template_id = 0;
+    std::uint16_t schema_id = 0;
+    std::uint16_t version = 0;
+    std::uint16_t block_length = 0;
+    std::int64_t correlation_id = 0;
+    std::int64_t session_id = 0;
+    std::int32_t leader_member_id = 0;
+    std::int32_t event_code = 0;
+    std::int64_t leadership_term_id = 0;
+    // The payload carries "_sequence_number", which the reference evaluates with jsoncpp
+    // (src/sbe_encoder.cpp:1031-1125); sequence_number is then left 0 here (parity unpinned).
+    bool sequence_key_present = false;
+
+    bool is_session_event() const {
+        return template_id == SBEConstants::SESSION_EVENT_TEMPLATE_ID && schema_id == SBEConstants::CLUSTER_SCHEMA_ID;
+    }
+    bool is_topic_message() const;
+    bool is_acknowledgment() const {
+        return template_id == SBEConstants::ACKNOWLEDGMENT_TEMPLATE_ID && schema_id == SBEConstants::TOPIC_SCHEMA_ID;
+    }
+};
+
+// include/aeron_cluster/ack_decoder.hpp:9-15
+struct AckInfo {
+    std::uint64_t timestamp_nanos{};
+    std::string message_id;
+    std::string topic;
+    std::string correlation_id;
+    bool simple_control_ack{false};
+};
+
+// One TopicMessage's fields, wire order (TopicMessage.h:515-1231).
+struct TopicMessageFields {
+    std::string_view topic, message_type, uuid, payload, headers;
+    std::int64_t timestamp = 0;  // 0 → the encoder's clock, as the reference does
+};
+
+// A packed batch of encoded records: record i = bytes[offsets[i], offsets[i+1]).
+struct EncodedBatch {
+    std::vector<std::uint8_t> bytes;
+    std::vector<std::uint64_t> offsets;
+    std::vector<std::uint8_t> status;  // SBE_ENC_* per record
+    std::string_view record(std::size_t i) const {
+        return {reinterpret_cast<const char*>(bytes.data()) + offsets[i], static_cast<std::size_t>(offsets[i + 1] - offsets[i])};
+    }
+};
+
+enum class EncodeLength {
+    Reference,  // exactly what SBEEncoder::encode_topic_message returns (26+Σlen)
+    Wire        // the full wire record (34+Σlen), as ClusterClient::publish_topic emits
+};
+
+class SBEEncoder {
+public:
+    // src/sbe_encoder.cpp:131-167: timestamp 0 → system_clock milliseconds; throws
+    // std::runtime_error("<field>Length too long for length type [E109]") above 65534 bytes.
+    static std::vector<std::uint8_t> encode_topic_message(const std::string& topic, const std::string& message_type,
+                                                          const std::string& uuid, const std::string& payload,
+                                                          const std::string& headers, std::int64_t timestamp = 0);
+    // Batch encode: one GPU launch; records with E109 get status != 0 and zero bytes.
+    static EncodedBatch encode_topic_batch(const std::vector<TopicMessageFields>& msgs,
+                                           EncodeLength length = EncodeLength::Wire);
+};
+
+class MessageParser {
+public:
+    static ParseResult parse_message(const std::uint8_t* data, std::size_t length);
+    // Batch: records data[rec_off[i], rec_off[i+1]), one GPU launch.
+    static std::vector<ParseResult> parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
+};
+
+std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len);
+
+using TopicMessageCallback = std::function<void(std::string_view topic, std::string_view msg_type,
+                                                std::string_view uuid, std::string_view payload,
+                                                std::string_view headers)>;
+using AckCallback = std::function<void(const AckInfo&)>;
+
+class MessageHandler {
+public:
+    MessageHandler();
+    ~MessageHandler();
+    void handleMessage(const ParseResult& result);  // src/message_handler.cpp:10-16
+    void on_egress(const std::uint8_t* data, std::size_t len);
+    // Batch form: callbacks in record order; a record where the reference throws stops the batch
+    // with the same std::runtime_error after the callbacks of the records before it.
+    void on_egress_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
+    void set_topic_message_callback(TopicMessageCallback cb) { tm_cb_ = std::move(cb); }
+    void set_ack_callback(AckCallback cb) { ack_cb_ = std::move(cb); }
+
+private:
+    TopicMessageCallback tm_cb_;
+    AckCallback ack_cb_;
+};
+
+// The raw ingress sink (ClusterClient::offer_ingress signature).  Feeds every encoded record of a
+// batch to it in order; returns the number accepted before the first refusal.
+using OfferFn = std::function<bool(const std::uint8_t* data, std::size_t len)>;
+std::size_t offer_batch(const EncodedBatch& batch, const OfferFn& offer);
+
+// true when a gfx950 device is usable (all entry points above need one).
+bool gpu_codec_available();
+
+}  // namespace aeron_cluster

@@ -1,0 +1,186 @@
+// GPU test of the C++ host mirror (aeron-cluster-client-cpp_amd/host): the reference-shaped API
+// against SURVEY Appendix B probe observations and against the oracle (oracle/liboracle.so).
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "aeron_cluster_amd.hpp"
+#include "../../oracle/sbe_oracle.h"
+
+using namespace aeron_cluster;
+
+static int failures = 0;
+#define CHECK(c)                                                            \
+    do {                                                                    \
+        if (!(c)) {                                                         \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                                     \
+        }                                                                   \
+    } while (0)
+
+static std::string hex(const std::vector<uint8_t>& v) {
+    std::string s;
+    char b[3];
+    for (auto c : v) {
+        std::snprintf(b, 3, "%02x", c);
+        s += b;
+    }
+    return s;
+}
+
+static std::vector<uint8_t> wire_tm(const std::vector<std::string>& f, uint64_t ts, uint16_t blk = 16) {
+    std::vector<uint8_t> b = {(uint8_t)blk, (uint8_t)(blk >> 8), 1, 0, 1, 0, 1, 0};
+    for (int i = 0; i < 8; ++i) b.push_back((uint8_t)(ts >> (8 * i)));
+    for (int i = 0; i < 8; ++i) b.push_back(0);
+    for (auto& s : f) {
+        b.push_back((uint8_t)s.size());
+        b.push_back((uint8_t)(s.size() >> 8));
+        b.insert(b.end(), s.begin(), s.end());
+    }
+    return b;
+}
+
+int main() {
+    if (!gpu_codec_available()) {
+        std::fprintf(stderr, "no gfx950 device\n");
+        return 2;
+    }
+    const std::vector<std::string> f5 = {"orders", "CREATE_ORDER", "msg_1", "{\"a\":1}", "{\"h\":2}"};
+    // --- SBEEncoder::encode_topic_message
+    auto e = SBEEncoder::encode_topic_message(f5[0], f5[1], f5[2], f5[3], f5[4], 0x1122334455667788LL);
+    CHECK(e.size() == 63);
+    CHECK(hex(e).rfind("100001000100010088776655443322110000000000000000", 0) == 0);
+    CHECK(hex(e).size() >= 20 && hex(e).substr(hex(e).size() - 20) == "07007b2261223a317d07");
+    CHECK(SBEEncoder::encode_topic_message("", "", "", "", "", 1).size() == 26);
+    CHECK(SBEEncoder::encode_topic_message(f5[0], f5[1], f5[2], f5[3], "", 1).size() == 56);
+    try {
+        SBEEncoder::encode_topic_message(std::string(65535, 'x'), "a", "b", "c", "d", 1);
+        CHECK(false);
+    } catch (const std::runtime_error& ex) {
+        CHECK(std::string(ex.what()) == "topicLength too long for length type [E109]");
+    }
+    // timestamp 0 → wall clock milliseconds
+    auto z = SBEEncoder::encode_topic_message("t", "m", "u", "p", "h", 0);
+    uint64_t zts = 0;
+    for (int i = 7; i >= 0; --i) zts = (zts << 8) | z[8 + i];
+    CHECK(zts > 1700000000000ULL && zts < 100000000000000ULL);
+
+    // --- MessageParser::parse_message probes
+    auto wire = wire_tm(f5, 0x1122334455667788ULL);
+    auto pr = MessageParser::parse_message(e.data(), e.size());
+    CHECK(pr.success && pr.message_type == "CREATE_ORDER" && pr.message_id == "msg_1" && pr.payload == "{\"a\":1}" &&
+          pr.headers.empty());
+    CHECK(pr.is_topic_message());
+    std::vector<uint8_t> cut(wire.begin(), wire.begin() + 50);
+    pr = MessageParser::parse_message(cut.data(), cut.size());
+    CHECK(!pr.success && pr.template_id == 0 && pr.error_message == "SBE TopicMessage decoding failed: buffer too short [E100]");
+    auto t9 = wire;
+    t9[2] = 9;
+    pr = MessageParser::parse_message(t9.data(), t9.size());
+    CHECK(!pr.success && pr.template_id == 9 && pr.schema_id == 1 &&
+          pr.error_message == "Unknown message type: template=9, schema=1");
+    auto b8 = wire_tm(f5, 0x1122334455667788ULL, 8);
+    pr = MessageParser::parse_message(b8.data(), b8.size());
+    CHECK(pr.success && pr.message_type.empty() && pr.message_id.empty() && pr.payload.empty() && pr.headers == "orders");
+    pr = MessageParser::parse_message(wire.data(), 3);
+    CHECK(!pr.success && pr.error_message == "Failed to decode message header");
+    pr = MessageParser::parse_message(nullptr, 0);
+    CHECK(!pr.success && pr.error_message == "Null or empty data");
+    std::vector<uint8_t> sack = {8, 0, 2, 0, 1, 0, 1, 0};
+    const uint64_t ms = 1000000000000ULL;
+    for (int i = 0; i < 8; ++i) sack.push_back((uint8_t)(ms >> (8 * i)));
+    pr = MessageParser::parse_message(sack.data(), sack.size());
+    CHECK(pr.success && pr.message_type == "Acknowledgment" && pr.message_id == "ack_1000000000000" &&
+          pr.payload == "SUCCESS" && pr.timestamp == 1000000000000LL);
+
+    // --- decode_ack / on_egress probes
+    auto a = decode_ack(sack.data(), sack.size());
+    CHECK(a && a->simple_control_ack && a->timestamp_nanos == 1000000000000000000ULL);
+    std::vector<uint8_t> ack37 = {8, 0, 2, 0, 1, 0, 1, 0};
+    for (int i = 0; i < 8; ++i) ack37.push_back((uint8_t)(1700000000000ULL >> (8 * i)));
+    for (std::string s : {"msg_1", "orders", "corr"}) {
+        ack37.push_back((uint8_t)s.size());
+        ack37.push_back(0);
+        ack37.insert(ack37.end(), s.begin(), s.end());
+    }
+    CHECK(ack37.size() == 37 && !decode_ack(ack37.data(), ack37.size()));
+    auto ack45 = ack37;
+    ack45.resize(45, 0);
+    a = decode_ack(ack45.data(), ack45.size());
+    CHECK(a && !a->simple_control_ack && a->message_id == "msg_1" && a->topic == "orders" && a->correlation_id == "corr" &&
+          a->timestamp_nanos == 1700000000000000000ULL);
+    MessageHandler h;
+    int acks = 0, tms = 0;
+    h.set_ack_callback([&](const AckInfo&) { ++acks; });
+    h.set_topic_message_callback([&](std::string_view t, std::string_view, std::string_view, std::string_view,
+                                     std::string_view hd) {
+        ++tms;
+        CHECK(t == "orders" && hd == "{\"h\":2}");
+    });
+    bool threw = false;
+    try {
+        h.on_egress(wire.data(), wire.size());
+    } catch (const std::runtime_error& ex) {
+        threw = std::string(ex.what()) == "buffer too short [E100]";
+    }
+    CHECK(threw);
+    h.on_egress(ack37.data(), ack37.size());
+    CHECK(acks == 0 && tms == 0);
+    h.on_egress(ack45.data(), ack45.size());
+    auto wire8 = wire;
+    wire8.resize(wire.size() + 8, 0);
+    h.on_egress(wire8.data(), wire8.size());
+    CHECK(acks == 1 && tms == 1);
+
+    // --- batch encode / parse vs the oracle on random records
+    std::mt19937_64 rng(42);
+    std::vector<std::vector<std::string>> recs(5000);
+    std::vector<TopicMessageFields> msgs;
+    std::string arena;
+    std::vector<uint32_t> lens;
+    std::vector<uint64_t> tss;
+    for (auto& r : recs) {
+        for (int k = 0; k < 5; ++k) {
+            std::string s(rng() % 90, ' ');
+            for (auto& c : s) c = (char)(32 + rng() % 95);
+            r.push_back(s);
+            arena += s;
+            lens.push_back((uint32_t)s.size());
+        }
+        tss.push_back(rng() | 1);
+    }
+    for (size_t i = 0; i < recs.size(); ++i)
+        msgs.push_back({recs[i][0], recs[i][1], recs[i][2], recs[i][3], recs[i][4], (int64_t)tss[i]});
+    for (auto len : {EncodeLength::Wire, EncodeLength::Reference}) {
+        EncodedBatch b = SBEEncoder::encode_topic_batch(msgs, len);
+        std::vector<uint8_t> eo(arena.size() + 34 * recs.size() + 16);
+        std::vector<uint64_t> eoff(recs.size() + 1);
+        std::vector<uint8_t> est(recs.size());
+        orc_encode_batch(reinterpret_cast<const uint8_t*>(arena.data()), nullptr, lens.data(), tss.data(), recs.size(), 0,
+                         len == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8 : 0u, eo.data(), eoff.data(), est.data(), 1);
+        CHECK(b.offsets == eoff);
+        CHECK(b.bytes.size() == eoff.back() && std::memcmp(b.bytes.data(), eo.data(), b.bytes.size()) == 0);
+        size_t offered = 0;
+        CHECK(offer_batch(b, [&](const uint8_t*, size_t) { ++offered; return true; }) == recs.size());
+        CHECK(offered == recs.size());
+        auto prs = MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), recs.size());
+        for (size_t i = 0; i < recs.size(); ++i) {
+            // the reference-length form drops the last 8 bytes: with headers shorter than 6 bytes
+            // that cuts into the payload and parse_message fails with E100
+            if (len == EncodeLength::Reference && recs[i][4].size() < 6) {
+                CHECK(!prs[i].success &&
+                      prs[i].error_message == "SBE TopicMessage decoding failed: buffer too short [E100]");
+                continue;
+            }
+            CHECK(prs[i].success && prs[i].message_type == recs[i][1] && prs[i].message_id == recs[i][2] &&
+                  prs[i].payload == recs[i][3] && (int64_t)tss[i] == prs[i].timestamp);
+            CHECK(prs[i].headers == (len == EncodeLength::Wire ? recs[i][4] : std::string()));
+            if (failures > 20) break;
+        }
+    }
+    std::printf("host api test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
+    return failures ? 1 : 0;
+}
