@@ -65,6 +65,10 @@ __device__ __forceinline__ void lds_write_chunk(uint32_t* win, uint32_t c, uint4
 }
 
 __device__ __forceinline__ uint32_t lds_dw(const uint32_t* win, uint32_t i) { return win[swz(i)]; }
+// the four dwords of logical chunk c in swizzled (permuted) order
+__device__ __forceinline__ uint4 lds_read_chunk_raw(const uint32_t* win, uint32_t c) {
+    return *reinterpret_cast<const uint4*>(win + ((4u * c) ^ (((c >> 4) & 31u) & 28u)));
+}
 
 // ------------------------------------------------------------------------------------------
 // wave helpers
@@ -699,22 +703,55 @@ __device__ __forceinline__ uint32_t has_byte(uint32_t w, uint32_t byte) {
 
 // "_sequence_number" anywhere in [p, p+n) of the record (flag only; src/sbe_encoder.cpp:1031-1125).
 // Any occurrence fully covers one 4-aligned dword, which then equals key[j..j+4) for j = (4 - s%4)%4:
-// one aligned dword read per 4 payload bytes, compared with those four slices; a hit is verified.
+// one aligned dword per 4 payload bytes, compared with those four slices; a hit is verified.
+constexpr uint32_t kSeqK0 = 0x7165735fu, kSeqK1 = 0x636e6575u, kSeqK2 = 0x756e5f65u, kSeqK3 = 0x7265626du;
+constexpr uint32_t kSeqS1 = 0x75716573u, kSeqS2 = 0x65757165u, kSeqS3 = 0x6e657571u;  // key[1..5), [2..6), [3..7)
+
+// candidate test of the aligned dword w at record offset q
+template <typename R_t>
+__device__ __forceinline__ bool seq_key_at(const R_t& R, uint32_t q, uint32_t w, uint32_t p, uint32_t n) {
+    constexpr uint32_t K = 16;  // strlen("_sequence_number")
+    if (!(w == kSeqK0 || w == kSeqS1 || w == kSeqS2 || w == kSeqS3)) return false;
+    const uint32_t j = w == kSeqK0 ? 0u : w == kSeqS1 ? 1u : w == kSeqS2 ? 2u : 3u;
+    if (q < p + j || q - j + K > p + n) return false;
+    const uint32_t st = q - j;
+    return R.u32(st) == kSeqK0 && R.u32(st + 4) == kSeqK1 && R.u32(st + 8) == kSeqK2 && R.u32(st + 12) == kSeqK3;
+}
+
 template <typename R_t>
 __device__ bool has_seq_key(const R_t& R, uint32_t p, uint32_t n) {
-    constexpr uint32_t K = 16;  // strlen("_sequence_number")
-    if (n < K) return false;
-    const uint32_t k0 = 0x7165735fu, k1 = 0x636e6575u, k2 = 0x756e5f65u, k3 = 0x7265626du;
-    const uint32_t s1 = 0x75716573u, s2 = 0x65757165u, s3 = 0x6e657571u;  // key[1..5), [2..6), [3..7)
+    if (n < 16) return false;
     const uint32_t lead = (4u - R.abs_align(p)) & 3u;  // first aligned record offset is p + lead
-    for (uint32_t q = p + lead; q + 4 <= p + n; q += 4) {
-        const uint32_t w = R.adw(q);
-        const bool hit = w == k0 || w == s1 || w == s2 || w == s3;
-        if (hit) {
-            const uint32_t j = w == k0 ? 0u : w == s1 ? 1u : w == s2 ? 2u : 3u;
-            if (q >= p + j && q - j + K <= p + n) {
-                const uint32_t st = q - j;
-                if (R.u32(st) == k0 && R.u32(st + 4) == k1 && R.u32(st + 8) == k2 && R.u32(st + 12) == k3) return true;
+    for (uint32_t q = p + lead; q + 4 <= p + n; q += 4)
+        if (seq_key_at(R, q, R.adw(q), p, n)) return true;
+    return false;
+}
+
+__device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte of w equal to 'q' (plus borrow noise above a hit)
+    const uint32_t x = w ^ 0x71717171u;
+    return (x - 0x01010101u) & ~x;
+}
+
+// Staged records: every key dword contains 'q' (key[3]), so a 16-byte chunk (one ds_read_b128; the
+// in-chunk swizzle permutes dwords, which a membership test does not care about) without a 'q'
+// byte holds no candidate.  Only flagged chunks run the exact per-dword test.
+template <>
+__device__ bool has_seq_key<LdsRec>(const LdsRec& R, uint32_t p, uint32_t n) {
+    if (n < 16) return false;
+    const uint32_t a0 = R.base + p, a1 = a0 + n;  // window byte range
+    const uint32_t c1 = (a1 + 15) >> 4;
+    for (uint32_t c = a0 >> 4; c < c1; c += 2) {
+        const uint4 v0 = lds_read_chunk_raw(R.win, c);
+        const uint4 v1 = c + 1 < c1 ? lds_read_chunk_raw(R.win, c + 1) : make_uint4(0, 0, 0, 0);
+        const uint32_t t0 = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w)) & 0x80808080u;
+        const uint32_t t1 = (q_bytes(v1.x) | q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
+        if (t0 | t1) {
+#pragma nounroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t A = 16 * c + 4 * k;  // window offset of an aligned dword
+                if (A < a0 || A + 4 > a1) continue;
+                const uint32_t q = A - R.base;
+                if (seq_key_at(R, q, R.adw(q), p, n)) return true;
             }
         }
     }
@@ -931,14 +968,29 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
     const uint64_t wb = T0 & ~15ull;
     const uint64_t end = (T1 + 15) & ~15ull;
     const uint64_t we = (wb + kWin) < end ? wb + kWin : end;
-    const uint32_t nch = (uint32_t)((we - wb) >> 4);
-    for (uint32_t ch = lane; ch < nch; ch += kWave)
-        lds_write_chunk(win, ch, gload128(reinterpret_cast<uintptr_t>(a.in) + wb + 16ull * ch));
+    {
+        // all loads in flight before the first LDS write: one HBM round trip per tile
+        constexpr int kDecRegs = kWin / 16 / kWave;
+        const uint32_t nch = (uint32_t)((we - wb) >> 4);
+        const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
+        uint4 I[kDecRegs];
+#pragma unroll
+        for (int k = 0; k < kDecRegs; ++k) {
+            const uint32_t ch = lane + kWave * k;
+            I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < kDecRegs; ++k) {
+            const uint32_t ch = lane + kWave * k;
+            if (ch < nch) lds_write_chunk(win, ch, I[k]);
+        }
+    }
     __syncthreads();
 
-    if (!valid) return;
     Desc d;
-    if (rl > 0xffffffffull) {  // records beyond u32 sizes are not SBE frames we can bound-check in 32 bits
+    d.clear();
+    if (!valid) {
+    } else if (rl > 0xffffffffull) {  // records beyond u32 sizes are not SBE frames we can bound-check in 32 bits
         d.clear();
         d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE : SBE_ST_ERR_TM_E100;
     } else if (rs >= wb && rs + rl <= we) {
@@ -963,15 +1015,31 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
         return;
     }
 #endif
-    a.status[r] = (uint8_t)d.status;
-    a.flags[r] = (uint8_t)d.flags;
-    *reinterpret_cast<uint2*>(a.hdr + 4 * r) =
-        make_uint2((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16), (uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16));
-    a.ts[r] = d.ts;
+    if (valid) {
+        a.status[r] = (uint8_t)d.status;
+        a.flags[r] = (uint8_t)d.flags;
+        *reinterpret_cast<uint2*>(a.hdr + 4 * r) = make_uint2((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16),
+                                                             (uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16));
+        a.ts[r] = d.ts;
+    }
+    // views [n][5]: transpose through LDS so each store instruction writes 256 contiguous bytes
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        a.view_off[5 * r + k] = d.off[k];
-        a.view_len[5 * r + k] = d.len[k];
+        win[5 * lane + k] = d.off[k];
+        win[5 * kWave + 5 * lane + k] = d.len[k];
+    }
+    __syncthreads();
+    const uint32_t nv = 5u * (uint32_t)(last - t0);
+    uint32_t* vo = a.view_off + 5 * t0;
+    uint32_t* vl = a.view_len + 5 * t0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t i = lane + kWave * k;
+        if (i < nv) {
+            vo[i] = win[i];
+            vl[i] = win[5 * kWave + i];
+        }
     }
 }
 

@@ -130,6 +130,47 @@ def test_decode_edges_every_alignment(codec, mode):
         assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
 
 
+def seq_key_records():
+    """"_sequence_number" (and near misses) at every payload position and alignment, 'q'-dense
+    filler, the key split across the payload/headers boundary and inside other fields."""
+    key = b"_sequence_number"
+    misses = [key[:-1] + b"X", b"X" + key[1:], key[:8] + b"Q" + key[9:], b"qqqq_seqqsequ"]
+    rng = np.random.default_rng(3)
+    recs = []
+    for plen in (16, 17, 18, 19, 20, 31, 33, 47, 64, 95):
+        for pos in range(0, plen - len(key) + 1):
+            for fill in (b"a", b"q", b"e"):
+                pay = bytearray(fill * plen)
+                pay[pos:pos + len(key)] = key
+                recs.append(T.tm_wire([b"t" * (pos % 5), b"ty", b"u" * (plen % 7), bytes(pay), b"{}"], pos))
+    for m in misses:
+        for pos in range(0, 24):
+            pay = b"q" * pos + m + b"u" * (pos % 3)
+            recs.append(T.tm_wire([b"tp", b"", b"id", pay, b"h"], pos))
+    for cut in range(1, len(key)):  # key split between payload and headers: not in the payload
+        recs.append(T.tm_wire([b"t", b"y", b"u", b"xx" + key[:cut], key[cut:] + b"yy"], cut))
+        recs.append(T.tm_wire([key, b"y", key, b"p" * cut, key], cut))
+    for k in range(300):  # random 'q'/'_'-rich payloads
+        n = int(rng.integers(0, 200))
+        pay = rng.choice(np.frombuffer(b"q_sequnbr", np.uint8), n).tobytes()
+        if k % 3 == 0 and n >= 16:
+            at = int(rng.integers(0, n - 15))
+            pay = pay[:at] + key + pay[at + 16:]
+        recs.append(T.tm_wire([b"topic", b"TYPE", b"id", pay, b"{}"], k))
+    return recs
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_seq_key_positions(codec, mode):
+    recs = seq_key_records()
+    for lead in (0, 1, 2, 3, 5, 9, 14):
+        data, off = T.pack_records([b"\0" * lead] + recs)
+        exp = T.oracle_decode(data, off, mode)
+        if mode == T.DEC_PARSE:
+            assert 100 < int((exp["flags"] & T.FL_SEQ_KEY != 0).sum()) < len(recs)
+        assert_same_decode(gpu_decode(codec, data, off, mode), exp)
+
+
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
 def test_decode_mixed(codec, mode):
     data, off = T.mixed_records(50000)
