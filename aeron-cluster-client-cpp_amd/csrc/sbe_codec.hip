@@ -267,78 +267,117 @@ __global__ __launch_bounds__(kScanThreads) void sbe_enc_scan(uint64_t* bsum, uin
 constexpr int32_t kEW = SBE_ENC_WIN;            // output window bytes per pass
 constexpr int32_t kEWIn = SBE_ENC_WIN + 256;    // staged input bytes per pass
 
-__device__ __forceinline__ uint32_t swz_byte(int32_t pos) { return swz((uint32_t)pos >> 2) * 4u + ((uint32_t)pos & 3u); }
+// ---- K3 LDS layout -------------------------------------------------------------------------
+// Input window: linear bytes (window byte 0 sits kInSlack bytes into the array, so the reads a
+// lane makes up to 4 bytes before / 8 bytes after a string stay inside it); per-lane string
+// reads are ds_read_b32 at immediate offsets from one base.  Output window: 256-byte rows
+// padded by 8 bytes, so the two lanes of each of 32 records (256 B apart) write banks
+// 2r + 32q + k: at most 2-way, which ds_write_b32 absorbs.
+constexpr int32_t kInSlack = 16;
+constexpr int32_t kRowPad = 8;
+constexpr int32_t kWoutBytes = kEW + (kEW / 256) * kRowPad;
+constexpr int32_t kWinBytes = kEWIn + 2 * kInSlack;
 
-// Byte-addressed stream of source dwords: the staged LDS input window or global memory.
-struct LdsSrc {
-    const uint32_t* w;
-    __device__ __forceinline__ uint32_t dw(int32_t i) const { return lds_dw(w, (uint32_t)i); }
+__device__ __forceinline__ uint32_t wout_addr(int32_t d) { return (uint32_t)d + (((uint32_t)d >> 8) * kRowPad); }
+
+// Sources of string dwords: dw(i) = the aligned dword i of the source (byte 4i..4i+3).
+struct LdsLin {
+    const uint8_t* b;  // window byte 0
+    __device__ __forceinline__ uint32_t dw(int32_t i) const { return reinterpret_cast<const uint32_t*>(b)[i]; }
 };
-struct GlbSrc {
-    uintptr_t base;  // 4-aligned absolute address of dword 0
-    __device__ __forceinline__ uint32_t dw(int32_t i) const { return gload32(base + 4 * (int64_t)i); }
+struct GlbClamp {  // global memory; reads outside [imin, imax] fetch a neighbour (only don't-care bytes)
+    uintptr_t base4;
+    int32_t imax;
+    __device__ __forceinline__ uint32_t dw(int32_t i) const {
+        i = i < 0 ? 0 : (i > imax ? imax : i);
+        return gload32(base4 + 4u * (uint32_t)i);
+    }
 };
 
-// Write string bytes [o, o+L) of the output window (window-relative; clipped to [lo, hi)) from a
-// source whose byte 0 is stream byte `sb` of S.  Interior dwords: one source read, one
-// v_alignbyte, one ds_write_b32; the (<= 3 + 3) edge bytes are written one by one.
-template <typename Src>
-__device__ __forceinline__ void put_string(uint32_t* wout, int32_t o, int32_t L, int32_t lo, int32_t hi,
-                                           const Src& S, int32_t sb) {
-    int32_t a = o > lo ? o : lo;
-    const int32_t e = (o + L) < hi ? (o + L) : hi;
-    if (a >= e) return;
-    uint8_t* wb8 = reinterpret_cast<uint8_t*>(wout);
-    // head bytes up to the next aligned dword
-    const int32_t ah = (a + 3) & ~3;
-    for (; a < e && a < ah; ++a) {
-        const int32_t b = sb + (a - o);
-        wb8[swz_byte(a)] = (uint8_t)(S.dw(b >> 2) >> (8 * (b & 3)));
-    }
-    const int32_t ee = e & ~3;
-    if (a < ee) {
-        const int32_t b = sb + (a - o);
-        const uint32_t sh = (uint32_t)(b & 3);
-        int32_t i = b >> 2;
-        uint32_t prev = S.dw(i);
-        for (; a < ee; a += 4) {
-            const uint32_t next = sh ? S.dw(i + 1) : 0u;
-            wout[swz((uint32_t)a >> 2)] = __builtin_amdgcn_alignbyte(next, prev, sh);
-            prev = next;
-            ++i;
-            if (!sh) prev = S.dw(i);
-        }
-    }
-    for (; a < e; ++a) {
-        const int32_t b = sb + (a - o);
-        wb8[swz_byte(a)] = (uint8_t)(S.dw(b >> 2) >> (8 * (b & 3)));
-    }
-}
+__device__ __forceinline__ uint64_t low_bytes64(uint64_t v, int32_t n) { return n >= 8 ? v : v & ((1ull << (8 * n)) - 1); }
 
-__device__ __noinline__ void put_string_global(uint32_t* wout, int32_t o, int32_t L, int32_t lo, int32_t hi,
-                                              uintptr_t sa) {
-    const uintptr_t b4 = sa & ~(uintptr_t)3;
-    put_string(wout, o, L, lo, hi, GlbSrc{b4}, (int32_t)(sa - b4));
-}
+// Streams one lane's part of a record into the output window as whole-dword writes: `carry`
+// holds the bytes [pos & ~3, pos) not yet written (zero above them; bytes below `lo` belong to the
+// previous record and are never written).  Only the part's first and last dwords, which a
+// record boundary may share with a neighbour, are written byte by byte.
+struct Writer {
+    uint8_t* w;
+    int32_t lo, pos;
+    uint32_t carry;
 
-// literal bytes [o, o+n) (n <= 8) held little-endian in v, clipped to [lo, hi)
-__device__ __forceinline__ void put_lit(uint32_t* wout, int32_t o, int32_t n, uint64_t v, int32_t lo, int32_t hi) {
-    if (o + n <= lo || o >= hi) return;
-    uint8_t* wb8 = reinterpret_cast<uint8_t*>(wout);
-    if (o >= lo && o + n <= hi) {
-        if ((o & 3) == 0 && n == 8) {
-            wout[swz((uint32_t)o >> 2)] = (uint32_t)v;
-            wout[swz((uint32_t)(o + 4) >> 2)] = (uint32_t)(v >> 32);
-            return;
-        }
-        if ((o & 1) == 0 && n == 2) {  // u16 length field on an even byte: one ds_write_b16
-            *reinterpret_cast<uint16_t*>(wb8 + swz_byte(o)) = (uint16_t)v;
-            return;
-        }
+    __device__ __forceinline__ void put_dw(int32_t d, uint32_t v) const {
+        *reinterpret_cast<uint32_t*>(w + wout_addr(d)) = v;
     }
+    __device__ __forceinline__ void put_bytes(int32_t d, uint32_t v, int32_t b0, int32_t b1) const {
+        uint8_t* p = w + wout_addr(d);
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (k < n && o + k >= lo && o + k < hi) wb8[swz_byte(o + k)] = (uint8_t)(v >> (8 * k));
+        for (int k = 0; k < 4; ++k)
+            if (k >= b0 && k < b1) p[k] = (uint8_t)(v >> (8 * k));
+    }
+    __device__ __forceinline__ void put_first(int32_t d, uint32_t v) const {
+        if (d >= lo) put_dw(d, v); else put_bytes(d, v, lo - d, 4);
+    }
+    // n (1..8) literal bytes, v zero above them
+    __device__ __forceinline__ void lit(uint64_t v, int32_t n) {
+        const int32_t t = pos & 3, d = pos & ~3, total = t + n;
+        const uint64_t lo64 = (v << (8 * t)) | carry;
+        const uint32_t x0 = (uint32_t)lo64, x1 = (uint32_t)(lo64 >> 32);
+        const uint32_t x2 = t ? (uint32_t)(v >> (64 - 8 * t)) : 0u;
+        if (total >= 4) put_first(d, x0);
+        if (total >= 8) put_dw(d + 4, x1);
+        carry = total >= 8 ? x2 : (total >= 4 ? x1 : x0);
+        pos += n;
+    }
+    // m >= 1 bytes from source bytes [s, s+m): output dword d+4k takes source bytes
+    // [u+4k, u+4k+4), u = s - (pos & 3) — one v_alignbyte of two source dwords.
+    template <typename Src>
+    __device__ __forceinline__ void str(const Src& S, int32_t s, int32_t m) {
+        const int32_t t = pos & 3, d = pos & ~3, total = t + m;
+        const int32_t u = s - t;
+        const uint32_t sh = (uint32_t)u & 3u;
+        const int32_t i0 = u >> 2;
+        const int32_t nd = total >> 2, rem = total & 3;
+        uint32_t prev = S.dw(i0);
+        const uint32_t nx = S.dw(i0 + 1);
+        const uint32_t w0 = (__builtin_amdgcn_alignbyte(nx, prev, sh) & ~byte_mask_bits((uint32_t)t)) | carry;
+        pos += m;
+        if (nd == 0) {
+            carry = w0 & byte_mask_bits((uint32_t)total);
+            return;
+        }
+        put_first(d, w0);
+        prev = nx;
+        int32_t k = 1;
+        for (; k + 4 <= nd; k += 4) {
+            const uint32_t n0 = S.dw(i0 + k + 1), n1 = S.dw(i0 + k + 2), n2 = S.dw(i0 + k + 3), n3 = S.dw(i0 + k + 4);
+            put_dw(d + 4 * k, __builtin_amdgcn_alignbyte(n0, prev, sh));
+            put_dw(d + 4 * k + 4, __builtin_amdgcn_alignbyte(n1, n0, sh));
+            put_dw(d + 4 * k + 8, __builtin_amdgcn_alignbyte(n2, n1, sh));
+            put_dw(d + 4 * k + 12, __builtin_amdgcn_alignbyte(n3, n2, sh));
+            prev = n3;
+        }
+        for (; k < nd; ++k) {
+            const uint32_t n0 = S.dw(i0 + k + 1);
+            put_dw(d + 4 * k, __builtin_amdgcn_alignbyte(n0, prev, sh));
+            prev = n0;
+        }
+        carry = rem ? (__builtin_amdgcn_alignbyte(S.dw(i0 + nd + 1), prev, sh) & byte_mask_bits((uint32_t)rem)) : 0u;
+    }
+    __device__ __forceinline__ void flush() const {
+        const int32_t t = pos & 3;
+        if (t) {
+            const int32_t d = pos & ~3;
+            put_bytes(d, carry, lo > d ? lo - d : 0, t);
+        }
+    }
+};
+
+// string bytes from global memory (gather mode, or outside the staged window)
+__device__ __noinline__ Writer str_global(Writer W, uintptr_t sa, int32_t m) {
+    const uintptr_t b4 = sa & ~(uintptr_t)3;
+    const int32_t sl = (int32_t)(sa - b4);
+    W.str(GlbClamp{b4, (sl + m - 1) >> 2}, sl, m);
+    return W;
 }
 
 // ---- K3: persistent, software-pipelined pack kernel ---------------------------------------
@@ -468,17 +507,19 @@ __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int l
     }
 }
 
-__device__ __forceinline__ void stage_write(uint32_t* win_in, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
+__device__ __forceinline__ void stage_write(uint8_t* inb, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        if ((int32_t)(16 * ch) < nbytes) lds_write_chunk(win_in, ch, I[k]);
+        if ((int32_t)(16 * ch) < nbytes) *reinterpret_cast<uint4*>(inb + 16 * ch) = I[k];
     }
 }
 
-// compose this lane's part of its record for output window [wb, we)
+// compose this lane's part [ps, pe) of its record, clipped to output window [wb, we); record
+// layout TopicMessage.h:221-238 (header), :362-437 (timestamp, sequenceNumber 0), :515-1231
+// (u16 length + bytes per string)
 template <bool kPacked>
-__device__ __forceinline__ void compose(uint32_t* wout, const uint32_t* win_in, const TileSt& S, uint64_t wb,
+__device__ __forceinline__ void compose(uint8_t* wout, const uint8_t* inb, const TileSt& S, uint64_t wb,
                                         uint64_t we, uintptr_t swb, int32_t win_bytes) {
     if (!(S.rec_out && S.ps < S.pe && S.ps < we && S.pe > wb)) return;
     const int32_t R0 = (int32_t)((int64_t)S.rs - (int64_t)wb);
@@ -486,59 +527,95 @@ __device__ __forceinline__ void compose(uint32_t* wout, const uint32_t* win_in, 
     const int32_t lo = pl > 0 ? pl : 0;
     const int32_t hr = (int32_t)((int64_t)S.pe - (int64_t)wb);
     const int32_t hi = hr < (int32_t)(we - wb) ? hr : (int32_t)(we - wb);
-    // header {16,1,1,1}, timestamp, sequenceNumber 0 (TopicMessage.h:221-238, :362-437)
-    put_lit(wout, R0, 8, (uint64_t)(SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16)) |
-                             ((uint64_t)(SBE_TOPIC_SCHEMA_ID | (1u << 16)) << 32), lo, hi);
-    put_lit(wout, R0 + 8, 8, S.ts, lo, hi);
-    put_lit(wout, R0 + 16, 8, 0ull, lo, hi);
-    int32_t o = R0 + 24;
-    uint64_t sin = S.in0;
-#pragma nounroll
-    for (int f = 0; f < 5; ++f) {
-        const uint32_t Lu = f == 0 ? S.L[0] : f == 1 ? S.L[1] : f == 2 ? S.L[2] : f == 3 ? S.L[3] : S.L[4];
-        put_lit(wout, o, 2, Lu & 0xffffu, lo, hi);  // u16 length, then the bytes (:515-529)
-        o += 2;
-        const int32_t Lf = (int32_t)Lu;
-        if (Lf && o < hi && o + Lf > lo) {
-            uintptr_t sa;
-            if (kPacked) {
-                sa = S.in_tile + sin;
-            } else {
-                sa = f == 0 ? S.gsrc[0] : f == 1 ? S.gsrc[1] : f == 2 ? S.gsrc[2] : f == 3 ? S.gsrc[3] : S.gsrc[4];
-            }
-            if (kPacked && sa >= swb && sa + Lf <= swb + (uint32_t)win_bytes) {
-                put_string(wout, o, Lf, lo, hi, LdsSrc{win_in}, (int32_t)(sa - swb));
-            } else {
-                put_string_global(wout, o, Lf, lo, hi, sa);
+    Writer W{wout, lo, lo, 0u};
+    int32_t x = lo - R0;  // record-relative position of W.pos
+    const int32_t end = hi - R0;
+    {
+        const uint64_t hdr = (uint64_t)(SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16)) |
+                             ((uint64_t)(SBE_TOPIC_SCHEMA_ID | (1u << 16)) << 32);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint64_t v = j == 0 ? hdr : (j == 1 ? S.ts : 0ull);
+            if (x < 8 * j + 8 && x < end) {
+                const int32_t e = end < 8 * j + 8 ? end : 8 * j + 8;
+                W.lit(low_bytes64(v >> (8 * (x - 8 * j)), e - x), e - x);
+                x = e;
             }
         }
-        o += Lf;
-        sin += (uint32_t)Lf;
     }
+    int32_t o = 24;
+    const int64_t src0 = kPacked ? (int64_t)(S.in_tile + S.in0) - (int64_t)swb : 0;
+    int64_t src = src0;
+#pragma nounroll
+    for (int f = 0; f < 5; ++f) {
+        if (x >= end) break;
+        const uint32_t Lu = f == 0 ? S.L[0] : f == 1 ? S.L[1] : f == 2 ? S.L[2] : f == 3 ? S.L[3] : S.L[4];
+        const int32_t Lf = (int32_t)Lu;
+        if (x < o + 2) {
+            const int32_t e = end < o + 2 ? end : o + 2;
+            W.lit((uint64_t)((Lu & 0xffffu) >> (8 * (x - o))) & ((1u << (8 * (e - x))) - 1u), e - x);
+            x = e;
+            if (x >= end) break;
+        }
+        const int32_t so = o + 2;
+        if (x < so + Lf) {
+            const int32_t e = end < so + Lf ? end : so + Lf;
+            const int32_t m = e - x, off = x - so;
+            if (kPacked && src + off >= 0 && src + off + m <= (int64_t)win_bytes) {
+                W.str(LdsLin{inb}, (int32_t)(src + off), m);
+            } else {
+                uintptr_t sa;
+                if (kPacked) {
+                    sa = swb + (uintptr_t)(src + off);
+                } else {
+                    sa = (f == 0 ? S.gsrc[0] : f == 1 ? S.gsrc[1] : f == 2 ? S.gsrc[2] : f == 3 ? S.gsrc[3] : S.gsrc[4]) +
+                         (uintptr_t)off;
+                }
+                W = str_global(W, sa, m);
+            }
+            x = e;
+        }
+        o = so + Lf;
+        src += Lf;
+    }
+    W.flush();
 }
 
-__device__ __forceinline__ void store_window(uint8_t* out, const uint32_t* wout, uint64_t T0, uint64_t wb, uint64_t we,
+// window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte
+__device__ __forceinline__ void store_window(uint8_t* out, const uint8_t* wout, uint64_t T0, uint64_t wb, uint64_t we,
                                              int lane) {
+    constexpr int kIt = kEW / 16 / kWave;
     const uint64_t lo = wb > T0 ? wb : T0;
     const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
-    for (uint32_t ch = lane; ch < nch; ch += kWave) {
-        const uint64_t g = wb + 16ull * ch;
-        const uint4 v = lds_read_chunk(wout, ch);
-        if (g >= lo && g + 16 <= we) {
-            *reinterpret_cast<uint4*>(out + g) = v;
-        } else {
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    uint4 v[kIt];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k)
-                if (g + k >= lo && g + k < we) out[g + k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+    for (int k = 0; k < kIt; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        const uint2* p = reinterpret_cast<const uint2*>(wout + 16 * ch + (ch >> 4) * kRowPad);
+        const uint2 a0 = p[0], a1 = p[1];
+        v[k] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+    }
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        if (ch >= nch) continue;
+        const uint64_t g = wb + 16ull * ch;
+        if (g >= lo && g + 16 <= we) {
+            *reinterpret_cast<uint4*>(out + g) = v[k];
+        } else {
+            const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (g + j >= lo && g + j < we) out[g + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
         }
     }
 }
 
 template <bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
-    __shared__ uint32_t wout[kEW / 4];
-    __shared__ uint32_t win_in[kPacked ? kEWIn / 4 : 4];
+    __shared__ __attribute__((aligned(16))) uint8_t wout[kWoutBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
+    uint8_t* const win_in = win_raw + kInSlack;
     const int lane = threadIdx.x;
     const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
     const uint64_t G = gridDim.x;
@@ -596,8 +673,20 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
                 int32_t nbw = 0;
                 if (kPacked) {
                     stage_range(S, wb, lane, sw, nbw);
-                    const uint32_t nch = (uint32_t)(nbw >> 4);
-                    for (uint32_t ch = lane; ch < nch; ch += kWave) lds_write_chunk(win_in, ch, gload128(sw + 16u * ch));
+                    // I holds the next tile's prefetch: stage this window in batches of 3 chunks
+                    for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
+                        uint4 J[3];
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const uint32_t ch = lane + kWave * (k0 + k);
+                            J[k] = (int32_t)(16 * ch) < nbw ? gload128(sw + 16u * ch) : make_uint4(0, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const uint32_t ch = lane + kWave * (k0 + k);
+                            if ((int32_t)(16 * ch) < nbw) *reinterpret_cast<uint4*>(win_in + 16 * ch) = J[k];
+                        }
+                    }
                     __syncthreads();
                 }
                 compose<kPacked>(wout, win_in, S, wb, we, sw, nbw);
