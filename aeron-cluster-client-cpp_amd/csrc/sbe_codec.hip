@@ -278,12 +278,28 @@ constexpr int32_t kRowPad = 8;
 constexpr int32_t kWoutBytes = kEW + (kEW / 256) * kRowPad;
 constexpr int32_t kWinBytes = kEWIn + 2 * kInSlack;
 
+// LDS pointers keep their address space through structs and non-inlined calls (a generic
+// pointer there would turn every window access into a flat_* instruction).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+typedef __attribute__((address_space(3))) const u32x2 lds_cu32x2;
+typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+__device__ __forceinline__ void lds_store16(lds_u8* p, uint4 v) {
+    u32x4 x;
+    x.x = v.x; x.y = v.y; x.z = v.z; x.w = v.w;
+    *reinterpret_cast<lds_u32x4*>(p) = x;
+}
+
 __device__ __forceinline__ uint32_t wout_addr(int32_t d) { return (uint32_t)d + (((uint32_t)d >> 8) * kRowPad); }
 
 // Sources of string dwords: dw(i) = the aligned dword i of the source (byte 4i..4i+3).
 struct LdsLin {
-    const uint8_t* b;  // window byte 0
-    __device__ __forceinline__ uint32_t dw(int32_t i) const { return reinterpret_cast<const uint32_t*>(b)[i]; }
+    lds_cu8* b;  // window byte 0
+    __device__ __forceinline__ uint32_t dw(int32_t i) const { return reinterpret_cast<lds_cu32*>(b)[i]; }
 };
 struct GlbClamp {  // global memory; reads outside [imin, imax] fetch a neighbour (only don't-care bytes)
     uintptr_t base4;
@@ -301,15 +317,15 @@ __device__ __forceinline__ uint64_t low_bytes64(uint64_t v, int32_t n) { return 
 // previous record and are never written).  Only the part's first and last dwords, which a
 // record boundary may share with a neighbour, are written byte by byte.
 struct Writer {
-    uint8_t* w;
+    lds_u8* w;
     int32_t lo, pos;
     uint32_t carry;
 
     __device__ __forceinline__ void put_dw(int32_t d, uint32_t v) const {
-        *reinterpret_cast<uint32_t*>(w + wout_addr(d)) = v;
+        *reinterpret_cast<lds_u32*>(w + wout_addr(d)) = v;
     }
     __device__ __forceinline__ void put_bytes(int32_t d, uint32_t v, int32_t b0, int32_t b1) const {
-        uint8_t* p = w + wout_addr(d);
+        lds_u8* p = w + wout_addr(d);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (k >= b0 && k < b1) p[k] = (uint8_t)(v >> (8 * k));
@@ -348,12 +364,24 @@ struct Writer {
         put_first(d, w0);
         prev = nx;
         int32_t k = 1;
+        // single dwords up to a 16-byte output boundary, then whole 16-byte groups (never
+        // across a padded row: one address, one ds_write2_b64), then the tail
+        const int32_t kg = 4 - ((d >> 2) & 3);
+        for (; k < kg && k < nd; ++k) {
+            const uint32_t n0 = S.dw(i0 + k + 1);
+            put_dw(d + 4 * k, __builtin_amdgcn_alignbyte(n0, prev, sh));
+            prev = n0;
+        }
         for (; k + 4 <= nd; k += 4) {
             const uint32_t n0 = S.dw(i0 + k + 1), n1 = S.dw(i0 + k + 2), n2 = S.dw(i0 + k + 3), n3 = S.dw(i0 + k + 4);
-            put_dw(d + 4 * k, __builtin_amdgcn_alignbyte(n0, prev, sh));
-            put_dw(d + 4 * k + 4, __builtin_amdgcn_alignbyte(n1, n0, sh));
-            put_dw(d + 4 * k + 8, __builtin_amdgcn_alignbyte(n2, n1, sh));
-            put_dw(d + 4 * k + 12, __builtin_amdgcn_alignbyte(n3, n2, sh));
+            u32x2 lo2, hi2;
+            lo2.x = __builtin_amdgcn_alignbyte(n0, prev, sh);
+            lo2.y = __builtin_amdgcn_alignbyte(n1, n0, sh);
+            hi2.x = __builtin_amdgcn_alignbyte(n2, n1, sh);
+            hi2.y = __builtin_amdgcn_alignbyte(n3, n2, sh);
+            lds_u8* g = w + wout_addr(d + 4 * k);
+            reinterpret_cast<lds_u32x2*>(g)[0] = lo2;
+            reinterpret_cast<lds_u32x2*>(g)[1] = hi2;
             prev = n3;
         }
         for (; k < nd; ++k) {
@@ -395,15 +423,16 @@ struct TileIn {  // raw per-lane loads of one tile
     uint64_t bo, bi;  // block prefix
 };
 
-struct TileSt {  // prepared per-lane state of one tile
-    uint64_t rs, re, ps, pe;  // record range, this lane's part of it
+struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from T0 / in_tile
+    uint32_t rs, rec_out, ps, pe;  // this lane's record and its part [ps, pe) of it
+    uint64_t in0;                  // packed: the record's first string byte
+    uint32_t L[5];
     uint64_t ts;
-    uint32_t L[5], rec_out;
-    uint64_t in0;             // packed: record's first string byte, relative to in_tile
-    uint64_t T0, T1;          // tile output range (clipped to capacity)
-    uintptr_t in_tile;        // packed: absolute address of the tile's first input byte
-    uint32_t agg_in;
-    uintptr_t gsrc[5];        // gather mode: absolute string addresses
+    uint64_t T0;                   // tile output start (uniform)
+    uint32_t len;                  // tile output bytes, clipped to the capacity (uniform)
+    uint32_t agg_in;               // packed: staged-input limit, bytes from in_tile (uniform)
+    uintptr_t in_tile;             // packed: absolute address of the tile's first input byte (uniform)
+    uintptr_t gsrc[5];             // gather mode: absolute string addresses
 };
 
 template <bool kPacked>
@@ -430,7 +459,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const int q = lane % kLpr, lead = lane - q;
     const uint64_t r = tile * kRpt + lane / kLpr;
     const bool valid = r < a.n;
-    uint32_t sum = 0;
+    uint64_t sum = 0;
     uint8_t st = SBE_ENC_OK;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
@@ -441,34 +470,42 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
         if (x.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
     const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
-    const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + sum : 0u;
-    const uint32_t rec_in = (kPacked && valid) ? sum : 0u;
+    const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
+    const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
     const uint64_t base_out = uniform64(x.bo + wave_sum64(x.po));
     const uint64_t base_in = kPacked ? uniform64(x.bi + wave_sum64(x.pi)) : 0ull;
-    const uint32_t lo_out = q == 0 ? rec_out : 0u, lo_in = q == 0 ? rec_in : 0u;
+    const uint32_t lo_out = q == 0 ? rec_out : 0u;
+    const uint64_t lo_in = q == 0 ? rec_in : 0ull;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
-    const uint32_t inc_in = kPacked ? wave_incl_scan(lo_in, lane) : 0u;
     const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
-    S.agg_in = kPacked ? __builtin_amdgcn_readfirstlane(__shfl(inc_in, kWave - 1, kWave)) : 0u;
-    const uint32_t ex_out = __shfl(inc_out - lo_out, lead, kWave);
-    S.in0 = kPacked ? (uint64_t)__shfl(inc_in - lo_in, lead, kWave) : 0ull;
+    S.rs = __shfl(inc_out - lo_out, lead, kWave);
     S.rec_out = rec_out;
-    S.rs = base_out + ex_out;
-    S.re = S.rs + rec_out;
+    if (kPacked) {
+        const uint64_t inc_in = wave_incl_scan64(lo_in, lane);
+        const uint64_t agg_in = uniform64(__shfl(inc_in, kWave - 1, kWave));
+        S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
+        S.in0 = __shfl(inc_in - lo_in, lead, kWave);
+    } else {
+        S.agg_in = 0;
+        S.in0 = 0;
+    }
     S.ts = x.ts ? x.ts : a.ts_default;
+    const uint32_t re = S.rs + rec_out;
+    const uint64_t cap_rel64 = a.cap > base_out ? a.cap - base_out : 0ull;
+    const uint32_t cap_rel = cap_rel64 < (uint64_t)agg_out ? (uint32_t)cap_rel64 : agg_out;
     if (valid && q == 0) {
-        if (st == SBE_ENC_OK && S.re > a.cap) st = SBE_ENC_OVERFLOW;
-        a.out_off[r] = S.rs;
-        if (r == a.n - 1) a.out_off[a.n] = S.re;
+        if (st == SBE_ENC_OK && (uint64_t)re > cap_rel64) st = SBE_ENC_OVERFLOW;
+        a.out_off[r] = base_out + S.rs;
+        if (r == a.n - 1) a.out_off[a.n] = base_out + re;
         if (a.status) a.status[r] = st;
     }
-    const uint64_t ps = q == 0 ? S.rs : ((S.rs + (uint64_t)q * rec_out / kLpr + 3) & ~3ull);
-    const uint64_t pe = q == kLpr - 1 ? S.re : ((S.rs + (uint64_t)(q + 1) * rec_out / kLpr + 3) & ~3ull);
-    const uint64_t hi_rec = S.re < a.cap ? S.re : a.cap;
-    S.ps = ps < S.re ? ps : S.re;
+    const uint32_t ps = q == 0 ? S.rs : ((S.rs + (uint32_t)q * rec_out / kLpr + 3) & ~3u);
+    const uint32_t pe = q == kLpr - 1 ? re : ((S.rs + (uint32_t)(q + 1) * rec_out / kLpr + 3) & ~3u);
+    const uint32_t hi_rec = re < cap_rel ? re : cap_rel;
+    S.ps = ps < re ? ps : re;
     S.pe = pe < hi_rec ? pe : hi_rec;
     S.T0 = base_out;
-    S.T1 = (base_out + agg_out) < a.cap ? (base_out + agg_out) : a.cap;
+    S.len = cap_rel;
     S.in_tile = reinterpret_cast<uintptr_t>(a.arena) + base_in;
     if (!kPacked) {
 #pragma unroll
@@ -479,19 +516,20 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
 }
 
 // one output window covers the tile: the pipelined path
-__device__ __forceinline__ bool single_window(const TileSt& S) { return S.T1 - (S.T0 & ~15ull) <= (uint64_t)kEW; }
+__device__ __forceinline__ bool single_window(const TileSt& S) { return S.len + (uint32_t)(S.T0 & 15) <= (uint32_t)kEW; }
 
-// Staged input range for output window [wb, ...): from the first string byte at/after max(wb,T0)
-// (input offset >= p - 34 within the record holding it) for kEWIn bytes, clipped to the tile.
-__device__ __forceinline__ void stage_range(const TileSt& S, uint64_t wb, int lane, uintptr_t& swb,
+// Staged input range for the output window starting wrel bytes from T0: from the first string
+// byte at/after max(wrel, 0) (input offset >= p - 34 within the record holding it) for kEWIn
+// bytes, clipped to the tile's input.
+__device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int lane, uintptr_t& swb,
                                             int32_t& nbytes) {
-    const uint64_t g = wb > S.T0 ? wb : S.T0;
+    const uint32_t g = wrel > 0 ? (uint32_t)wrel : 0u;
     const int q = lane % kLpr;
-    const uint64_t mine = __ballot(q == 0 && S.rec_out && S.rs <= g && g < S.re);
+    const uint64_t mine = __ballot(q == 0 && S.rec_out && S.rs <= g && g < S.rs + S.rec_out);
     const int ra = mine ? __builtin_ctzll(mine) : 0;
-    const uint64_t ra_rs = uniform64(__shfl(S.rs, ra, kWave));
+    const uint32_t ra_rs = __builtin_amdgcn_readfirstlane(__shfl(S.rs, ra, kWave));
     const uint64_t ra_in = uniform64(__shfl(S.in0, ra, kWave));
-    const uint64_t p = g - ra_rs;
+    const uint32_t p = g - ra_rs;
     const uintptr_t first = S.in_tile + ra_in + (p > 34 ? p - 34 : 0);
     swb = first & ~(uintptr_t)15;
     const uintptr_t lim = (S.in_tile + S.agg_in + 15) & ~(uintptr_t)15;
@@ -507,11 +545,11 @@ __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int l
     }
 }
 
-__device__ __forceinline__ void stage_write(uint8_t* inb, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
+__device__ __forceinline__ void stage_write(lds_u8* inb, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        if ((int32_t)(16 * ch) < nbytes) *reinterpret_cast<uint4*>(inb + 16 * ch) = I[k];
+        if ((int32_t)(16 * ch) < nbytes) lds_store16(inb + 16 * ch, I[k]);
     }
 }
 
@@ -519,14 +557,13 @@ __device__ __forceinline__ void stage_write(uint8_t* inb, int32_t nbytes, int la
 // layout TopicMessage.h:221-238 (header), :362-437 (timestamp, sequenceNumber 0), :515-1231
 // (u16 length + bytes per string)
 template <bool kPacked>
-__device__ __forceinline__ void compose(uint8_t* wout, const uint8_t* inb, const TileSt& S, uint64_t wb,
-                                        uint64_t we, uintptr_t swb, int32_t win_bytes) {
-    if (!(S.rec_out && S.ps < S.pe && S.ps < we && S.pe > wb)) return;
-    const int32_t R0 = (int32_t)((int64_t)S.rs - (int64_t)wb);
-    const int32_t pl = (int32_t)((int64_t)S.ps - (int64_t)wb);
+__device__ __forceinline__ void compose(lds_u8* wout, lds_cu8* inb, const TileSt& S, int32_t wrel, int32_t we_rel,
+                                        uintptr_t swb, int32_t win_bytes) {
+    if (!(S.rec_out && S.ps < S.pe && (int32_t)S.ps < we_rel && (int32_t)S.pe > wrel)) return;
+    const int32_t R0 = (int32_t)S.rs - wrel;
+    const int32_t pl = (int32_t)S.ps - wrel;
     const int32_t lo = pl > 0 ? pl : 0;
-    const int32_t hr = (int32_t)((int64_t)S.pe - (int64_t)wb);
-    const int32_t hi = hr < (int32_t)(we - wb) ? hr : (int32_t)(we - wb);
+    const int32_t hi = ((int32_t)S.pe < we_rel ? (int32_t)S.pe : we_rel) - wrel;
     Writer W{wout, lo, lo, 0u};
     int32_t x = lo - R0;  // record-relative position of W.pos
     const int32_t end = hi - R0;
@@ -582,7 +619,7 @@ __device__ __forceinline__ void compose(uint8_t* wout, const uint8_t* inb, const
 }
 
 // window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte
-__device__ __forceinline__ void store_window(uint8_t* out, const uint8_t* wout, uint64_t T0, uint64_t wb, uint64_t we,
+__device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64_t T0, uint64_t wb, uint64_t we,
                                              int lane) {
     constexpr int kIt = kEW / 16 / kWave;
     const uint64_t lo = wb > T0 ? wb : T0;
@@ -591,8 +628,8 @@ __device__ __forceinline__ void store_window(uint8_t* out, const uint8_t* wout, 
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
-        const uint2* p = reinterpret_cast<const uint2*>(wout + 16 * ch + (ch >> 4) * kRowPad);
-        const uint2 a0 = p[0], a1 = p[1];
+        lds_cu32x2* p = reinterpret_cast<lds_cu32x2*>(wout + 16 * ch + (ch >> 4) * kRowPad);
+        const u32x2 a0 = p[0], a1 = p[1];
         v[k] = make_uint4(a0.x, a0.y, a1.x, a1.y);
     }
 #pragma unroll
@@ -613,9 +650,10 @@ __device__ __forceinline__ void store_window(uint8_t* out, const uint8_t* wout, 
 
 template <bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t wout[kWoutBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
-    uint8_t* const win_in = win_raw + kInSlack;
+    lds_u8* const wout = (lds_u8*)wout_arr;
+    lds_u8* const win_in = (lds_u8*)win_raw + kInSlack;
     const int lane = threadIdx.x;
     const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
     const uint64_t G = gridDim.x;
@@ -629,7 +667,7 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
     int32_t nb = 0;
     bool fast = kPacked && single_window(S);
     if (fast) {
-        stage_range(S, S.T0 & ~15ull, lane, swb, nb);
+        stage_range(S, -(int32_t)(S.T0 & 15), lane, swb, nb);
         stage_issue(swb, nb, lane, I);
     }
     uint64_t tn = t + G;
@@ -649,7 +687,7 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
             Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane);
             fast = kPacked && single_window(Sn);
             if (fast) {
-                stage_range(Sn, Sn.T0 & ~15ull, lane, swb, nb);
+                stage_range(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
                 stage_issue(swb, nb, lane, I);
             }
             const uint64_t t2 = tn + G;
@@ -657,22 +695,22 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
         }
         // current tile: compose + store, one window (fast) or window by window
         if (cur_fast) {
-            const uint64_t wb = S.T0 & ~15ull;
+            const int32_t wrel = -(int32_t)(S.T0 & 15);
 #ifndef SBE_ABL_NO_COMPOSE
-            compose<kPacked>(wout, win_in, S, wb, S.T1, cur_swb, cur_nb);
+            compose<kPacked>(wout, win_in, S, wrel, (int32_t)S.len, cur_swb, cur_nb);
 #endif
             __syncthreads();
 #ifndef SBE_ABL_NO_STORE
-            store_window(a.out, wout, S.T0, wb, S.T1, lane);
+            store_window(a.out, wout, S.T0, S.T0 & ~15ull, S.T0 + S.len, lane);
 #endif
             __syncthreads();
         } else {
-            for (uint64_t wb = S.T0 & ~15ull; wb < S.T1; wb += kEW) {
-                const uint64_t we = wb + kEW < S.T1 ? wb + kEW : S.T1;
+            for (int32_t wrel = -(int32_t)(S.T0 & 15); wrel < (int32_t)S.len; wrel += kEW) {
+                const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
                 uintptr_t sw = 0;
                 int32_t nbw = 0;
                 if (kPacked) {
-                    stage_range(S, wb, lane, sw, nbw);
+                    stage_range(S, wrel, lane, sw, nbw);
                     // I holds the next tile's prefetch: stage this window in batches of 3 chunks
                     for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
                         uint4 J[3];
@@ -684,14 +722,14 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
 #pragma unroll
                         for (int k = 0; k < 3; ++k) {
                             const uint32_t ch = lane + kWave * (k0 + k);
-                            if ((int32_t)(16 * ch) < nbw) *reinterpret_cast<uint4*>(win_in + 16 * ch) = J[k];
+                            if ((int32_t)(16 * ch) < nbw) lds_store16(win_in + 16 * ch, J[k]);
                         }
                     }
                     __syncthreads();
                 }
-                compose<kPacked>(wout, win_in, S, wb, we, sw, nbw);
+                compose<kPacked>(wout, win_in, S, wrel, we_rel, sw, nbw);
                 __syncthreads();
-                store_window(a.out, wout, S.T0, wb, we, lane);
+                store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
                 __syncthreads();
             }
         }
@@ -769,6 +807,17 @@ struct Desc {
         ts = 0;
 #pragma unroll
         for (int k = 0; k < 5; ++k) off[k] = len[k] = 0;
+    }
+    // views[k] for a runtime k: compare-and-select, so the arrays stay in registers (a dynamic
+    // index would put the whole descriptor in scratch memory)
+    __device__ __forceinline__ void set_view(uint32_t k, uint32_t o, uint32_t l) {
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+            if (j == k) {
+                off[j] = o;
+                len[j] = l;
+            }
+        }
     }
     __device__ __forceinline__ void fail(uint32_t st, uint32_t param) {
         clear();
@@ -903,8 +952,7 @@ __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& 
                 ++run_len;
             } else {
                 if (run_len >= 3 && nruns < 3) {
-                    d.off[nruns] = (uint32_t)(b + run_start);
-                    d.len[nruns] = (uint32_t)run_len;
+                    d.set_view(nruns, (uint32_t)(b + run_start), (uint32_t)run_len);
                     ++nruns;
                 }
                 run_len = 0;
@@ -912,8 +960,7 @@ __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& 
         }
     }
     if (nruns < 3 && run_len >= 3) {
-        d.off[nruns] = (uint32_t)(b + run_start);
-        d.len[nruns] = (uint32_t)run_len;
+        d.set_view(nruns, (uint32_t)(b + run_start), (uint32_t)run_len);
         ++nruns;
     }
     if (nruns < 1) d.flags |= SBE_FL_ID_DEFAULT;
@@ -995,10 +1042,15 @@ __device__ void dec_on_egress(const R_t& R, uint32_t len, Desc& d) {
         const uint64_t lim = len - 8;
         uint64_t pos = 8u + blk;
         bool ok = pos <= lim;
-        for (int f = 0; f < 3 && ok; ++f) {
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+            if (!ok) continue;
             const uint64_t L = R.u16(pos);
             if (L > 0) {
-                if (pos + 2 + L > lim) { ok = false; break; }
+                if (pos + 2 + L > lim) {
+                    ok = false;
+                    continue;
+                }
                 d.off[f] = (uint32_t)(pos + 2);
                 d.len[f] = (uint32_t)L;
                 pos += 2 + L;
