@@ -273,8 +273,8 @@ constexpr int32_t kEWIn = SBE_ENC_WIN + 256;    // staged input bytes per pass
 // reads are ds_read_b32 at immediate offsets from one base.  Output window: 256-byte rows
 // padded by 8 bytes, so the two lanes of each of 32 records (256 B apart) write banks
 // 2r + 32q + k: at most 2-way, which ds_write_b32 absorbs.
-constexpr int32_t kInSlack = 16;
-constexpr int32_t kRowPad = 8;
+constexpr int32_t kInSlack = 64;
+constexpr int32_t kRowPad = 16;
 constexpr int32_t kWoutBytes = kEW + (kEW / 256) * kRowPad;
 constexpr int32_t kWinBytes = kEWIn + 2 * kInSlack;
 
@@ -425,6 +425,7 @@ struct TileIn {  // raw per-lane loads of one tile
 
 struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from T0 / in_tile
     uint32_t rs, rec_out, ps, pe;  // this lane's record and its part [ps, pe) of it
+    uint32_t pe_rec;               // end of the record's composed bytes (clipped to the capacity)
     uint64_t in0;                  // packed: the record's first string byte
     uint32_t L[5];
     uint64_t ts;
@@ -504,6 +505,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t hi_rec = re < cap_rel ? re : cap_rel;
     S.ps = ps < re ? ps : re;
     S.pe = pe < hi_rec ? pe : hi_rec;
+    S.pe_rec = hi_rec;
     S.T0 = base_out;
     S.len = cap_rel;
     S.in_tile = reinterpret_cast<uintptr_t>(a.arena) + base_in;
@@ -628,9 +630,8 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
-        lds_cu32x2* p = reinterpret_cast<lds_cu32x2*>(wout + 16 * ch + (ch >> 4) * kRowPad);
-        const u32x2 a0 = p[0], a1 = p[1];
-        v[k] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+        const u32x4 a0 = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * ch + (ch >> 4) * kRowPad);
+        v[k] = make_uint4(a0.x, a0.y, a0.z, a0.w);
     }
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
@@ -648,12 +649,263 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
     }
 }
 
+// ---- packed mode: chunk / fixup / literal passes ---------------------------------------------
+// Lane l owns the kCpl 16-byte chunks [l*kCpl, (l+1)*kCpl) of the window (128 contiguous bytes).
+// A chunk's string bytes all belong to the record holding its first byte (string bytes start 26 B
+// into a record, past any 16-byte chunk that begins before it), and within a record string f sits
+// at output = staged input + sh0 + 2f.  So one pass computes every chunk from the "zone" (string
+// index) of its first byte with five LDS dword reads and four v_alignbyte; a second pass rewrites
+// the bytes after a string start that falls inside a chunk (<= 15 per string), and a third
+// writes the header and the u16 lengths.  Non-string bytes are don't-care until the third pass.
+constexpr int32_t kChunks = kEW / 16;
+constexpr int32_t kCpl = kChunks / kWave;        // chunks per lane
+constexpr int32_t kLaneBytes = 16 * kCpl;
+static_assert(kChunks % kWave == 0 && 256 % kLaneBytes == 0, "window shape");
+constexpr int32_t kRecEnt = 8;                   // dwords per record-table entry
+
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
+
+struct RecEnt {     // window-relative (bytes from the window start)
+    int32_t rw;     // record start
+    int32_t rend;   // end of its composed bytes (record end clipped to the capacity)
+    int32_t sh0;    // string 0: output position - staged-input position (staged records)
+    int32_t z[5];   // record-relative starts of strings 1..4, end of string 4 (| kNotStaged)
+};
+constexpr int32_t kNotStaged = 0x40000000;  // z[4] flag: strings not all in the staged window
+
+__device__ __forceinline__ RecEnt rec_load(lds_i32* rt, int32_t r) {
+    const i32x4 a = reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0];
+    const i32x4 b = reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1];
+    RecEnt E;
+    E.rw = a.x; E.rend = a.y; E.sh0 = a.z; E.z[0] = a.w;
+    E.z[1] = b.x; E.z[2] = b.y; E.z[3] = b.z; E.z[4] = b.w;
+    return E;
+}
+
+// the 16 bytes at staged-input position u (any alignment); the base is clamped into the array
+// (a clamped read only ever feeds don't-care bytes)
+__device__ __forceinline__ u32x4 chunk_lds(lds_cu8* inb, int32_t u, int32_t imax) {
+    int32_t i = u >> 2;
+    i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+    const uint32_t sh = (uint32_t)u & 3u;
+    lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    return v;
+}
+// the 16 bytes at absolute address a, dword reads clamped to [lo4, hi4] (the record's strings)
+__device__ __forceinline__ u32x4 chunk_glb(uint64_t a, uint64_t lo4, uint64_t hi4) {
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        uint64_t q = (a & ~3ull) + 4ull * k;
+        q = q < lo4 ? lo4 : (q > hi4 ? hi4 : q);
+        d[k] = gload32((uintptr_t)q);
+    }
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+    v.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+    v.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+    v.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+    return v;
+}
+
+// bytes [lo, hi) of the dword at window position d (4-aligned)
+__device__ __forceinline__ void put_clip(lds_u8* wout, int32_t d, uint32_t v, int32_t lo, int32_t hi) {
+    if (d >= lo && d + 4 <= hi) {
+        *reinterpret_cast<lds_u32*>(wout + wout_addr(d)) = v;
+    } else if (d + 4 > lo && d < hi) {
+        lds_u8* q = wout + wout_addr(d);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (d + k >= lo && d + k < hi) q[k] = (uint8_t)(v >> (8 * k));
+    }
+}
+
+// Record table, bucket table and per-record absolute string bases for one window; returns true
+// (wave-uniform) when some record of the window has strings outside the staged input.
+__device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t* sbase, const TileSt& S,
+                                             int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int lane) {
+    const int q = lane % kLpr, r = lane / kLpr;
+    bk[lane] = 0;
+    bool outside = false;
+    if (q == 0) {
+        const int32_t rw = (int32_t)S.rs - wrel;
+        const int32_t rend = (S.rec_out ? (int32_t)S.pe_rec : (int32_t)S.rs) - wrel;
+        const uint64_t s0 = S.in_tile + S.in0;                 // absolute address of string 0
+        const int64_t src0 = (int64_t)s0 - (int64_t)swb;       // its staged position
+        uint32_t nstr = 0;
+#pragma unroll
+        for (int f = 0; f < 5; ++f) nstr += S.L[f];
+        const bool staged = src0 >= 0 && src0 + (int64_t)nstr <= (int64_t)nb;
+        outside = S.rec_out && !staged && rend > (rw > 0 ? rw : 0) && (rw < wlen);
+        i32x4 a, b;
+        a.x = rw;
+        a.y = rend;
+        a.z = staged ? rw + 26 - (int32_t)src0 : 0;
+        int32_t z = 26;
+        z += (int32_t)S.L[0] + 2; a.w = z;
+        z += (int32_t)S.L[1] + 2; b.x = z;
+        z += (int32_t)S.L[2] + 2; b.y = z;
+        z += (int32_t)S.L[3] + 2; b.z = z;
+        b.w = (z + (int32_t)S.L[4]) | (staged ? 0 : kNotStaged);
+        reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0] = a;
+        reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = b;
+        sbase[r] = s0;
+        // buckets bb with bb*kLaneBytes inside [rw, rend) ∩ [0, wlen)
+        const int32_t s1 = rw > 0 ? rw : 0;
+        const int32_t e1 = rend < wlen ? rend : wlen;
+        if (S.rec_out && s1 < e1) {
+            for (int32_t bb = (s1 + kLaneBytes - 1) / kLaneBytes; bb * kLaneBytes < e1; ++bb) bk[bb] = r;
+        }
+    }
+    return __ballot(outside) != 0;
+}
+
+__device__ __forceinline__ int32_t zone_of(const RecEnt& E, int32_t X) {
+    return (X >= E.z[0]) + (X >= E.z[1]) + (X >= E.z[2]) + (X >= E.z[3]);
+}
+
+// kGlobal = false: every chunk from the staged input (chunks of not-staged records get don't-care
+// data); kGlobal = true: only the chunks of not-staged records, from HBM.
+template <bool kGlobal>
+__device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk,
+                                           const uint64_t* sbase, int32_t wlen, int32_t nb, int lane) {
+    const int32_t imax = (nb + kInSlack) / 4 - 5;
+    int32_t r = bk[lane];
+    RecEnt E = rec_load(rt, r);
+    lds_u8* const wl = wout + kLaneBytes * lane + (kLaneBytes * lane / 256) * kRowPad;  // 16-byte rows never split a lane
+#pragma unroll
+    for (int k = 0; k < kCpl; ++k) {
+        const int32_t p = kLaneBytes * lane + 16 * k;
+        if (p >= wlen) break;
+        while (p >= E.rend && r + 1 < kRpt) {
+            ++r;
+            E = rec_load(rt, r);
+        }
+        const int32_t X = p - E.rw;
+        const int32_t f = zone_of(E, X);
+        if (!kGlobal) {
+            const u32x4 v = chunk_lds(inb, p - E.sh0 - 2 * f, imax);
+            *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
+        } else if (E.z[4] & kNotStaged) {
+            const uint64_t s0 = sbase[r];
+            const uint32_t nstr = (uint32_t)((E.z[4] & ~kNotStaged) - 34);
+            const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - 26 - 2 * f), s0 & ~3ull,
+                                      (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
+            *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
+        }
+    }
+}
+
+// string starts 1..4 inside a chunk: bytes [z_f, min(chunk end, end of string f)) from zone f
+__device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, const uint64_t* sbase,
+                                           const TileSt& S, int32_t wlen, int32_t nb, int lane) {
+    const int q = lane % kLpr, r = lane / kLpr;
+    if (!S.rec_out) return;
+    const RecEnt E = rec_load(rt, r);
+    const bool staged = !(E.z[4] & kNotStaged);
+    const int32_t zend = E.z[4] & ~kNotStaged;
+    const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
+    const int32_t imax = (nb + kInSlack) / 4 - 5;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j % kLpr != q) continue;
+        const int f = j + 1;
+        const int32_t A = E.rw + E.z[j];
+        const int32_t Lf = (j + 1 < 4 ? E.z[j + 1] - 2 : zend) - E.z[j];  // length of string f
+        int32_t B = (A | 15) + 1;
+        if (A + Lf < B) B = A + Lf;
+        if (hi_all < B) B = hi_all;
+        const int32_t lo = A > 0 ? A : 0;
+        if ((A & 15) == 0 || lo >= B) continue;
+        const int32_t d0 = lo & ~3;
+        u32x4 v;
+        if (staged) {
+            v = chunk_lds(inb, d0 - E.sh0 - 2 * f, imax);
+        } else {
+            const uint64_t s0 = sbase[r];
+            const uint32_t nstr = (uint32_t)(zend - 34);
+            v = chunk_glb(s0 + (uint64_t)(int64_t)(d0 - E.rw - 26 - 2 * f), s0 & ~3ull,
+                          (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
+        }
+        put_clip(wout, d0, v.x, lo, B);
+        put_clip(wout, d0 + 4, v.y, lo, B);
+        put_clip(wout, d0 + 8, v.z, lo, B);
+        put_clip(wout, d0 + 12, v.w, lo, B);
+    }
+}
+
+// header {16,1,1,1}, timestamp, sequenceNumber 0 (TopicMessage.h:221-238, :362-437) and the five
+// u16 lengths (:515-1231), clipped to the window and the record's composed bytes
+__device__ __forceinline__ void literal_pass(lds_u8* wout, lds_i32* rt, const TileSt& S, int32_t wlen, int lane) {
+    const int q = lane % kLpr, r = lane / kLpr;
+    if (!S.rec_out) return;
+    const RecEnt E = rec_load(rt, r);
+    const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
+    const int32_t lo_all = E.rw > 0 ? E.rw : 0;
+    if (q == 0) {
+        const uint32_t H[6] = {SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16), SBE_TOPIC_SCHEMA_ID | (1u << 16),
+                               (uint32_t)S.ts, (uint32_t)(S.ts >> 32), 0u, 0u};
+        const int32_t a = E.rw & 3, d0 = E.rw - a;
+        const int32_t hi = E.rw + 24 < hi_all ? E.rw + 24 : hi_all;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const uint32_t cur = j < 6 ? H[j] : 0u, prv = j > 0 ? H[j - 1] : 0u;
+            const uint32_t v = a ? __builtin_amdgcn_alignbyte(cur, prv, 4u - (uint32_t)a) : cur;
+            put_clip(wout, d0 + 4 * j, v, lo_all, hi);
+        }
+    }
+    if (q == (kLpr > 1 ? 1 : 0)) {
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+            const int32_t P = E.rw + (f == 0 ? 24 : E.z[f - 1] - 2);
+            const uint32_t L = S.L[f] & 0xffffu;
+            const int32_t lo = P > lo_all ? P : lo_all;
+            const int32_t hi = P + 2 < hi_all ? P + 2 : hi_all;
+            if (lo >= hi) continue;
+            if (lo == P && hi == P + 2 && (P & 1) == 0) {
+                *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wout + wout_addr(P)) = (uint16_t)L;
+            } else {
+                if (P >= lo && P < hi) wout[wout_addr(P)] = (uint8_t)L;
+                if (P + 1 >= lo && P + 1 < hi) wout[wout_addr(P + 1)] = (uint8_t)(L >> 8);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void pack_window(lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk, uint64_t* sbase,
+                                            const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
+                                            int lane) {
+    const bool outside = build_tables(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
+    __syncthreads();
+#ifndef SBE_ABL_NO_COMPOSE
+    chunk_pass<false>(wout, inb, rt, bk, sbase, wlen, nb, lane);
+    if (outside) chunk_pass<true>(wout, inb, rt, bk, sbase, wlen, nb, lane);
+    __syncthreads();
+    fixup_pass(wout, inb, rt, sbase, S, wlen, nb, lane);
+    literal_pass(wout, rt, S, wlen, lane);
+#endif
+}
+
 template <bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
+    __shared__ __attribute__((aligned(16))) int32_t rt_arr[kPacked ? kRpt * kRecEnt : 4];
+    __shared__ int32_t bk_arr[kPacked ? kWave : 1];
+    __shared__ uint64_t sbase[kPacked ? kRpt : 1];
     lds_u8* const wout = (lds_u8*)wout_arr;
     lds_u8* const win_in = (lds_u8*)win_raw + kInSlack;
+    lds_i32* const rt = (lds_i32*)rt_arr;
+    lds_i32* const bk = (lds_i32*)bk_arr;
     const int lane = threadIdx.x;
     const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
     const uint64_t G = gridDim.x;
@@ -679,7 +931,6 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
         const int32_t cur_nb = nb;
         const bool cur_fast = fast;
         if (cur_fast) stage_write(win_in, cur_nb, lane, I);
-        __syncthreads();
         // next tile: prepare it and put its input loads in flight; prefetch the one after
         const bool have_next = tn < ntiles;
         TileSt Sn;
@@ -694,18 +945,21 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
             if (t2 < ntiles) x = tile_load<kPacked>(a, t2, lane);
         }
         // current tile: compose + store, one window (fast) or window by window
+        const int32_t wrel0 = -(int32_t)(S.T0 & 15);
         if (cur_fast) {
-            const int32_t wrel = -(int32_t)(S.T0 & 15);
-#ifndef SBE_ABL_NO_COMPOSE
-            compose<kPacked>(wout, win_in, S, wrel, (int32_t)S.len, cur_swb, cur_nb);
-#endif
+            if (kPacked) {
+                pack_window(wout, win_in, rt, bk, sbase, S, wrel0, (int32_t)S.len - wrel0, cur_swb, cur_nb, lane);
+            } else {
+                __syncthreads();
+                compose<false>(wout, win_in, S, wrel0, (int32_t)S.len, cur_swb, cur_nb);
+            }
             __syncthreads();
 #ifndef SBE_ABL_NO_STORE
             store_window(a.out, wout, S.T0, S.T0 & ~15ull, S.T0 + S.len, lane);
 #endif
             __syncthreads();
         } else {
-            for (int32_t wrel = -(int32_t)(S.T0 & 15); wrel < (int32_t)S.len; wrel += kEW) {
+            for (int32_t wrel = wrel0; wrel < (int32_t)S.len; wrel += kEW) {
                 const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
                 uintptr_t sw = 0;
                 int32_t nbw = 0;
@@ -725,9 +979,13 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
                             if ((int32_t)(16 * ch) < nbw) lds_store16(win_in + 16 * ch, J[k]);
                         }
                     }
-                    __syncthreads();
                 }
-                compose<kPacked>(wout, win_in, S, wrel, we_rel, sw, nbw);
+                if (kPacked) {
+                    pack_window(wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
+                } else {
+                    __syncthreads();
+                    compose<false>(wout, win_in, S, wrel, we_rel, sw, nbw);
+                }
                 __syncthreads();
                 store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
                 __syncthreads();
@@ -1214,6 +1472,39 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
     return tiles < cached ? tiles : cached;
 }
 
+// Optional launch profiling: HIP events recorded on the launch stream around the pack kernel
+// and the decode kernel of every call, kept in a ring per kernel (read by sbe_profile_read).
+struct ProfRing {
+    static constexpr int kCap = 256;
+    hipEvent_t ev[kCap][2];
+    int head = 0, count = 0;
+    bool ready = false;
+};
+thread_local bool g_prof_on = false;
+thread_local ProfRing g_prof[2];
+
+hipEvent_t prof_begin(int which, hipStream_t s) {
+    if (!g_prof_on) return nullptr;
+    ProfRing& R = g_prof[which];
+    if (!R.ready) {
+        for (int i = 0; i < ProfRing::kCap; ++i)
+            for (int j = 0; j < 2; ++j)
+                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return nullptr;
+        R.ready = true;
+    }
+    hipEvent_t b = R.ev[R.head][0];
+    (void)hipEventRecord(b, s);
+    return b;
+}
+void prof_end(int which, hipStream_t s) {
+    if (!g_prof_on) return;
+    ProfRing& R = g_prof[which];
+    if (!R.ready) return;
+    (void)hipEventRecord(R.ev[R.head][1], s);
+    R.head = (R.head + 1) % ProfRing::kCap;
+    if (R.count < ProfRing::kCap) ++R.count;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1277,7 +1568,9 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
         const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<P, T>), tiles);   \
         hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)blocks), dim3(kBlk), 0, s, a);        \
         hipLaunchKernelGGL(sbe_enc_scan, dim3(1), dim3(kScanThreads), 0, s, a.bsum, blocks);          \
+        prof_begin(0, s);                                                                             \
         hipLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, a);        \
+        prof_end(0, s);                                                                               \
     } while (0)
     if (packed && !trunc) SBE_ENC_LAUNCH(true, false);
     else if (packed && trunc) SBE_ENC_LAUNCH(true, true);
@@ -1303,11 +1596,33 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     DecArgs a{in, rec_off, n, out->status, out->flags, out->hdr, out->ts, out->view_off, out->view_len};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((uint32_t)tiles), block(kWave);
+    prof_begin(1, s);
     if (mode == SBE_DEC_ON_EGRESS)
         hipLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_ON_EGRESS>), grid, block, 0, s, a);
     else
         hipLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, a);
+    prof_end(1, s);
     return record_hip(hipGetLastError());
+}
+
+int sbe_profile_enable(int on) {
+    g_prof_on = on != 0;
+    for (auto& R : g_prof) R.head = R.count = 0;
+    return SBE_OK;
+}
+
+int sbe_profile_read(int kernel, float* ms, int max) {
+    if (kernel < 0 || kernel > 1 || (!ms && max > 0)) return SBE_EINVAL;
+    ProfRing& R = g_prof[kernel];
+    const int n = R.count < max ? R.count : max;
+    const int first = (R.head - R.count + ProfRing::kCap) % ProfRing::kCap;
+    for (int i = 0; i < n; ++i) {
+        const int k = (first + R.count - n + i) % ProfRing::kCap;
+        const hipError_t e = hipEventElapsedTime(&ms[i], R.ev[k][0], R.ev[k][1]);
+        if (e != hipSuccess) return record_hip(e);
+    }
+    R.head = R.count = 0;
+    return n;
 }
 
 }  // extern "C"

@@ -75,6 +75,10 @@ def _load():
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.POINTER(_Decoded), ctypes.c_void_p]
+    lib.sbe_profile_enable.restype = ctypes.c_int
+    lib.sbe_profile_enable.argtypes = [ctypes.c_int]
+    lib.sbe_profile_read.restype = ctypes.c_int
+    lib.sbe_profile_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     if lib.sbe_abi_version() != ABI_VERSION:
         raise SbeError("libsbecodec.so ABI version mismatch")
     return lib
@@ -115,6 +119,23 @@ def _dev(t, dtype, name):
 def require_device():
     if not torch.cuda.is_available() or lib().sbe_device_ready() != 1:
         raise SbeError("no gfx950 device visible: the SBE codec runs only on MI355X")
+
+
+PROF_PACK, PROF_DECODE = 0, 1
+
+
+def profile_enable(on: bool = True):
+    """Record HIP events around the pack / decode kernel of every call (sbecodec.h profiling)."""
+    _check(lib().sbe_profile_enable(1 if on else 0), "sbe_profile_enable")
+
+
+def profile_read(kernel: int, max_n: int = 256) -> list:
+    """Elapsed ms of the recorded launches of `kernel` (oldest first); synchronise first."""
+    buf = (ctypes.c_float * max_n)()
+    n = lib().sbe_profile_read(kernel, buf, max_n)
+    if n < 0:
+        _check(n, "sbe_profile_read")
+    return [float(buf[i]) for i in range(n)]
 
 
 def output_bound(n: int, string_bytes: int, flags: int = 0) -> int:

@@ -34,7 +34,7 @@ import sbecodec  # noqa: E402
 METRIC = "SBE records encoded+decoded/sec (device-resident), 256 B Order msgs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # algorithmic bytes per 256-B record
-ENC_BYTES = 222 + 20 + 8 + 256 + 8 + 1  # strings + lengths + ts read; record + out_off + status written
+ENC_BYTES = 222 + 20 + 8 + 256 + 8 + 1  # pack kernel: strings + lengths + ts read; record + out_off + status written
 DEC_BYTES = 256 + 8 + 2 + 8 + 8 + 40    # record + rec_off read; status,flags + hdr + ts + 5 views written
 
 
@@ -144,6 +144,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    sbecodec.profile_enable(True)  # events around the pack / decode kernels on the launch stream
     if args.verify:
         torch.cuda.synchronize()
         import sbe_testlib as T
@@ -162,6 +163,9 @@ def main():
 
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_enc]))
     dec_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_dec]))
+    pack_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_PACK)))
+    deck_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_DECODE)))
+    sbecodec.profile_enable(False)
     total = n * world * args.steps
     value = total / el
 
@@ -172,10 +176,14 @@ def main():
     if rank == 0:
         enc_gbs = n * ENC_BYTES / (enc_ms * 1e-3) / 1e9
         dec_gbs = n * DEC_BYTES / (dec_ms * 1e-3) / 1e9
-        if enc_ms >= dec_ms:
-            dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, ms=enc_ms, gbs=enc_gbs)
+        pack_gbs = n * ENC_BYTES / (pack_ms * 1e-3) / 1e9
+        deck_gbs = n * DEC_BYTES / (deck_ms * 1e-3) / 1e9
+        if pack_ms >= deck_ms:
+            dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, ms=pack_ms, gbs=pack_gbs)
         else:
-            dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES, ms=dec_ms, gbs=dec_gbs)
+            dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES, ms=deck_ms,
+                       gbs=deck_gbs)
+        traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(min(n, 200_000), args.cpu_seconds, args.cpu_threads)
@@ -187,9 +195,11 @@ def main():
                        "encode": "wire-correct TopicMessage, packed SoA input",
                        "decode": "parse_message descriptors (views)", "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": dom["gbs"] / HBM_PEAK_GBS, "traffic": None, "kernel": dom["kernel"],
+                         "frac": dom["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
                          "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"]},
             "kernels": {"encode_ms": enc_ms, "encode_gbs": enc_gbs, "decode_ms": dec_ms, "decode_gbs": dec_gbs,
+                        "pack_ms": pack_ms, "pack_gbs": pack_gbs, "decode_kernel_ms": deck_ms,
+                        "decode_kernel_gbs": deck_gbs,
                         "roundtrip_gbs": n * (ENC_BYTES + DEC_BYTES) / ((enc_ms + dec_ms) * 1e-3) / 1e9},
             "cpu_baseline": cpu,
         }
@@ -199,6 +209,18 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def measured_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_counters.sh →
+    profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), scaled from the
+    records per launch it was measured at; None when no summary covers the kernel."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        d = json.load(open(path))[kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    return d["bytes_per_launch"] * n / d["records"]
 
 
 def time_gather(out, out_off, n, world, rank, dev):

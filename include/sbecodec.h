@@ -168,6 +168,16 @@ typedef struct sbe_decoded {
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream);
 
+/* ================================== profiling ================================== */
+/* Optional (off by default; thread-local): when enabled, each sbe_encode_topic_batch /
+ * sbe_decode_batch call records a pair of HIP events on its stream around its main kernel
+ * (kernel 0 = the encode pack kernel, 1 = the decode kernel), kept in a ring of the last 256.
+ * sbe_profile_read copies the elapsed milliseconds of up to `max` most recent launches (oldest
+ * first) into ms[], clears the ring and returns the count; the caller synchronises the streams
+ * first.  Used by bench.py to time the dominant kernel inside its timed region. */
+int sbe_profile_enable(int on);
+int sbe_profile_read(int kernel, float* ms, int max);
+
 /* ===================================== misc ===================================== */
 int sbe_abi_version(void);
 /* 1 if a gfx950 device is visible to HIP, 0 if not, <0 on HIP error. */

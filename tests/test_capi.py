@@ -60,3 +60,15 @@ def test_invalid_arguments_are_rejected_before_any_launch(lib):
     assert lib.sbe_decode_batch(None, None, 5, 7, None, None) == -1      # unknown mode
     assert lib.sbe_decode_batch(None, None, 5, 0, None, None) == -1      # null buffers
     assert lib.sbe_decode_batch(None, None, 0, 0, None, None) == 0       # empty batch: nothing to do
+
+
+def test_profiling_ring_without_launches(lib):
+    lib.sbe_profile_enable.restype = ctypes.c_int
+    lib.sbe_profile_enable.argtypes = [ctypes.c_int]
+    lib.sbe_profile_read.restype = ctypes.c_int
+    lib.sbe_profile_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    buf = (ctypes.c_float * 4)()
+    assert lib.sbe_profile_enable(1) == 0
+    assert lib.sbe_profile_read(0, buf, 4) == 0       # nothing launched yet
+    assert lib.sbe_profile_read(2, buf, 4) == -1      # unknown kernel
+    assert lib.sbe_profile_enable(0) == 0
