@@ -137,7 +137,7 @@ struct EncArgs {
     uint64_t cap;
     uint64_t* out_off;
     uint8_t* status;
-    uint64_t* tsum;  // [tiles][2]   output / input bytes per tile
+    uint64_t* tsum;  // [tiles][2]   output / input bytes before the tile within its block
     uint64_t* bsum;  // [blocks][2]  per block; K2 turns it into exclusive prefixes
 };
 
@@ -175,39 +175,38 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
 
 template <bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kBlk) void sbe_enc_sums(EncArgs a) {
-    __shared__ uint64_t red[2][kBlk / kWave];
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    __shared__ uint64_t tl[2][kTilesPerBlk];
+    const int lane = threadIdx.x & (kWave - 1);
     const uint64_t r = (uint64_t)blockIdx.x * kBlk + threadIdx.x;
     uint32_t L[5], ob, ib;
     uint8_t st;
     rec_sizes<kTrunc>(a, r, L, ob, ib, st);
-    if (!kPacked) ib = 0;
-    // per pack tile (kRpt records = kRpt consecutive lanes): segmented sums via shuffles
-    uint32_t to = ob, ti = ib;
+    // per pack tile (kRpt consecutive lanes): segmented sums via shuffles (input side in 64 bits:
+    // E109 records may carry up to 5 x 4 GiB of strings)
+    uint32_t to = ob;
+    uint64_t ti = kPacked ? ib : 0u;
 #pragma unroll
     for (int d = 1; d < kRpt; d <<= 1) {
         to += __shfl_xor(to, d, kWave);
-        ti += __shfl_xor(ti, d, kWave);
+        if (kPacked) ti += __shfl_xor(ti, d, kWave);
     }
-    const uint64_t tile = r / kRpt;
-    if ((lane & (kRpt - 1)) == 0 && r < a.n) {
-        a.tsum[2 * tile] = to;
-        a.tsum[2 * tile + 1] = ti;
-    }
-    const uint64_t so = wave_sum64(ob), si = kPacked ? wave_sum64(ib) : 0ull;
-    if (lane == 0) {
-        red[0][w] = so;
-        red[1][w] = si;
+    if ((lane & (kRpt - 1)) == 0) {
+        tl[0][threadIdx.x / kRpt] = to;
+        tl[1][threadIdx.x / kRpt] = ti;
     }
     __syncthreads();
+    // tile prefixes within the block, and the block's totals (K2 scans them)
     if (threadIdx.x == 0) {
-        uint64_t bo = 0, bi = 0;
-        for (int j = 0; j < kBlk / kWave; ++j) {
-            bo += red[0][j];
-            bi += red[1][j];
+        uint64_t po = 0, pi = 0;
+        for (int j = 0; j < kTilesPerBlk; ++j) {
+            const uint64_t tile = (uint64_t)blockIdx.x * kTilesPerBlk + j;
+            a.tsum[2 * tile] = po;
+            a.tsum[2 * tile + 1] = pi;
+            po += tl[0][j];
+            pi += tl[1][j];
         }
-        a.bsum[2 * blockIdx.x] = bo;
-        a.bsum[2 * blockIdx.x + 1] = bi;
+        a.bsum[2 * blockIdx.x] = po;
+        a.bsum[2 * blockIdx.x + 1] = pi;
     }
 }
 
@@ -419,8 +418,7 @@ constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging r
 struct TileIn {  // raw per-lane loads of one tile
     uint32_t L[5];
     uint64_t ts;
-    uint64_t po, pi;  // one preceding tile sum of the block (lane-indexed)
-    uint64_t bo, bi;  // block prefix
+    uint64_t base_out, base_in;  // tile start in the output / packed input (uniform)
 };
 
 struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from T0 / in_tile
@@ -443,14 +441,9 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
 #pragma unroll
     for (int f = 0; f < 5; ++f) x.L[f] = r < a.n ? a.str_len[5 * r + f] : 0u;
     x.ts = r < a.n ? a.timestamp[r] : 0ull;
-    const uint64_t blk = tile / kTilesPerBlk, tib = tile - blk * kTilesPerBlk;
-    x.po = x.pi = 0;
-    if ((uint64_t)lane < tib) {
-        x.po = a.tsum[2 * (blk * kTilesPerBlk + lane)];
-        if (kPacked) x.pi = a.tsum[2 * (blk * kTilesPerBlk + lane) + 1];
-    }
-    x.bo = a.bsum[2 * blk];
-    x.bi = kPacked ? a.bsum[2 * blk + 1] : 0ull;
+    const uint64_t blk = tile / kTilesPerBlk;  // uniform: scalar loads
+    x.base_out = a.bsum[2 * blk] + a.tsum[2 * tile];
+    x.base_in = kPacked ? a.bsum[2 * blk + 1] + a.tsum[2 * tile + 1] : 0ull;
     return x;
 }
 
@@ -473,19 +466,28 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
-    const uint64_t base_out = uniform64(x.bo + wave_sum64(x.po));
-    const uint64_t base_in = kPacked ? uniform64(x.bi + wave_sum64(x.pi)) : 0ull;
+    const uint64_t base_out = uniform64(x.base_out);
+    const uint64_t base_in = kPacked ? uniform64(x.base_in) : 0ull;
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
-    const uint64_t lo_in = q == 0 ? rec_in : 0ull;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
     const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
     S.rs = __shfl(inc_out - lo_out, lead, kWave);
     S.rec_out = rec_out;
     if (kPacked) {
-        const uint64_t inc_in = wave_incl_scan64(lo_in, lane);
-        const uint64_t agg_in = uniform64(__shfl(inc_in, kWave - 1, kWave));
-        S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
-        S.in0 = __shfl(inc_in - lo_in, lead, kWave);
+        // every record of the tile encodable: input offsets follow the output ones (34 B apart
+        // per record); otherwise (E109 / past the end) a 64-bit scan of the input sizes
+        if (__ballot(!(valid && st == SBE_ENC_OK)) == 0) {
+            const uint32_t ovh0 = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+            S.in0 = S.rs - ovh0 * (uint32_t)(lane / kLpr);
+            const uint64_t agg_in = agg_out - (uint64_t)ovh0 * kRpt;
+            S.agg_in = (uint32_t)agg_in;
+        } else {
+            const uint64_t lo_in = q == 0 ? rec_in : 0ull;
+            const uint64_t inc_in = wave_incl_scan64(lo_in, lane);
+            const uint64_t agg_in = uniform64(__shfl(inc_in, kWave - 1, kWave));
+            S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
+            S.in0 = __shfl(inc_in - lo_in, lead, kWave);
+        }
     } else {
         S.agg_in = 0;
         S.in0 = 0;
@@ -540,10 +542,16 @@ __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int l
 }
 
 __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int lane, uint4 (&I)[kStageRegs]) {
+    g_u32x4* const base = reinterpret_cast<g_u32x4*>(swb);  // uniform base + 32-bit lane offsets
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        I[k] = (int32_t)(16 * ch) < nbytes ? gload128(swb + 16u * ch) : make_uint4(0, 0, 0, 0);
+        if ((int32_t)(16 * ch) < nbytes) {
+            const u32x4 v = base[ch];
+            I[k] = make_uint4(v.x, v.y, v.z, v.w);
+        } else {
+            I[k] = make_uint4(0, 0, 0, 0);
+        }
     }
 }
 
@@ -626,6 +634,9 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
     constexpr int kIt = kEW / 16 / kWave;
     const uint64_t lo = wb > T0 ? wb : T0;
     const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
+    const uint32_t c_lo = (uint32_t)((lo - wb + 15) >> 4);  // chunks [c_lo, c_hi) lie inside [lo, we)
+    const uint32_t c_hi = (uint32_t)((we - wb) >> 4);
+    uint4* const ob = reinterpret_cast<uint4*>(out + wb);   // uniform base + 32-bit lane offsets
     uint4 v[kIt];
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
@@ -637,10 +648,10 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
         if (ch >= nch) continue;
-        const uint64_t g = wb + 16ull * ch;
-        if (g >= lo && g + 16 <= we) {
-            *reinterpret_cast<uint4*>(out + g) = v[k];
+        if (ch >= c_lo && ch < c_hi) {
+            ob[ch] = v[k];
         } else {
+            const uint64_t g = wb + 16ull * ch;
             const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
             for (uint32_t j = 0; j < 16; ++j)
@@ -671,16 +682,29 @@ struct RecEnt {     // window-relative (bytes from the window start)
     int32_t rw;     // record start
     int32_t rend;   // end of its composed bytes (record end clipped to the capacity)
     int32_t sh0;    // string 0: output position - staged-input position (staged records)
-    int32_t z[5];   // record-relative starts of strings 1..4, end of string 4 (| kNotStaged)
+    int32_t z1, z2, z3, z4;  // record-relative starts of strings 1..4
+    int32_t z5;              // end of string 4 (| kNotStaged); scalars, so selects never become a
+                             // dynamically indexed (scratch) array
 };
 constexpr int32_t kNotStaged = 0x40000000;  // z[4] flag: strings not all in the staged window
+
+// z_{j+1} for a compile-time j (unrolled loops)
+__device__ __forceinline__ int32_t zat(const RecEnt& E, int j) {
+    switch (j) {
+        case 0: return E.z1;
+        case 1: return E.z2;
+        case 2: return E.z3;
+        case 3: return E.z4;
+        default: return E.z5;
+    }
+}
 
 __device__ __forceinline__ RecEnt rec_load(lds_i32* rt, int32_t r) {
     const i32x4 a = reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0];
     const i32x4 b = reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1];
     RecEnt E;
-    E.rw = a.x; E.rend = a.y; E.sh0 = a.z; E.z[0] = a.w;
-    E.z[1] = b.x; E.z[2] = b.y; E.z[3] = b.z; E.z[4] = b.w;
+    E.rw = a.x; E.rend = a.y; E.sh0 = a.z; E.z1 = a.w;
+    E.z2 = b.x; E.z3 = b.y; E.z4 = b.z; E.z5 = b.w;
     return E;
 }
 
@@ -770,7 +794,7 @@ __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t*
 }
 
 __device__ __forceinline__ int32_t zone_of(const RecEnt& E, int32_t X) {
-    return (X >= E.z[0]) + (X >= E.z[1]) + (X >= E.z[2]) + (X >= E.z[3]);
+    return (X >= E.z1) + (X >= E.z2) + (X >= E.z3) + (X >= E.z4);
 }
 
 // kGlobal = false: every chunk from the staged input (chunks of not-staged records get don't-care
@@ -795,9 +819,9 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
         if (!kGlobal) {
             const u32x4 v = chunk_lds(inb, p - E.sh0 - 2 * f, imax);
             *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
-        } else if (E.z[4] & kNotStaged) {
+        } else if (E.z5 & kNotStaged) {
             const uint64_t s0 = sbase[r];
-            const uint32_t nstr = (uint32_t)((E.z[4] & ~kNotStaged) - 34);
+            const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - 34);
             const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - 26 - 2 * f), s0 & ~3ull,
                                       (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
             *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
@@ -811,16 +835,16 @@ __device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     const int q = lane % kLpr, r = lane / kLpr;
     if (!S.rec_out) return;
     const RecEnt E = rec_load(rt, r);
-    const bool staged = !(E.z[4] & kNotStaged);
-    const int32_t zend = E.z[4] & ~kNotStaged;
+    const bool staged = !(E.z5 & kNotStaged);
+    const int32_t zend = E.z5 & ~kNotStaged;
     const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
     const int32_t imax = (nb + kInSlack) / 4 - 5;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         if (j % kLpr != q) continue;
         const int f = j + 1;
-        const int32_t A = E.rw + E.z[j];
-        const int32_t Lf = (j + 1 < 4 ? E.z[j + 1] - 2 : zend) - E.z[j];  // length of string f
+        const int32_t A = E.rw + zat(E, j);
+        const int32_t Lf = (j + 1 < 4 ? zat(E, j + 1) - 2 : zend) - zat(E, j);  // length of string f
         int32_t B = (A | 15) + 1;
         if (A + Lf < B) B = A + Lf;
         if (hi_all < B) B = hi_all;
@@ -866,7 +890,7 @@ __device__ __forceinline__ void literal_pass(lds_u8* wout, lds_i32* rt, const Ti
     if (q == (kLpr > 1 ? 1 : 0)) {
 #pragma unroll
         for (int f = 0; f < 5; ++f) {
-            const int32_t P = E.rw + (f == 0 ? 24 : E.z[f - 1] - 2);
+            const int32_t P = E.rw + (f == 0 ? 24 : zat(E, f - 1) - 2);
             const uint32_t L = S.L[f] & 0xffffu;
             const int32_t lo = P > lo_all ? P : lo_all;
             const int32_t hi = P + 2 < hi_all ? P + 2 : hi_all;
@@ -886,11 +910,15 @@ __device__ __forceinline__ void pack_window(lds_u8* wout, lds_u8* inb, lds_i32* 
                                             int lane) {
     const bool outside = build_tables(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
     __syncthreads();
-#ifndef SBE_ABL_NO_COMPOSE
+#ifndef SBE_ABL_NO_CHUNK
     chunk_pass<false>(wout, inb, rt, bk, sbase, wlen, nb, lane);
     if (outside) chunk_pass<true>(wout, inb, rt, bk, sbase, wlen, nb, lane);
+#endif
     __syncthreads();
+#ifndef SBE_ABL_NO_FIXUP
     fixup_pass(wout, inb, rt, sbase, S, wlen, nb, lane);
+#endif
+#ifndef SBE_ABL_NO_LITERAL
     literal_pass(wout, rt, S, wlen, lane);
 #endif
 }
