@@ -139,7 +139,9 @@ struct EncArgs {
     uint8_t* status;
     uint64_t* tsum;  // [tiles][2]   output / input bytes before the tile within its block
     uint64_t* bsum;  // [blocks][2]  per block; K2 turns it into exclusive prefixes
+    uint8_t* sink;   // kSinkBytes of workspace: target of the pack kernel's don't-care stores
 };
+constexpr int kSinkBytes = 16 * 64;
 
 // Sizes of record r: output bytes (0 on E109) and packed-input bytes (its strings, always).
 template <bool kTrunc>
@@ -407,6 +409,11 @@ __device__ __noinline__ Writer str_global(Writer W, uintptr_t sa, int32_t m) {
     return W;
 }
 
+// K3 workgroups are one wave, whose LDS accesses execute in issue order: a phase change needs only
+// a compiler barrier.  (__syncthreads() would also wait on vmcnt(0), draining the next tile's
+// prefetch loads and this tile's stores at every phase.)
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
+
 // ---- K3: persistent, software-pipelined pack kernel ---------------------------------------
 // One wave per workgroup loops over tiles t = blockIdx.x, += gridDim.x.  While it composes tile
 // t it already holds tile t+G's staged-input loads in flight (registers) and tile t+2G's lengths,
@@ -418,7 +425,9 @@ constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging r
 struct TileIn {  // raw per-lane loads of one tile
     uint32_t L[5];
     uint64_t ts;
-    uint64_t base_out, base_in;  // tile start in the output / packed input (uniform)
+    // tile start = block prefix + tile prefix (output / packed input), added in tile_prepare: an
+    // add here would wait on these loads, and vmcnt retires in order, so on the prefetch too
+    uint64_t bo, to, bi, ti;
 };
 
 struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from T0 / in_tile
@@ -437,13 +446,18 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
 template <bool kPacked>
 __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane) {
     TileIn x;
-    const uint64_t r = tile * kRpt + lane / kLpr;
+    // unconditional loads at a clamped index: a select on the loaded value here would make the
+    // compiler wait for it (tile_prepare applies r < n)
+    uint64_t r = tile * kRpt + lane / kLpr;
+    r = r < a.n ? r : a.n - 1;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) x.L[f] = r < a.n ? a.str_len[5 * r + f] : 0u;
-    x.ts = r < a.n ? a.timestamp[r] : 0ull;
+    for (int f = 0; f < 5; ++f) x.L[f] = a.str_len[5 * r + f];
+    x.ts = a.timestamp[r];
     const uint64_t blk = tile / kTilesPerBlk;  // uniform: scalar loads
-    x.base_out = a.bsum[2 * blk] + a.tsum[2 * tile];
-    x.base_in = kPacked ? a.bsum[2 * blk + 1] + a.tsum[2 * tile + 1] : 0ull;
+    x.bo = a.bsum[2 * blk];
+    x.to = a.tsum[2 * tile];
+    x.bi = kPacked ? a.bsum[2 * blk + 1] : 0ull;
+    x.ti = kPacked ? a.tsum[2 * tile + 1] : 0ull;
     return x;
 }
 
@@ -457,17 +471,17 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     uint8_t st = SBE_ENC_OK;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-        S.L[f] = x.L[f];
-        sum += x.L[f];
+        S.L[f] = valid ? x.L[f] : 0u;
+        sum += S.L[f];
     }
 #pragma unroll
     for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
-        if (x.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
+        if (S.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
     const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
-    const uint64_t base_out = uniform64(x.base_out);
-    const uint64_t base_in = kPacked ? uniform64(x.base_in) : 0ull;
+    const uint64_t base_out = uniform64(x.bo + x.to);
+    const uint64_t base_in = kPacked ? uniform64(x.bi + x.ti) : 0ull;
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
     const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
@@ -492,7 +506,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
         S.agg_in = 0;
         S.in0 = 0;
     }
-    S.ts = x.ts ? x.ts : a.ts_default;
+    S.ts = (valid && x.ts) ? x.ts : a.ts_default;
     const uint32_t re = S.rs + rec_out;
     const uint64_t cap_rel64 = a.cap > base_out ? a.cap - base_out : 0ull;
     const uint32_t cap_rel = cap_rel64 < (uint64_t)agg_out ? (uint32_t)cap_rel64 : agg_out;
@@ -541,25 +555,28 @@ __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int l
     nbytes = (int32_t)(swe - swb);
 }
 
+// Always kStageRegs loads (all lanes, offsets clamped into [swb, swb + nbytes); swb must be
+// readable for 16 bytes when nbytes == 0): the loop body's vector-memory operations are then
+// straight-line, so the compiler's vmcnt waits count them exactly instead of draining all.
 __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int lane, uint4 (&I)[kStageRegs]) {
     g_u32x4* const base = reinterpret_cast<g_u32x4*>(swb);  // uniform base + 32-bit lane offsets
+    const uint32_t last = nbytes >= 16 ? (uint32_t)(nbytes - 16) >> 4 : 0u;
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        if ((int32_t)(16 * ch) < nbytes) {
-            const u32x4 v = base[ch];
-            I[k] = make_uint4(v.x, v.y, v.z, v.w);
-        } else {
-            I[k] = make_uint4(0, 0, 0, 0);
-        }
+        const u32x4 v = base[ch < last ? ch : last];
+        I[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
 
+// The staged chunks into LDS, unconditionally like stage_issue (lanes past the end rewrite the
+// last chunk with its own bytes), so every path consumes the staging registers.
 __device__ __forceinline__ void stage_write(lds_u8* inb, int32_t nbytes, int lane, const uint4 (&I)[kStageRegs]) {
+    const uint32_t last = nbytes >= 16 ? (uint32_t)(nbytes - 16) >> 4 : 0u;
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        if ((int32_t)(16 * ch) < nbytes) lds_store16(inb + 16 * ch, I[k]);
+        lds_store16(inb + 16 * (ch < last ? ch : last), I[k]);
     }
 }
 
@@ -629,8 +646,8 @@ __device__ __forceinline__ void compose(lds_u8* wout, lds_cu8* inb, const TileSt
 }
 
 // window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte
-__device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64_t T0, uint64_t wb, uint64_t we,
-                                             int lane) {
+__device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu8* wout, uint64_t T0, uint64_t wb,
+                                             uint64_t we, int lane) {
     constexpr int kIt = kEW / 16 / kWave;
     const uint64_t lo = wb > T0 ? wb : T0;
     const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
@@ -644,19 +661,23 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
         const u32x4 a0 = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * ch + (ch >> 4) * kRowPad);
         v[k] = make_uint4(a0.x, a0.y, a0.z, a0.w);
     }
+    // kIt unconditional 16-byte stores (chunks not wholly inside [lo, we) go to the sink)
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
-        if (ch >= nch) continue;
-        if (ch >= c_lo && ch < c_hi) {
-            ob[ch] = v[k];
-        } else {
-            const uint64_t g = wb + 16ull * ch;
-            const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        const bool full = ch >= c_lo && ch < c_hi;
+        uint4* dst = full ? ob + ch : reinterpret_cast<uint4*>(sink) + lane;
+        *dst = v[k];
+    }
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (g + j >= lo && g + j < we) out[g + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
-        }
+    for (int k = 0; k < kIt; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        if (ch >= nch || (ch >= c_lo && ch < c_hi)) continue;
+        const uint64_t g = wb + 16ull * ch;
+        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+            if (g + j >= lo && g + j < we) out[g + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
     }
 }
 
@@ -797,16 +818,59 @@ __device__ __forceinline__ int32_t zone_of(const RecEnt& E, int32_t X) {
     return (X >= E.z1) + (X >= E.z2) + (X >= E.z3) + (X >= E.z4);
 }
 
-// kGlobal = false: every chunk from the staged input (chunks of not-staged records get don't-care
-// data); kGlobal = true: only the chunks of not-staged records, from HBM.
-template <bool kGlobal>
-__device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk,
-                                           const uint64_t* sbase, int32_t wlen, int32_t nb, int lane) {
+// Every chunk of the lane from the staged input (chunks of not-staged records get don't-care
+// data, redone by chunk_pass_global).  Three phases so the LDS latency is paid once, not per
+// chunk: source offsets (walking the record table, next entry prefetched), all source reads,
+// then v_alignbyte + one ds_write_b128 per chunk.
+__device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk, int32_t wlen,
+                                           int32_t nb, int lane) {
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
+    RecEnt N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
+    int32_t u[kCpl];
+#pragma unroll
+    for (int k = 0; k < kCpl; ++k) {
+        const int32_t p = kLaneBytes * lane + 16 * k;
+        if (p >= E.rend && r + 1 < kRpt) {
+            do {  // records shorter than a chunk step: rare second iteration
+                ++r;
+                E = N;
+                N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
+            } while (p >= E.rend && r + 1 < kRpt);
+        }
+        u[k] = p - E.sh0 - 2 * zone_of(E, p - E.rw);
+    }
+    uint32_t d[kCpl][5];
+#pragma unroll
+    for (int k = 0; k < kCpl; ++k) {
+        int32_t i = u[k] >> 2;
+        i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) d[k][j] = q[j];
+    }
     lds_u8* const wl = wout + kLaneBytes * lane + (kLaneBytes * lane / 256) * kRowPad;  // 16-byte rows never split a lane
 #pragma unroll
+    for (int k = 0; k < kCpl; ++k) {
+        const uint32_t sh = (uint32_t)u[k] & 3u;
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], sh);
+        v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
+        v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
+        v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
+        if (kLaneBytes * lane + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
+    }
+}
+
+// the chunks of records whose strings are not all staged, from HBM (rare: a record straddling a
+// window of a multi-window tile, or valid records behind E109 records with large strings)
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+__device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i32* bk, const lds_u64* sbase,
+                                               int32_t wlen, int lane) {
+    int32_t r = bk[lane];
+    RecEnt E = rec_load(rt, r);
+    lds_u8* const wl = wout + kLaneBytes * lane + (kLaneBytes * lane / 256) * kRowPad;
     for (int k = 0; k < kCpl; ++k) {
         const int32_t p = kLaneBytes * lane + 16 * k;
         if (p >= wlen) break;
@@ -814,18 +878,14 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
             ++r;
             E = rec_load(rt, r);
         }
+        if (!(E.z5 & kNotStaged)) continue;
         const int32_t X = p - E.rw;
         const int32_t f = zone_of(E, X);
-        if (!kGlobal) {
-            const u32x4 v = chunk_lds(inb, p - E.sh0 - 2 * f, imax);
-            *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
-        } else if (E.z5 & kNotStaged) {
-            const uint64_t s0 = sbase[r];
-            const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - 34);
-            const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - 26 - 2 * f), s0 & ~3ull,
-                                      (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
-            *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
-        }
+        const uint64_t s0 = sbase[r];
+        const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - 34);
+        const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - 26 - 2 * f), s0 & ~3ull,
+                                  (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
+        *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
 
@@ -909,12 +969,12 @@ __device__ __forceinline__ void pack_window(lds_u8* wout, lds_u8* inb, lds_i32* 
                                             const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
                                             int lane) {
     const bool outside = build_tables(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
-    __syncthreads();
+    wsync();
 #ifndef SBE_ABL_NO_CHUNK
-    chunk_pass<false>(wout, inb, rt, bk, sbase, wlen, nb, lane);
-    if (outside) chunk_pass<true>(wout, inb, rt, bk, sbase, wlen, nb, lane);
+    chunk_pass(wout, inb, rt, bk, wlen, nb, lane);
+    if (outside) chunk_pass_global(wout, rt, bk, (const lds_u64*)sbase, wlen, lane);
 #endif
-    __syncthreads();
+    wsync();
 #ifndef SBE_ABL_NO_FIXUP
     fixup_pass(wout, inb, rt, sbase, S, wlen, nb, lane);
 #endif
@@ -948,29 +1008,38 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
     bool fast = kPacked && single_window(S);
     if (fast) {
         stage_range(S, -(int32_t)(S.T0 & 15), lane, swb, nb);
+    } else {
+        swb = reinterpret_cast<uintptr_t>(a.sink);
+        nb = 0;
+    }
+    if (kPacked) {
         stage_issue(swb, nb, lane, I);
+        stage_write(win_in, nb, lane, I);
     }
     uint64_t tn = t + G;
-    if (tn < ntiles) x = tile_load<kPacked>(a, tn, lane);
+    x = tile_load<kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane);
 
+    // Steady state, per tile: [next tile: prepare, lengths of the one after, staging loads]
+    // [compose + store this tile] [next tile's staged input → LDS].  The staging registers are
+    // written to LDS after this tile's stores, so that wait leaves exactly those stores in flight.
     for (;;) {
-        // current tile's staged input: registers → LDS
         const uintptr_t cur_swb = swb;
         const int32_t cur_nb = nb;
         const bool cur_fast = fast;
-        if (cur_fast) stage_write(win_in, cur_nb, lane, I);
-        // next tile: prepare it and put its input loads in flight; prefetch the one after
         const bool have_next = tn < ntiles;
         TileSt Sn;
         if (have_next) {
             Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane);
+            const uint64_t t2 = tn + G;
+            x = tile_load<kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane);
             fast = kPacked && single_window(Sn);
             if (fast) {
                 stage_range(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
-                stage_issue(swb, nb, lane, I);
+            } else {
+                swb = reinterpret_cast<uintptr_t>(a.sink);
+                nb = 0;
             }
-            const uint64_t t2 = tn + G;
-            if (t2 < ntiles) x = tile_load<kPacked>(a, t2, lane);
+            if (kPacked) stage_issue(swb, nb, lane, I);
         }
         // current tile: compose + store, one window (fast) or window by window
         const int32_t wrel0 = -(int32_t)(S.T0 & 15);
@@ -978,14 +1047,14 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
             if (kPacked) {
                 pack_window(wout, win_in, rt, bk, sbase, S, wrel0, (int32_t)S.len - wrel0, cur_swb, cur_nb, lane);
             } else {
-                __syncthreads();
+                wsync();
                 compose<false>(wout, win_in, S, wrel0, (int32_t)S.len, cur_swb, cur_nb);
             }
-            __syncthreads();
+            wsync();
 #ifndef SBE_ABL_NO_STORE
-            store_window(a.out, wout, S.T0, S.T0 & ~15ull, S.T0 + S.len, lane);
+            store_window(a.out, a.sink, wout, S.T0, S.T0 & ~15ull, S.T0 + S.len, lane);
 #endif
-            __syncthreads();
+            wsync();
         } else {
             for (int32_t wrel = wrel0; wrel < (int32_t)S.len; wrel += kEW) {
                 const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
@@ -1011,15 +1080,17 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
                 if (kPacked) {
                     pack_window(wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
                 } else {
-                    __syncthreads();
+                    wsync();
                     compose<false>(wout, win_in, S, wrel, we_rel, sw, nbw);
                 }
-                __syncthreads();
-                store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
-                __syncthreads();
+                wsync();
+                store_window(a.out, a.sink, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
+                wsync();
             }
         }
         if (!have_next) break;
+        if (kPacked) stage_write(win_in, nb, lane, I);  // after the compose above read win_in
+        wsync();
         S = Sn;
         tn += G;
     }
@@ -1559,7 +1630,7 @@ int sbe_device_ready(void) {
 size_t sbe_encode_workspace_size(uint64_t n) {
     const uint64_t blocks = (n + kBlk - 1) / kBlk;
     const uint64_t tiles = blocks * kTilesPerBlk;
-    return (size_t)(16 * (tiles + blocks) + 16);
+    return (size_t)(16 * (tiles + blocks) + kSinkBytes + 16);
 }
 
 uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t flags) {
@@ -1588,7 +1659,8 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
     if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
     uint64_t* ws = static_cast<uint64_t*>(workspace);
     EncArgs a{in->arena, in->str_off, in->str_len, in->timestamp, n,  ts_default,
-              out,       out_capacity, out_off,   status,        ws, ws + 2 * blocks * kTilesPerBlk};
+              out,       out_capacity, out_off,   status,        ws, ws + 2 * blocks * kTilesPerBlk,
+              reinterpret_cast<uint8_t*>(ws + 2 * blocks * (kTilesPerBlk + 1))};
     const bool packed = in->str_off == nullptr;
     const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
 #define SBE_ENC_LAUNCH(P, T)                                                                          \
