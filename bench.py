@@ -193,7 +193,7 @@ def main():
                        gbs=deck_gbs)
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(min(n, 200_000), args.cpu_seconds, args.cpu_threads)
         line = {
             "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world, "steps": args.steps,
