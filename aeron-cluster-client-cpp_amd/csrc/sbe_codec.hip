@@ -18,6 +18,7 @@
 //       global_load_dwordx4
 //    2. each lane parses its record from LDS (template-ID dispatch per lane) and writes the
 //       descriptor SoA; bytes outside the window are read from global memory.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -109,6 +110,28 @@ __device__ __forceinline__ uint4 gload128(uintptr_t addr) {
     const u32x4 v = *reinterpret_cast<g_u32x4*>(addr);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// streamed-once loads / stores with the non-temporal cache policy (nt)
+__device__ __forceinline__ uint4 gload128_nt(uintptr_t addr) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(addr));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#ifndef SBE_DEC_LD_NT
+#define SBE_DEC_LD_NT 1
+#endif
+#ifndef SBE_DEC_ST_NT
+#define SBE_DEC_ST_NT 1
+#endif
+#ifndef SBE_ENC_LD_NT
+#define SBE_ENC_LD_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void dst_store(T* p, T v) {
+#if SBE_DEC_ST_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 
 // ------------------------------------------------------------------------------------------
 // Encode: three launches, no inter-workgroup hand-off inside any of them.
@@ -142,6 +165,15 @@ struct EncArgs {
     uint8_t* sink;   // kSinkBytes of workspace: target of the pack kernel's don't-care stores
 };
 constexpr int kSinkBytes = 16 * 64;
+
+// Output store form of the pack kernel: buffer stores with cache-policy bits SBE_OUT_AUX
+// (0 default, 2 nt, 16 sc1 write-through) or plain global stores with a sink.
+#ifndef SBE_OUT_STORE_BUF
+#define SBE_OUT_STORE_BUF 1
+#endif
+#ifndef SBE_OUT_AUX
+#define SBE_OUT_AUX 2
+#endif
 
 // Sizes of record r: output bytes (0 on E109) and packed-input bytes (its strings, always).
 template <bool kTrunc>
@@ -564,7 +596,11 @@ __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int l
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
+#if SBE_ENC_LD_NT
+        const u32x4 v = __builtin_nontemporal_load(&base[ch < last ? ch : last]);
+#else
         const u32x4 v = base[ch < last ? ch : last];
+#endif
         I[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -661,6 +697,21 @@ __device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu
         const u32x4 a0 = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * ch + (ch >> 4) * kRowPad);
         v[k] = make_uint4(a0.x, a0.y, a0.z, a0.w);
     }
+#if SBE_OUT_STORE_BUF
+    // kIt unconditional 16-byte buffer stores; chunks not wholly inside [lo, we) take an offset past
+    // the descriptor's range, which the hardware drops (cache policy SBE_OUT_AUX)
+    (void)ob;
+    (void)sink;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + wb, 0, (int)(16u * c_hi), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        const bool full = ch >= c_lo && ch < c_hi;
+        u32x4 x;
+        x.x = v[k].x; x.y = v[k].y; x.z = v[k].z; x.w = v[k].w;
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, full ? (int)(16u * ch) : 0x7ffffff0, 0, SBE_OUT_AUX);
+    }
+#else
     // kIt unconditional 16-byte stores (chunks not wholly inside [lo, we) go to the sink)
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
@@ -669,6 +720,7 @@ __device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu
         uint4* dst = full ? ob + ch : reinterpret_cast<uint4*>(sink) + lane;
         *dst = v[k];
     }
+#endif
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -1475,7 +1527,11 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
 #pragma unroll
         for (int k = 0; k < kDecRegs; ++k) {
             const uint32_t ch = lane + kWave * k;
+#if SBE_DEC_LD_NT
+            I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+#else
             I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < kDecRegs; ++k) {
@@ -1514,11 +1570,12 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
     }
 #endif
     if (valid) {
-        a.status[r] = (uint8_t)d.status;
-        a.flags[r] = (uint8_t)d.flags;
-        *reinterpret_cast<uint2*>(a.hdr + 4 * r) = make_uint2((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16),
-                                                             (uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16));
-        a.ts[r] = d.ts;
+        dst_store(a.status + r, (uint8_t)d.status);
+        dst_store(a.flags + r, (uint8_t)d.flags);
+        dst_store(reinterpret_cast<uint64_t*>(a.hdr + 4 * r),
+                  (uint64_t)((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16)) |
+                      ((uint64_t)((uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16)) << 32));
+        dst_store(a.ts + r, d.ts);
     }
     // views [n][5]: transpose through LDS so each store instruction writes 256 contiguous bytes
     __syncthreads();
@@ -1535,8 +1592,8 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
     for (int k = 0; k < 5; ++k) {
         const uint32_t i = lane + kWave * k;
         if (i < nv) {
-            vo[i] = win[i];
-            vl[i] = win[5 * kWave + i];
+            dst_store(vo + i, win[i]);
+            dst_store(vl + i, win[5 * kWave + i]);
         }
     }
 }
@@ -1571,35 +1628,37 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
     return tiles < cached ? tiles : cached;
 }
 
-// Optional launch profiling: HIP events recorded on the launch stream around the pack kernel
-// and the decode kernel of every call, kept in a ring per kernel (read by sbe_profile_read).
+// Optional launch profiling: every `g_prof_every`-th launch of the pack kernel and of the decode
+// kernel carries a pair of HIP events, kept in a ring per kernel (read by sbe_profile_read).
 struct ProfRing {
     static constexpr int kCap = 256;
     hipEvent_t ev[kCap][2];
     int head = 0, count = 0;
+    uint64_t launches = 0;
     bool ready = false;
 };
-thread_local bool g_prof_on = false;
+thread_local int g_prof_every = 0;
 thread_local ProfRing g_prof[2];
 
-hipEvent_t prof_begin(int which, hipStream_t s) {
-    if (!g_prof_on) return nullptr;
+// The ring slot's (start, stop) events for this launch of `which`, or nulls when it is not
+// sampled.  They are handed to hipExtLaunchKernel, which timestamps the kernel's own dispatch.
+void prof_slot(int which, hipEvent_t* start, hipEvent_t* stop) {
+    *start = *stop = nullptr;
+    if (g_prof_every <= 0) return;
     ProfRing& R = g_prof[which];
+    if (R.launches++ % (uint64_t)g_prof_every != 0) return;
     if (!R.ready) {
         for (int i = 0; i < ProfRing::kCap; ++i)
             for (int j = 0; j < 2; ++j)
-                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return nullptr;
+                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return;
         R.ready = true;
     }
-    hipEvent_t b = R.ev[R.head][0];
-    (void)hipEventRecord(b, s);
-    return b;
+    *start = R.ev[R.head][0];
+    *stop = R.ev[R.head][1];
 }
-void prof_end(int which, hipStream_t s) {
-    if (!g_prof_on) return;
+void prof_commit(int which, hipEvent_t start) {
+    if (!start) return;
     ProfRing& R = g_prof[which];
-    if (!R.ready) return;
-    (void)hipEventRecord(R.ev[R.head][1], s);
     R.head = (R.head + 1) % ProfRing::kCap;
     if (R.count < ProfRing::kCap) ++R.count;
 }
@@ -1668,9 +1727,10 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
         const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<P, T>), tiles);   \
         hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)blocks), dim3(kBlk), 0, s, a);        \
         hipLaunchKernelGGL(sbe_enc_scan, dim3(1), dim3(kScanThreads), 0, s, a.bsum, blocks);          \
-        prof_begin(0, s);                                                                             \
-        hipLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, a);        \
-        prof_end(0, s);                                                                               \
+        hipEvent_t e0, e1;                                                                            \
+        prof_slot(0, &e0, &e1);                                                                       \
+        hipExtLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a); \
+        prof_commit(0, e0);                                                                               \
     } while (0)
     if (packed && !trunc) SBE_ENC_LAUNCH(true, false);
     else if (packed && trunc) SBE_ENC_LAUNCH(true, true);
@@ -1696,18 +1756,20 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     DecArgs a{in, rec_off, n, out->status, out->flags, out->hdr, out->ts, out->view_off, out->view_len};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((uint32_t)tiles), block(kWave);
-    prof_begin(1, s);
+    hipEvent_t e0, e1;
+    prof_slot(1, &e0, &e1);
     if (mode == SBE_DEC_ON_EGRESS)
-        hipLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_ON_EGRESS>), grid, block, 0, s, a);
+        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_ON_EGRESS>), grid, block, 0, s, e0, e1, 0, a);
     else
-        hipLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, a);
-    prof_end(1, s);
+        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, e0, e1, 0, a);
+    prof_commit(1, e0);
     return record_hip(hipGetLastError());
 }
 
-int sbe_profile_enable(int on) {
-    g_prof_on = on != 0;
-    for (auto& R : g_prof) R.head = R.count = 0;
+int sbe_profile_enable(int every) {
+    if (every < 0) return SBE_EINVAL;
+    g_prof_every = every;
+    for (auto& R : g_prof) R.head = R.count = 0, R.launches = 0;
     return SBE_OK;
 }
 

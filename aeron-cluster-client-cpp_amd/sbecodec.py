@@ -124,9 +124,9 @@ def require_device():
 PROF_PACK, PROF_DECODE = 0, 1
 
 
-def profile_enable(on: bool = True):
-    """Record HIP events around the pack / decode kernel of every call (sbecodec.h profiling)."""
-    _check(lib().sbe_profile_enable(1 if on else 0), "sbe_profile_enable")
+def profile_enable(every: int = 1):
+    """HIP events on the pack / decode kernel dispatch of every `every`-th call (0: off)."""
+    _check(lib().sbe_profile_enable(int(every)), "sbe_profile_enable")
 
 
 def profile_read(kernel: int, max_n: int = 256) -> list:

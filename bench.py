@@ -49,6 +49,9 @@ def parse_args():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--gather", action="store_true", help="also time the RCCL gather of encoded shards")
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
+    p.add_argument("--event-every", type=int, default=4,
+                   help="HIP events on the pack / decode dispatches of every k-th timed step (0: none, "
+                        "diagnosis only: kernel times then come from an extra untimed pass)")
     return p.parse_args()
 
 
@@ -146,7 +149,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    sbecodec.profile_enable(True)  # events around the pack / decode kernels on the launch stream
+    sbecodec.profile_enable(args.event_every)  # events on the pack / decode dispatches
     if args.verify:
         torch.cuda.synchronize()
         import sbe_testlib as T
@@ -164,9 +167,14 @@ def main():
     el = max_over_ranks(time.perf_counter() - t0, world)
     # the dominant kernels' durations, from the events the library recorded around them on the
     # launch stream inside the timed region
+    if args.event_every == 0:  # diagnosis: kernel times from an extra, untimed pass
+        sbecodec.profile_enable(1)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
     pack_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_PACK)))
     deck_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_DECODE)))
-    sbecodec.profile_enable(False)
+    sbecodec.profile_enable(0)
 
     # informational, untimed: whole-call encode (sums + scan + pack) and decode times
     for k in range(args.steps):
@@ -204,7 +212,9 @@ def main():
                        "decode": "parse_message descriptors (views)", "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": dom["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
-                         "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"]},
+                         "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"],
+                         "timing": (f"HIP events on the kernel's dispatch in every {args.event_every}th timed step"
+                                    if args.event_every else "HIP events, untimed pass (diagnosis run)")},
             "kernels": {"encode_ms": enc_ms, "encode_gbs": enc_gbs, "decode_ms": dec_ms, "decode_gbs": dec_gbs,
                         "pack_ms": pack_ms, "pack_gbs": pack_gbs, "decode_kernel_ms": deck_ms,
                         "decode_kernel_gbs": deck_gbs,

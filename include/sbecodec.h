@@ -169,13 +169,16 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
                      const sbe_decoded* out, void* stream);
 
 /* ================================== profiling ================================== */
-/* Optional (off by default; thread-local): when enabled, each sbe_encode_topic_batch /
- * sbe_decode_batch call records a pair of HIP events on its stream around its main kernel
- * (kernel 0 = the encode pack kernel, 1 = the decode kernel), kept in a ring of the last 256.
- * sbe_profile_read copies the elapsed milliseconds of up to `max` most recent launches (oldest
- * first) into ms[], clears the ring and returns the count; the caller synchronises the streams
- * first.  Used by bench.py to time the dominant kernel inside its timed region. */
-int sbe_profile_enable(int on);
+/* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every
+ * `every`-th sbe_encode_topic_batch / sbe_decode_batch call of this thread carry a pair of HIP
+ * events on its main kernel's dispatch (kernel 0 = the encode pack kernel, 1 = the decode
+ * kernel; hipExtLaunchKernel timestamps), kept in a ring of the last 256 per kernel; 0 turns it
+ * off.  Each call resets the rings and launch counters.  sbe_profile_read copies the elapsed
+ * milliseconds of up to `max` most recent sampled launches (oldest first) into ms[], clears the
+ * ring and returns the count; the caller synchronises the streams first.  Used by bench.py to
+ * time the dominant kernel inside its timed region (a timed dispatch costs the GPU several us,
+ * hence the sampling). */
+int sbe_profile_enable(int every);
 int sbe_profile_read(int kernel, float* ms, int max);
 
 /* ===================================== misc ===================================== */
