@@ -134,20 +134,24 @@ __device__ __forceinline__ void dst_store(T* p, T v) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Encode: three launches, no inter-workgroup hand-off inside any of them.
-//   K1 sbe_enc_sums   per 64-record tile and per 256-record block: output / packed-input bytes
-//   K2 sbe_enc_scan   one workgroup: exclusive scan of the block sums (in place)
-//   K3 sbe_enc_pack   one wave per tile: record offsets, LDS-staged input, per-lane record
-//                     composition into an LDS output window, coalesced 16-byte stores
+// Encode: two launches, no inter-workgroup hand-off inside either.
+//   K1 sbe_enc_sums   one workgroup per 4096-record superblock: every 32-record tile's output /
+//                     packed-input byte prefix inside its superblock, and the superblock totals
+//   K3 sbe_enc_pack   persistent, one wave per tile: the superblock totals before the tile (a
+//                     running sum per workgroup: its tiles come in increasing order), record
+//                     offsets, LDS-staged input, per-lane record composition into an LDS output
+//                     window, coalesced 16-byte stores
 // ------------------------------------------------------------------------------------------
 #ifndef SBE_ENC_RPT
 #define SBE_ENC_RPT 32
 #endif
-constexpr int kBlk = 256;                             // records per K1/K2 block
+constexpr int kSbRec = 4096;                          // records per superblock (one K1 workgroup)
+constexpr int kSbThreads = 1024;
 constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
 constexpr int kLpr = kWave / kRpt;                    // lanes per record in K3
-constexpr int kTilesPerBlk = kBlk / kRpt;
-static_assert(kWave % kRpt == 0 && kBlk % kRpt == 0, "tile shape");
+constexpr int kTilesPerSb = kSbRec / kRpt;
+static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt == 0 &&
+              kTilesPerSb == 2 * kWave, "tile shape");
 
 struct EncArgs {
     const uint8_t* arena;
@@ -160,8 +164,8 @@ struct EncArgs {
     uint64_t cap;
     uint64_t* out_off;
     uint8_t* status;
-    uint64_t* tsum;  // [tiles][2]   output / input bytes before the tile within its block
-    uint64_t* bsum;  // [blocks][2]  per block; K2 turns it into exclusive prefixes
+    uint64_t* tsum;  // [tiles][2]        output / input bytes before the tile within its superblock
+    uint64_t* bsum;  // [superblocks][2]  output / input bytes of the superblock
     uint8_t* sink;   // kSinkBytes of workspace: target of the pack kernel's don't-care stores
 };
 constexpr int kSinkBytes = 16 * 64;
@@ -207,90 +211,47 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
     return v;
 }
 
+// K1: superblock sb = records [4096 sb, 4096 (sb+1)).  Thread t takes records t, t+1024, t+2048,
+// t+3072 of it (each load instruction of a wave then covers 1280 contiguous bytes of lengths); the
+// 32 records of a tile are 32 consecutive threads.  Tile sums go through LDS to one wave, which
+// writes the 128 tile prefixes and the superblock's totals.
 template <bool kPacked, bool kTrunc>
-__global__ __launch_bounds__(kBlk) void sbe_enc_sums(EncArgs a) {
-    __shared__ uint64_t tl[2][kTilesPerBlk];
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t r = (uint64_t)blockIdx.x * kBlk + threadIdx.x;
-    uint32_t L[5], ob, ib;
-    uint8_t st;
-    rec_sizes<kTrunc>(a, r, L, ob, ib, st);
-    // per pack tile (kRpt consecutive lanes): segmented sums via shuffles (input side in 64 bits:
-    // E109 records may carry up to 5 x 4 GiB of strings)
-    uint32_t to = ob;
-    uint64_t ti = kPacked ? ib : 0u;
+__global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
+    __shared__ uint64_t tl[2][kTilesPerSb];
+    const int tid = threadIdx.x;
+    const uint64_t sb = blockIdx.x;
 #pragma unroll
-    for (int d = 1; d < kRpt; d <<= 1) {
-        to += __shfl_xor(to, d, kWave);
-        if (kPacked) ti += __shfl_xor(ti, d, kWave);
-    }
-    if ((lane & (kRpt - 1)) == 0) {
-        tl[0][threadIdx.x / kRpt] = to;
-        tl[1][threadIdx.x / kRpt] = ti;
+    for (int j = 0; j < kSbRec / kSbThreads; ++j) {
+        const uint64_t r = sb * kSbRec + (uint64_t)j * kSbThreads + tid;
+        uint32_t L[5], ob, ib;
+        uint8_t st;
+        rec_sizes<kTrunc>(a, r, L, ob, ib, st);
+        // per tile (kRpt consecutive lanes): sums via shuffles (input side in 64 bits: E109
+        // records may carry up to 5 x 4 GiB of strings)
+        uint32_t to = ob;
+        uint64_t ti = kPacked ? ib : 0u;
+#pragma unroll
+        for (int d = 1; d < kRpt; d <<= 1) {
+            to += __shfl_xor(to, d, kWave);
+            if (kPacked) ti += __shfl_xor(ti, d, kWave);
+        }
+        if ((tid & (kRpt - 1)) == 0) {
+            const int tile = j * (kSbThreads / kRpt) + tid / kRpt;
+            tl[0][tile] = to;
+            tl[1][tile] = ti;
+        }
     }
     __syncthreads();
-    // tile prefixes within the block, and the block's totals (K2 scans them)
-    if (threadIdx.x == 0) {
-        uint64_t po = 0, pi = 0;
-        for (int j = 0; j < kTilesPerBlk; ++j) {
-            const uint64_t tile = (uint64_t)blockIdx.x * kTilesPerBlk + j;
-            a.tsum[2 * tile] = po;
-            a.tsum[2 * tile + 1] = pi;
-            po += tl[0][j];
-            pi += tl[1][j];
-        }
-        a.bsum[2 * blockIdx.x] = po;
-        a.bsum[2 * blockIdx.x + 1] = pi;
-    }
-}
-
-// exclusive scan of nb (out, in) pairs in place; one workgroup of 1024 threads
-constexpr int kScanThreads = 1024, kScanPer = 4;
-__global__ __launch_bounds__(kScanThreads) void sbe_enc_scan(uint64_t* bsum, uint64_t nb) {
-    __shared__ uint64_t wt[2][kScanThreads / kWave];
-    __shared__ uint64_t carry[2];
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-    if (tid == 0) carry[0] = carry[1] = 0;
-    __syncthreads();
-    for (uint64_t base = 0; base < nb; base += (uint64_t)kScanThreads * kScanPer) {
-        uint64_t vo[kScanPer], vi[kScanPer], so = 0, si = 0;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const uint64_t i = base + (uint64_t)tid * kScanPer + k;
-            vo[k] = i < nb ? bsum[2 * i] : 0;
-            vi[k] = i < nb ? bsum[2 * i + 1] : 0;
-            so += vo[k];
-            si += vi[k];
-        }
-        const uint64_t io = wave_incl_scan64(so, lane), ii = wave_incl_scan64(si, lane);
-        if (lane == kWave - 1) {
-            wt[0][w] = io;
-            wt[1][w] = ii;
-        }
-        __syncthreads();
-        uint64_t po = carry[0], pi = carry[1];
-        for (int j = 0; j < w; ++j) {
-            po += wt[0][j];
-            pi += wt[1][j];
-        }
-        po += io - so;
-        pi += ii - si;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            const uint64_t i = base + (uint64_t)tid * kScanPer + k;
-            if (i < nb) {
-                bsum[2 * i] = po;
-                bsum[2 * i + 1] = pi;
-            }
-            po += vo[k];
-            pi += vi[k];
-        }
-        __syncthreads();
-        if (tid == kScanThreads - 1) {
-            carry[0] = po;
-            carry[1] = pi;
-        }
-        __syncthreads();
+    if (tid < kWave) {  // exclusive scan of the 128 tile sums, two per lane
+        const int lane = tid;
+        const uint64_t o0 = tl[0][2 * lane], o1 = tl[0][2 * lane + 1];
+        const uint64_t i0 = tl[1][2 * lane], i1 = tl[1][2 * lane + 1];
+        const uint64_t io = wave_incl_scan64(o0 + o1, lane), ii = wave_incl_scan64(i0 + i1, lane);
+        const uint64_t eo = io - o0 - o1, ei = ii - i0 - i1;
+        const uint64_t t0 = sb * kTilesPerSb + 2 * lane;
+        *reinterpret_cast<ulonglong2*>(a.tsum + 2 * t0) = make_ulonglong2(eo, ei);
+        *reinterpret_cast<ulonglong2*>(a.tsum + 2 * t0 + 2) = make_ulonglong2(eo + o0, ei + i0);
+        if (lane == kWave - 1) *reinterpret_cast<ulonglong2*>(a.bsum + 2 * sb) = make_ulonglong2(io, ii);
     }
 }
 
@@ -457,9 +418,12 @@ constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging r
 struct TileIn {  // raw per-lane loads of one tile
     uint32_t L[5];
     uint64_t ts;
-    // tile start = block prefix + tile prefix (output / packed input), added in tile_prepare: an
-    // add here would wait on these loads, and vmcnt retires in order, so on the prefetch too
-    uint64_t bo, to, bi, ti;
+    // tile start = (superblock totals before the tile) + tile prefix inside its superblock, for
+    // output / packed input.  The superblock totals the workgroup has not yet summed come as
+    // per-lane partials (po, pi); tile_prepare reduces them: an add here would wait on these
+    // loads, and vmcnt retires in order, so on the prefetch too.
+    uint64_t to, ti, po, pi;
+    uint32_t pcount;  // uniform: lanes [0, pcount) of po / pi are superblock totals to add
 };
 
 struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from T0 / in_tile
@@ -475,8 +439,10 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
     uintptr_t gsrc[5];             // gather mode: absolute string addresses
 };
 
+// sb_next: the first superblock whose total this workgroup has not loaded yet (tiles come in
+// increasing order; a clamped repeat of the last tile loads nothing new)
 template <bool kPacked>
-__device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane) {
+__device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane, uint64_t& sb_next) {
     TileIn x;
     // unconditional loads at a clamped index: a select on the loaded value here would make the
     // compiler wait for it (tile_prepare applies r < n)
@@ -485,16 +451,26 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
 #pragma unroll
     for (int f = 0; f < 5; ++f) x.L[f] = a.str_len[5 * r + f];
     x.ts = a.timestamp[r];
-    const uint64_t blk = tile / kTilesPerBlk;  // uniform: scalar loads
-    x.bo = a.bsum[2 * blk];
-    x.to = a.tsum[2 * tile];
-    x.bi = kPacked ? a.bsum[2 * blk + 1] : 0ull;
+    x.to = a.tsum[2 * tile];  // uniform: scalar loads
     x.ti = kPacked ? a.tsum[2 * tile + 1] : 0ull;
+    // totals of superblocks [sb_next, tile's superblock): lane l loads superblock sb_next + l at a
+    // clamped index, unconditionally (tile_prepare masks lanes >= count); at most G/128 + 1 of
+    // them, so one per lane while the persistent grid stays under 63 x 128 workgroups
+    const uint64_t sbt = tile / kTilesPerSb;
+    const uint64_t last_sb = (a.n - 1) / kSbRec;
+    uint64_t s = sb_next + (uint64_t)lane;
+    s = s < last_sb ? s : last_sb;
+    x.po = a.bsum[2 * s];
+    x.pi = kPacked ? a.bsum[2 * s + 1] : 0ull;
+    x.pcount = sbt > sb_next ? (uint32_t)(sbt - sb_next) : 0u;
+    sb_next = sbt > sb_next ? sbt : sb_next;
     return x;
 }
 
+// sp_out / sp_in: running totals of the superblocks before this workgroup's current tile
 template <bool kPacked, bool kTrunc>
-__device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane) {
+__device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
+                                               uint64_t& sp_out, uint64_t& sp_in) {
     TileSt S;
     const int q = lane % kLpr, lead = lane - q;
     const uint64_t r = tile * kRpt + lane / kLpr;
@@ -512,8 +488,10 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
-    const uint64_t base_out = uniform64(x.bo + x.to);
-    const uint64_t base_in = kPacked ? uniform64(x.bi + x.ti) : 0ull;
+    sp_out += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull));
+    if (kPacked) sp_in += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull));
+    const uint64_t base_out = uniform64(sp_out + x.to);
+    const uint64_t base_in = kPacked ? uniform64(sp_in + x.ti) : 0ull;
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
     const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
@@ -1052,8 +1030,9 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
     uint64_t t = blockIdx.x;
     if (t >= ntiles) return;
 
-    TileIn x = tile_load<kPacked>(a, t, lane);
-    TileSt S = tile_prepare<kPacked, kTrunc>(a, x, t, lane);
+    uint64_t sb_next = 0, sp_out = 0, sp_in = 0;
+    TileIn x = tile_load<kPacked>(a, t, lane, sb_next);
+    TileSt S = tile_prepare<kPacked, kTrunc>(a, x, t, lane, sp_out, sp_in);
     uint4 I[kStageRegs];
     uintptr_t swb = 0;
     int32_t nb = 0;
@@ -1069,7 +1048,7 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
         stage_write(win_in, nb, lane, I);
     }
     uint64_t tn = t + G;
-    x = tile_load<kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane);
+    x = tile_load<kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane, sb_next);
 
     // Steady state, per tile: [next tile: prepare, lengths of the one after, staging loads]
     // [compose + store this tile] [next tile's staged input → LDS].  The staging registers are
@@ -1081,9 +1060,9 @@ __global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
         const bool have_next = tn < ntiles;
         TileSt Sn;
         if (have_next) {
-            Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane);
+            Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane, sp_out, sp_in);
             const uint64_t t2 = tn + G;
-            x = tile_load<kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane);
+            x = tile_load<kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
             fast = kPacked && single_window(Sn);
             if (fast) {
                 stage_range(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
@@ -1625,7 +1604,9 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
         cached_k = kernel;
         cached_dev = dev;
     }
-    return tiles < cached ? tiles : cached;
+    // tile_load adds at most one superblock total per lane per tile step: G/128 + 1 <= 64
+    const uint64_t g = cached < (uint64_t)(kWave - 1) * kTilesPerSb ? cached : (uint64_t)(kWave - 1) * kTilesPerSb;
+    return tiles < g ? tiles : g;
 }
 
 // Optional launch profiling: every `g_prof_every`-th launch of the pack kernel and of the decode
@@ -1687,9 +1668,9 @@ int sbe_device_ready(void) {
 }
 
 size_t sbe_encode_workspace_size(uint64_t n) {
-    const uint64_t blocks = (n + kBlk - 1) / kBlk;
-    const uint64_t tiles = blocks * kTilesPerBlk;
-    return (size_t)(16 * (tiles + blocks) + kSinkBytes + 16);
+    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
+    const uint64_t tiles = sbs * kTilesPerSb;
+    return (size_t)(16 * (tiles + sbs) + kSinkBytes + 16);
 }
 
 uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t flags) {
@@ -1711,22 +1692,21 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
     if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
     if (!in->str_len || !in->timestamp || !in->arena || !out) return SBE_EINVAL;
     if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
-    const uint64_t blocks = (n + kBlk - 1) / kBlk;
+    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
     const uint64_t tiles = (n + kRpt - 1) / kRpt;
     if (tiles > kMaxTiles) return SBE_EINVAL;
     if (!workspace || workspace_bytes < sbe_encode_workspace_size(n)) return SBE_ENOSPC;
     if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
     uint64_t* ws = static_cast<uint64_t*>(workspace);
     EncArgs a{in->arena, in->str_off, in->str_len, in->timestamp, n,  ts_default,
-              out,       out_capacity, out_off,   status,        ws, ws + 2 * blocks * kTilesPerBlk,
-              reinterpret_cast<uint8_t*>(ws + 2 * blocks * (kTilesPerBlk + 1))};
+              out,       out_capacity, out_off,   status,        ws, ws + 2 * sbs * kTilesPerSb,
+              reinterpret_cast<uint8_t*>(ws + 2 * sbs * (kTilesPerSb + 1))};
     const bool packed = in->str_off == nullptr;
     const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
 #define SBE_ENC_LAUNCH(P, T)                                                                          \
     do {                                                                                              \
         const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<P, T>), tiles);   \
-        hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)blocks), dim3(kBlk), 0, s, a);        \
-        hipLaunchKernelGGL(sbe_enc_scan, dim3(1), dim3(kScanThreads), 0, s, a.bsum, blocks);          \
+        hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)sbs), dim3(kSbThreads), 0, s, a);     \
         hipEvent_t e0, e1;                                                                            \
         prof_slot(0, &e0, &e1);                                                                       \
         hipExtLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a); \

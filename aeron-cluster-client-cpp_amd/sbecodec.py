@@ -94,6 +94,13 @@ def lib():
     return _lib
 
 
+def use_library(path: str):
+    """Bind this module to another build of the codec (A/B timing of kernel variants)."""
+    global _lib, LIB_PATH
+    LIB_PATH = path
+    _lib = _load()
+
+
 def _check(rc: int, what: str):
     if rc != 0:
         raise SbeError(f"{what} failed: {_ERRORS.get(rc, rc)} {lib().sbe_last_error().decode()}")
