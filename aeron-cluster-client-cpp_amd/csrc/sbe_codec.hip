@@ -255,6 +255,9 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
     }
 }
 
+#ifndef SBE_PACK_MIN_WAVES  // minimum waves per SIMD the pack kernel's registers must allow
+#define SBE_PACK_MIN_WAVES 1
+#endif
 #ifndef SBE_ENC_WIN
 #define SBE_ENC_WIN 8192
 #endif
@@ -1014,7 +1017,7 @@ __device__ __forceinline__ void pack_window(lds_u8* wout, lds_u8* inb, lds_i32* 
 }
 
 template <bool kPacked, bool kTrunc>
-__global__ __launch_bounds__(kWave) void sbe_enc_pack(EncArgs a) {
+__global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
     __shared__ __attribute__((aligned(16))) int32_t rt_arr[kPacked ? kRpt * kRecEnt : 4];
@@ -1480,45 +1483,74 @@ __device__ void dec_on_egress(const R_t& R, uint32_t len, Desc& d) {
     d.status = SBE_ST_EG_TM;
 }
 
+#ifndef SBE_DEC_PERSIST
+#define SBE_DEC_PERSIST 0  // measured: the persistent form was 6-10 % slower (hardware WG dispatch overlaps better)
+#endif
+constexpr int kDecRegs = kWin / 16 / kWave;  // uint4 staging registers per lane (one tile)
+
+// One 64-record tile: its byte range and this lane's record.
+struct DecTile {
+    uint64_t T0, T1;  // rec_off[first], rec_off[last] (uniform)
+    uint64_t rs, re;  // this lane's record [rs, re) (clamped to the last record past the end)
+};
+
+__device__ __forceinline__ DecTile dec_tile_load(const DecArgs& a, uint64_t tile, int lane) {
+    DecTile x;
+    const uint64_t t0 = tile * kTile;
+    const uint64_t last = t0 + kTile < a.n ? t0 + kTile : a.n;
+    x.T0 = a.rec_off[t0];
+    x.T1 = a.rec_off[last];
+    uint64_t r = t0 + (uint64_t)lane;
+    r = r < a.n ? r : a.n - 1;
+    x.rs = a.rec_off[r];
+    x.re = a.rec_off[r + 1];
+    return x;
+}
+
+// staged window [wb, we) of a tile: from its first byte (16-B aligned down) for kWin bytes at most
+__device__ __forceinline__ void dec_window(const DecTile& x, uint64_t& wb, uint64_t& we) {
+    wb = uniform64(x.T0) & ~15ull;
+    const uint64_t end = (uniform64(x.T1) + 15) & ~15ull;
+    we = (wb + kWin) < end ? wb + kWin : end;
+}
+
+__device__ __forceinline__ void dec_stage_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane,
+                                                uint4 (&I)[kDecRegs]) {
+    const uint32_t nch = (uint32_t)((we - wb) >> 4);
+    const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
+#pragma unroll
+    for (int k = 0; k < kDecRegs; ++k) {
+        const uint32_t ch = lane + kWave * k;
+#if SBE_DEC_LD_NT
+        I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+#else
+        I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+#endif
+    }
+}
+
+__device__ __forceinline__ void dec_stage_write(uint32_t* win, uint64_t wb, uint64_t we, int lane,
+                                                const uint4 (&I)[kDecRegs]) {
+    const uint32_t nch = (uint32_t)((we - wb) >> 4);
+#pragma unroll
+    for (int k = 0; k < kDecRegs; ++k) {
+        const uint32_t ch = lane + kWave * k;
+        if (ch < nch) lds_write_chunk(win, ch, I[k]);
+    }
+}
+
+// Parse the tile's records (staged in win as [wb, we)) and write their descriptors.  The
+// workgroup is one wave, whose LDS accesses execute in issue order: phase changes are compiler
+// barriers (a __syncthreads() would wait vmcnt(0) and drain the next tile's staging loads).
 template <uint32_t kMode>
-__global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
-    __shared__ uint32_t win[kWinDw];
-    const int lane = threadIdx.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+__device__ __forceinline__ void dec_tile(const DecArgs& a, uint32_t* win, const DecTile& x, uint64_t wb,
+                                         uint64_t we, uint64_t tile, int lane) {
+    const uint64_t t0 = tile * kTile;
     const uint64_t r = t0 + lane;
     const bool valid = r < a.n;
     const uint64_t last = (t0 + kTile < a.n ? t0 + kTile : a.n);
-    const uint64_t T0 = uniform64(a.rec_off[t0]);
-    const uint64_t T1 = uniform64(a.rec_off[last]);
-    const uint64_t rs = valid ? a.rec_off[r] : 0;
-    const uint64_t rl = valid ? a.rec_off[r + 1] - rs : 0;
-
-    // ---- stage [wb, min(wb+kWin, align16(T1))) into LDS with 16-byte loads
-    const uint64_t wb = T0 & ~15ull;
-    const uint64_t end = (T1 + 15) & ~15ull;
-    const uint64_t we = (wb + kWin) < end ? wb + kWin : end;
-    {
-        // all loads in flight before the first LDS write: one HBM round trip per tile
-        constexpr int kDecRegs = kWin / 16 / kWave;
-        const uint32_t nch = (uint32_t)((we - wb) >> 4);
-        const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
-        uint4 I[kDecRegs];
-#pragma unroll
-        for (int k = 0; k < kDecRegs; ++k) {
-            const uint32_t ch = lane + kWave * k;
-#if SBE_DEC_LD_NT
-            I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
-#else
-            I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
-#endif
-        }
-#pragma unroll
-        for (int k = 0; k < kDecRegs; ++k) {
-            const uint32_t ch = lane + kWave * k;
-            if (ch < nch) lds_write_chunk(win, ch, I[k]);
-        }
-    }
-    __syncthreads();
+    const uint64_t rs = valid ? x.rs : 0;
+    const uint64_t rl = valid ? x.re - x.rs : 0;
 
     Desc d;
     d.clear();
@@ -1539,15 +1571,6 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
         else
             dec_parse_message(R, (uint32_t)rl, d);
     }
-
-#ifdef SBE_DABL_NOSTORE
-    {
-        uint32_t acc = d.status ^ d.flags ^ d.hdr[0] ^ d.hdr[1] ^ (uint32_t)d.ts;
-        for (int k = 0; k < 5; ++k) acc ^= d.off[k] ^ d.len[k];
-        if (acc == 0x12345678u) a.status[r] = 1;
-        return;
-    }
-#endif
     if (valid) {
         dst_store(a.status + r, (uint8_t)d.status);
         dst_store(a.flags + r, (uint8_t)d.flags);
@@ -1557,13 +1580,13 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
         dst_store(a.ts + r, d.ts);
     }
     // views [n][5]: transpose through LDS so each store instruction writes 256 contiguous bytes
-    __syncthreads();
+    wsync();
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         win[5 * lane + k] = d.off[k];
         win[5 * kWave + 5 * lane + k] = d.len[k];
     }
-    __syncthreads();
+    wsync();
     const uint32_t nv = 5u * (uint32_t)(last - t0);
     uint32_t* vo = a.view_off + 5 * t0;
     uint32_t* vl = a.view_len + 5 * t0;
@@ -1577,6 +1600,69 @@ __global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
     }
 }
 
+#if SBE_DEC_PERSIST
+// Persistent: one wave per workgroup loops over tiles t = blockIdx.x, += gridDim.x.  While it
+// parses tile t it holds tile t+G's 16 KiB of staging loads in flight (registers) and tile
+// t+2G's record offsets, so a tile's two dependent HBM round trips hide behind the previous
+// tile's parse.
+template <uint32_t kMode>
+__global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
+    __shared__ uint32_t win[kWinDw];
+    const int lane = threadIdx.x;
+    const uint64_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint64_t G = gridDim.x;
+    uint64_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    DecTile cur = dec_tile_load(a, t, lane);
+    uint64_t wb, we;
+    dec_window(cur, wb, we);
+    uint4 I[kDecRegs];
+    dec_stage_issue(a, wb, we, lane, I);
+    uint64_t tn = t + G;
+    DecTile nxt = dec_tile_load(a, tn < ntiles ? tn : ntiles - 1, lane);
+    dec_stage_write(win, wb, we, lane, I);
+    for (;;) {
+        const bool have_next = tn < ntiles;
+        uint64_t nwb = 0, nwe = 0;
+        DecTile after = nxt;
+        if (have_next) {
+            dec_window(nxt, nwb, nwe);
+            dec_stage_issue(a, nwb, nwe, lane, I);
+            const uint64_t t2 = tn + G;
+            after = dec_tile_load(a, t2 < ntiles ? t2 : ntiles - 1, lane);
+        }
+        wsync();
+        dec_tile<kMode>(a, win, cur, wb, we, t, lane);
+        if (!have_next) break;
+        wsync();
+        dec_stage_write(win, nwb, nwe, lane, I);
+        wsync();
+        cur = nxt;
+        nxt = after;
+        wb = nwb;
+        we = nwe;
+        t = tn;
+        tn += G;
+    }
+}
+#else
+// one workgroup per tile
+template <uint32_t kMode>
+__global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
+    __shared__ uint32_t win[kWinDw];
+    const int lane = threadIdx.x;
+    const uint64_t t = blockIdx.x;
+    const DecTile cur = dec_tile_load(a, t, lane);
+    uint64_t wb, we;
+    dec_window(cur, wb, we);
+    uint4 I[kDecRegs];
+    dec_stage_issue(a, wb, we, lane, I);
+    dec_stage_write(win, wb, we, lane, I);
+    __syncthreads();
+    dec_tile<kMode>(a, win, cur, wb, we, t, lane);
+}
+#endif
+
 thread_local char g_last_error[256] = "";
 
 int record_hip(hipError_t e) {
@@ -1589,23 +1675,33 @@ constexpr uint64_t kMaxTiles = 0xffffffffull;
 
 // Persistent grid of the pack kernel: every workgroup resident at once (occupancy x CUs).
 uint64_t pack_grid(const void* kernel, uint64_t tiles) {
-    static thread_local const void* cached_k = nullptr;
-    static thread_local int cached_dev = -1;
-    static thread_local uint64_t cached = 0;
+    struct Entry {
+        const void* k;
+        int dev;
+        uint64_t g;
+    };
+    static thread_local Entry cache[8] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    if (kernel != cached_k || dev != cached_dev) {
+    uint64_t g = 0;
+    for (const Entry& e : cache)
+        if (e.k == kernel && e.dev == dev) g = e.g;
+    if (g == 0) {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWave, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
-        cached = (uint64_t)per_cu * (uint64_t)cus;
-        cached_k = kernel;
-        cached_dev = dev;
+        g = (uint64_t)per_cu * (uint64_t)cus;
+        for (Entry& e : cache)
+            if (e.k == nullptr) {
+                e = Entry{kernel, dev, g};
+                break;
+            }
     }
-    // tile_load adds at most one superblock total per lane per tile step: G/128 + 1 <= 64
-    const uint64_t g = cached < (uint64_t)(kWave - 1) * kTilesPerSb ? cached : (uint64_t)(kWave - 1) * kTilesPerSb;
+    // the pack kernel's tile_load adds at most one superblock total per lane per tile step:
+    // G/128 + 1 <= 64
+    if (g > (uint64_t)(kWave - 1) * kTilesPerSb) g = (uint64_t)(kWave - 1) * kTilesPerSb;
     return tiles < g ? tiles : g;
 }
 
@@ -1735,7 +1831,14 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     if (tiles > kMaxTiles) return SBE_EINVAL;
     DecArgs a{in, rec_off, n, out->status, out->flags, out->hdr, out->ts, out->view_off, out->view_len};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#if SBE_DEC_PERSIST
+    const void* kfn = mode == SBE_DEC_ON_EGRESS
+                          ? reinterpret_cast<const void*>(&sbe_decode_kernel<SBE_DEC_ON_EGRESS>)
+                          : reinterpret_cast<const void*>(&sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>);
+    const dim3 grid((uint32_t)pack_grid(kfn, tiles)), block(kWave);
+#else
     const dim3 grid((uint32_t)tiles), block(kWave);
+#endif
     hipEvent_t e0, e1;
     prof_slot(1, &e0, &e1);
     if (mode == SBE_DEC_ON_EGRESS)
