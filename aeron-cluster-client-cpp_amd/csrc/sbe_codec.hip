@@ -153,11 +153,38 @@ constexpr int kTilesPerSb = kSbRec / kRpt;
 static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt == 0 &&
               kTilesPerSb == 2 * kWave, "tile shape");
 
+// Record layouts (compile-time): kPre bytes of session header, the 8-byte SBE header, a kBlk-byte
+// fixed block, then kNF u16-length-prefixed strings.
+//   LayTM   TopicMessage                     TopicMessage.h:98-1435
+//   LayTMS  SessionMessageHeader + TopicMessage  src/session_manager.cpp:936-967, :1118-1144
+//   LayL2   CommitOffsetLite (301)           include/model/CommitOffsetLite.h:114-118
+//   LayL3   OrderRequestLite / OrderNotificationLite (201 / 202)  OrderRequestLite.h:114-118
+template <int kPre_, int kBlk_, int kNF_, bool kTM_>
+struct Lay {
+    static constexpr int32_t kPre = kPre_;
+    static constexpr int32_t kBlk = kBlk_;
+    static constexpr int kNF = kNF_;
+    static constexpr bool kTM = kTM_;                 // TopicMessage block (timestamp default, truncation)
+    static constexpr int32_t kLit = kPre + 8 + kBlk;  // literal prefix bytes (multiple of 4)
+    static constexpr int32_t kS0 = kLit + 2;          // first string byte
+    static constexpr int32_t kOvh = kLit + 2 * kNF;   // wire overhead
+    static constexpr int32_t ovh(bool trunc) { return kOvh - (trunc ? 8 : 0); }
+};
+using LayTM = Lay<0, 16, 5, true>;
+using LayTMS = Lay<32, 16, 5, true>;
+using LayL2 = Lay<0, 12, 2, false>;
+using LayL3 = Lay<0, 12, 3, false>;
+static_assert(LayTM::kOvh == SBE_TM_WIRE_OVERHEAD && LayTM::ovh(true) == SBE_TM_REF_OVERHEAD, "TM layout");
+static_assert(LayL2::kOvh == SBE_LITE_OVERHEAD(2) && LayTMS::kPre == SBE_SESSION_HDR_LEN, "layouts");
+
 struct EncArgs {
     const uint8_t* arena;
     const uint32_t* str_off;
-    const uint32_t* str_len;
-    const uint64_t* timestamp;
+    const uint32_t* str_len;   // [n][kNF]
+    const uint64_t* timestamp; // TopicMessage timestamp / Lite sequence
+    const uint32_t* topic_id;  // Lite topicId
+    uint32_t tmpl;             // Lite template id
+    int64_t term_id, sess_id;  // session header
     uint64_t n;
     uint64_t ts_default;
     uint8_t* out;
@@ -180,7 +207,7 @@ constexpr int kSinkBytes = 16 * 64;
 #endif
 
 // Sizes of record r: output bytes (0 on E109) and packed-input bytes (its strings, always).
-template <bool kTrunc>
+template <class LY, bool kTrunc>
 __device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t (&L)[5], uint32_t& out_b,
                                           uint32_t& in_b, uint8_t& st) {
     uint32_t sum = 0;
@@ -189,15 +216,15 @@ __device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t
     for (int f = 0; f < 5; ++f) L[f] = 0;
     if (r < a.n) {
 #pragma unroll
-        for (int f = 0; f < 5; ++f) {
-            L[f] = a.str_len[5 * r + f];
+        for (int f = 0; f < LY::kNF; ++f) {
+            L[f] = a.str_len[LY::kNF * r + f];
             sum += L[f];
         }
 #pragma unroll
-        for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
+        for (int f = LY::kNF - 1; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
             if (L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
     }
-    const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+    const uint32_t ovh = (uint32_t)LY::ovh(kTrunc);
     out_b = (r < a.n && st == SBE_ENC_OK) ? ovh + sum : 0u;
     in_b = r < a.n ? sum : 0u;
 }
@@ -215,7 +242,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
 // t+3072 of it (each load instruction of a wave then covers 1280 contiguous bytes of lengths); the
 // 32 records of a tile are 32 consecutive threads.  Tile sums go through LDS to one wave, which
 // writes the 128 tile prefixes and the superblock's totals.
-template <bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
     __shared__ uint64_t tl[2][kTilesPerSb];
     const int tid = threadIdx.x;
@@ -225,7 +252,7 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
         const uint64_t r = sb * kSbRec + (uint64_t)j * kSbThreads + tid;
         uint32_t L[5], ob, ib;
         uint8_t st;
-        rec_sizes<kTrunc>(a, r, L, ob, ib, st);
+        rec_sizes<LY, kTrunc>(a, r, L, ob, ib, st);
         // per tile (kRpt consecutive lanes): sums via shuffles (input side in 64 bits: E109
         // records may carry up to 5 x 4 GiB of strings)
         uint32_t to = ob;
@@ -420,7 +447,8 @@ constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging r
 
 struct TileIn {  // raw per-lane loads of one tile
     uint32_t L[5];
-    uint64_t ts;
+    uint64_t ts;      // timestamp (TopicMessage) / sequence (Lite)
+    uint32_t tid;     // Lite topicId
     // tile start = (superblock totals before the tile) + tile prefix inside its superblock, for
     // output / packed input.  The superblock totals the workgroup has not yet summed come as
     // per-lane partials (po, pi); tile_prepare reduces them: an add here would wait on these
@@ -434,7 +462,8 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
     uint32_t pe_rec;               // end of the record's composed bytes (clipped to the capacity)
     uint64_t in0;                  // packed: the record's first string byte
     uint32_t L[5];
-    uint64_t ts;
+    uint64_t ts;                   // timestamp (default applied) / Lite sequence
+    uint32_t tid;                  // Lite topicId
     uint64_t T0;                   // tile output start (uniform)
     uint32_t len;                  // tile output bytes, clipped to the capacity (uniform)
     uint32_t agg_in;               // packed: staged-input limit, bytes from in_tile (uniform)
@@ -444,7 +473,7 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
 
 // sb_next: the first superblock whose total this workgroup has not loaded yet (tiles come in
 // increasing order; a clamped repeat of the last tile loads nothing new)
-template <bool kPacked>
+template <class LY, bool kPacked>
 __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane, uint64_t& sb_next) {
     TileIn x;
     // unconditional loads at a clamped index: a select on the loaded value here would make the
@@ -452,8 +481,9 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
     uint64_t r = tile * kRpt + lane / kLpr;
     r = r < a.n ? r : a.n - 1;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) x.L[f] = a.str_len[5 * r + f];
+    for (int f = 0; f < 5; ++f) x.L[f] = f < LY::kNF ? a.str_len[LY::kNF * r + f] : 0u;
     x.ts = a.timestamp[r];
+    x.tid = LY::kTM ? 0u : a.topic_id[r];
     x.to = a.tsum[2 * tile];  // uniform: scalar loads
     x.ti = kPacked ? a.tsum[2 * tile + 1] : 0ull;
     // totals of superblocks [sb_next, tile's superblock): lane l loads superblock sb_next + l at a
@@ -471,7 +501,7 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
 }
 
 // sp_out / sp_in: running totals of the superblocks before this workgroup's current tile
-template <bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, bool kTrunc>
 __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
                                                uint64_t& sp_out, uint64_t& sp_in) {
     TileSt S;
@@ -486,9 +516,9 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
         sum += S.L[f];
     }
 #pragma unroll
-    for (int f = 4; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
+    for (int f = LY::kNF - 1; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
         if (S.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
-    const uint32_t ovh = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+    const uint32_t ovh = (uint32_t)LY::ovh(kTrunc);
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
     sp_out += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull));
@@ -504,7 +534,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
         // every record of the tile encodable: input offsets follow the output ones (34 B apart
         // per record); otherwise (E109 / past the end) a 64-bit scan of the input sizes
         if (__ballot(!(valid && st == SBE_ENC_OK)) == 0) {
-            const uint32_t ovh0 = kTrunc ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
+            const uint32_t ovh0 = ovh;
             S.in0 = S.rs - ovh0 * (uint32_t)(lane / kLpr);
             const uint64_t agg_in = agg_out - (uint64_t)ovh0 * kRpt;
             S.agg_in = (uint32_t)agg_in;
@@ -519,7 +549,8 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
         S.agg_in = 0;
         S.in0 = 0;
     }
-    S.ts = (valid && x.ts) ? x.ts : a.ts_default;
+    S.ts = LY::kTM ? ((valid && x.ts) ? x.ts : a.ts_default) : x.ts;
+    S.tid = x.tid;
     const uint32_t re = S.rs + rec_out;
     const uint64_t cap_rel64 = a.cap > base_out ? a.cap - base_out : 0ull;
     const uint32_t cap_rel = cap_rel64 < (uint64_t)agg_out ? (uint32_t)cap_rel64 : agg_out;
@@ -541,7 +572,8 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     if (!kPacked) {
 #pragma unroll
         for (int f = 0; f < 5; ++f)
-            S.gsrc[f] = reinterpret_cast<uintptr_t>(a.arena) + (valid ? a.str_off[5 * r + f] : 0u);
+            S.gsrc[f] = reinterpret_cast<uintptr_t>(a.arena) +
+                        ((valid && f < LY::kNF) ? a.str_off[LY::kNF * r + f] : 0u);
     }
     return S;
 }
@@ -550,8 +582,9 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
 __device__ __forceinline__ bool single_window(const TileSt& S) { return S.len + (uint32_t)(S.T0 & 15) <= (uint32_t)kEW; }
 
 // Staged input range for the output window starting wrel bytes from T0: from the first string
-// byte at/after max(wrel, 0) (input offset >= p - 34 within the record holding it) for kEWIn
+// byte at/after max(wrel, 0) (input offset >= p - kOvh within the record holding it) for kEWIn
 // bytes, clipped to the tile's input.
+template <class LY>
 __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int lane, uintptr_t& swb,
                                             int32_t& nbytes) {
     const uint32_t g = wrel > 0 ? (uint32_t)wrel : 0u;
@@ -561,7 +594,7 @@ __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int l
     const uint32_t ra_rs = __builtin_amdgcn_readfirstlane(__shfl(S.rs, ra, kWave));
     const uint64_t ra_in = uniform64(__shfl(S.in0, ra, kWave));
     const uint32_t p = g - ra_rs;
-    const uintptr_t first = S.in_tile + ra_in + (p > 34 ? p - 34 : 0);
+    const uintptr_t first = S.in_tile + ra_in + (p > (uint32_t)LY::kOvh ? p - (uint32_t)LY::kOvh : 0);
     swb = first & ~(uintptr_t)15;
     const uintptr_t lim = (S.in_tile + S.agg_in + 15) & ~(uintptr_t)15;
     const uintptr_t swe = swb + kEWIn < lim ? swb + kEWIn : (lim > swb ? lim : swb);
@@ -597,12 +630,38 @@ __device__ __forceinline__ void stage_write(lds_u8* inb, int32_t nbytes, int lan
     }
 }
 
+// Dword j (compile-time after unrolling) of a record's literal prefix:
+//  session header {24, 1, 111, 8}, leadershipTermId, clusterSessionId, timestamp 0
+//    (src/session_manager.cpp:936-967, :1018-1046);
+//  SBE header {blockLength, templateId, schemaId 1, version 1} (TopicMessage.h:221-238);
+//  block: TopicMessage timestamp, sequenceNumber 0 (:362-437) / Lite u32 topicId, u64 sequence
+//    (CommitOffsetLite.h:337-420).
+template <class LY>
+__device__ __forceinline__ uint32_t lit_word(const EncArgs& a, const TileSt& S, int j) {
+    if (j < LY::kPre / 4) {
+        switch (j) {
+            case 0: return SBE_SESSION_BLOCK_LEN | (SBE_SESSION_TEMPLATE_ID << 16);
+            case 1: return SBE_CLUSTER_SCHEMA_ID | (SBE_CLUSTER_SCHEMA_VERSION << 16);
+            case 2: return (uint32_t)(uint64_t)a.term_id;
+            case 3: return (uint32_t)((uint64_t)a.term_id >> 32);
+            case 4: return (uint32_t)(uint64_t)a.sess_id;
+            case 5: return (uint32_t)((uint64_t)a.sess_id >> 32);
+            default: return 0u;
+        }
+    }
+    j -= LY::kPre / 4;
+    if (j == 0) return (uint32_t)LY::kBlk | ((LY::kTM ? SBE_TM_TEMPLATE_ID : a.tmpl) << 16);
+    if (j == 1) return SBE_TOPIC_SCHEMA_ID | (1u << 16);
+    if (LY::kTM) return j == 2 ? (uint32_t)S.ts : (j == 3 ? (uint32_t)(S.ts >> 32) : 0u);
+    return j == 2 ? S.tid : (j == 3 ? (uint32_t)S.ts : (uint32_t)(S.ts >> 32));
+}
+
 // compose this lane's part [ps, pe) of its record, clipped to output window [wb, we); record
 // layout TopicMessage.h:221-238 (header), :362-437 (timestamp, sequenceNumber 0), :515-1231
 // (u16 length + bytes per string)
-template <bool kPacked>
-__device__ __forceinline__ void compose(lds_u8* wout, lds_cu8* inb, const TileSt& S, int32_t wrel, int32_t we_rel,
-                                        uintptr_t swb, int32_t win_bytes) {
+template <class LY, bool kPacked>
+__device__ __forceinline__ void compose(const EncArgs& a, lds_u8* wout, lds_cu8* inb, const TileSt& S, int32_t wrel,
+                                        int32_t we_rel, uintptr_t swb, int32_t win_bytes) {
     if (!(S.rec_out && S.ps < S.pe && (int32_t)S.ps < we_rel && (int32_t)S.pe > wrel)) return;
     const int32_t R0 = (int32_t)S.rs - wrel;
     const int32_t pl = (int32_t)S.ps - wrel;
@@ -611,24 +670,19 @@ __device__ __forceinline__ void compose(lds_u8* wout, lds_cu8* inb, const TileSt
     Writer W{wout, lo, lo, 0u};
     int32_t x = lo - R0;  // record-relative position of W.pos
     const int32_t end = hi - R0;
-    {
-        const uint64_t hdr = (uint64_t)(SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16)) |
-                             ((uint64_t)(SBE_TOPIC_SCHEMA_ID | (1u << 16)) << 32);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const uint64_t v = j == 0 ? hdr : (j == 1 ? S.ts : 0ull);
-            if (x < 8 * j + 8 && x < end) {
-                const int32_t e = end < 8 * j + 8 ? end : 8 * j + 8;
-                W.lit(low_bytes64(v >> (8 * (x - 8 * j)), e - x), e - x);
-                x = e;
-            }
+    for (int j = 0; j < LY::kLit / 4; ++j) {
+        if (x < 4 * j + 4 && x < end) {
+            const int32_t e = end < 4 * j + 4 ? end : 4 * j + 4;
+            W.lit(low_bytes64((uint64_t)lit_word<LY>(a, S, j) >> (8 * (x - 4 * j)), e - x), e - x);
+            x = e;
         }
     }
-    int32_t o = 24;
+    int32_t o = LY::kLit;
     const int64_t src0 = kPacked ? (int64_t)(S.in_tile + S.in0) - (int64_t)swb : 0;
     int64_t src = src0;
 #pragma nounroll
-    for (int f = 0; f < 5; ++f) {
+    for (int f = 0; f < LY::kNF; ++f) {
         if (x >= end) break;
         const uint32_t Lu = f == 0 ? S.L[0] : f == 1 ? S.L[1] : f == 2 ? S.L[2] : f == 3 ? S.L[3] : S.L[4];
         const int32_t Lf = (int32_t)Lu;
@@ -809,6 +863,7 @@ __device__ __forceinline__ void put_clip(lds_u8* wout, int32_t d, uint32_t v, in
 
 // Record table, bucket table and per-record absolute string bases for one window; returns true
 // (wave-uniform) when some record of the window has strings outside the staged input.
+template <class LY>
 __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t* sbase, const TileSt& S,
                                              int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int lane) {
     const int q = lane % kLpr, r = lane / kLpr;
@@ -827,13 +882,23 @@ __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t*
         i32x4 a, b;
         a.x = rw;
         a.y = rend;
-        a.z = staged ? rw + 26 - (int32_t)src0 : 0;
-        int32_t z = 26;
-        z += (int32_t)S.L[0] + 2; a.w = z;
-        z += (int32_t)S.L[1] + 2; b.x = z;
-        z += (int32_t)S.L[2] + 2; b.y = z;
-        z += (int32_t)S.L[3] + 2; b.z = z;
-        b.w = (z + (int32_t)S.L[4]) | (staged ? 0 : kNotStaged);
+        a.z = staged ? rw + LY::kS0 - (int32_t)src0 : 0;
+        // string starts z_1..z_4 (record-relative); fields the layout lacks start at the end
+        int32_t zs[5];
+        int32_t z = LY::kS0;
+#pragma unroll
+        for (int f = 1; f < 5; ++f) {
+            if (f < LY::kNF) z += (int32_t)S.L[f - 1] + 2;
+            zs[f - 1] = z;
+        }
+        zs[4] = z + (int32_t)S.L[LY::kNF - 1];
+#pragma unroll
+        for (int f = LY::kNF; f < 5; ++f) zs[f - 1] = zs[4];
+        a.w = zs[0];
+        b.x = zs[1];
+        b.y = zs[2];
+        b.z = zs[3];
+        b.w = zs[4] | (staged ? 0 : kNotStaged);
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0] = a;
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = b;
         sbase[r] = s0;
@@ -899,6 +964,7 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
 // the chunks of records whose strings are not all staged, from HBM (rare: a record straddling a
 // window of a multi-window tile, or valid records behind E109 records with large strings)
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
+template <class LY>
 __device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i32* bk, const lds_u64* sbase,
                                                int32_t wlen, int lane) {
     int32_t r = bk[lane];
@@ -915,14 +981,15 @@ __device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i3
         const int32_t X = p - E.rw;
         const int32_t f = zone_of(E, X);
         const uint64_t s0 = sbase[r];
-        const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - 34);
-        const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - 26 - 2 * f), s0 & ~3ull,
+        const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - LY::kOvh);
+        const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - LY::kS0 - 2 * f), s0 & ~3ull,
                                   (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
         *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
 
 // string starts 1..4 inside a chunk: bytes [z_f, min(chunk end, end of string f)) from zone f
+template <class LY>
 __device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, const uint64_t* sbase,
                                            const TileSt& S, int32_t wlen, int32_t nb, int lane) {
     const int q = lane % kLpr, r = lane / kLpr;
@@ -933,11 +1000,11 @@ __device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
     const int32_t imax = (nb + kInSlack) / 4 - 5;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < LY::kNF - 1; ++j) {
         if (j % kLpr != q) continue;
         const int f = j + 1;
         const int32_t A = E.rw + zat(E, j);
-        const int32_t Lf = (j + 1 < 4 ? zat(E, j + 1) - 2 : zend) - zat(E, j);  // length of string f
+        const int32_t Lf = (j + 1 < LY::kNF - 1 ? zat(E, j + 1) - 2 : zend) - zat(E, j);  // length of string f
         int32_t B = (A | 15) + 1;
         if (A + Lf < B) B = A + Lf;
         if (hi_all < B) B = hi_all;
@@ -949,8 +1016,8 @@ __device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
             v = chunk_lds(inb, d0 - E.sh0 - 2 * f, imax);
         } else {
             const uint64_t s0 = sbase[r];
-            const uint32_t nstr = (uint32_t)(zend - 34);
-            v = chunk_glb(s0 + (uint64_t)(int64_t)(d0 - E.rw - 26 - 2 * f), s0 & ~3ull,
+            const uint32_t nstr = (uint32_t)(zend - LY::kOvh);
+            v = chunk_glb(s0 + (uint64_t)(int64_t)(d0 - E.rw - LY::kS0 - 2 * f), s0 & ~3ull,
                           (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
         }
         put_clip(wout, d0, v.x, lo, B);
@@ -960,30 +1027,31 @@ __device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     }
 }
 
-// header {16,1,1,1}, timestamp, sequenceNumber 0 (TopicMessage.h:221-238, :362-437) and the five
-// u16 lengths (:515-1231), clipped to the window and the record's composed bytes
-__device__ __forceinline__ void literal_pass(lds_u8* wout, lds_i32* rt, const TileSt& S, int32_t wlen, int lane) {
+// the literal prefix (lit_word) and the u16 lengths (TopicMessage.h:515-1231), clipped to the
+// window and the record's composed bytes
+template <class LY>
+__device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, lds_i32* rt, const TileSt& S,
+                                             int32_t wlen, int lane) {
     const int q = lane % kLpr, r = lane / kLpr;
     if (!S.rec_out) return;
     const RecEnt E = rec_load(rt, r);
     const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
     const int32_t lo_all = E.rw > 0 ? E.rw : 0;
     if (q == 0) {
-        const uint32_t H[6] = {SBE_TM_BLOCK_LEN | (SBE_TM_TEMPLATE_ID << 16), SBE_TOPIC_SCHEMA_ID | (1u << 16),
-                               (uint32_t)S.ts, (uint32_t)(S.ts >> 32), 0u, 0u};
+        constexpr int kW = LY::kLit / 4;
         const int32_t a = E.rw & 3, d0 = E.rw - a;
-        const int32_t hi = E.rw + 24 < hi_all ? E.rw + 24 : hi_all;
+        const int32_t hi = E.rw + LY::kLit < hi_all ? E.rw + LY::kLit : hi_all;
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-            const uint32_t cur = j < 6 ? H[j] : 0u, prv = j > 0 ? H[j - 1] : 0u;
+        for (int j = 0; j <= kW; ++j) {
+            const uint32_t cur = j < kW ? lit_word<LY>(ea, S, j) : 0u, prv = j > 0 ? lit_word<LY>(ea, S, j - 1) : 0u;
             const uint32_t v = a ? __builtin_amdgcn_alignbyte(cur, prv, 4u - (uint32_t)a) : cur;
             put_clip(wout, d0 + 4 * j, v, lo_all, hi);
         }
     }
     if (q == (kLpr > 1 ? 1 : 0)) {
 #pragma unroll
-        for (int f = 0; f < 5; ++f) {
-            const int32_t P = E.rw + (f == 0 ? 24 : zat(E, f - 1) - 2);
+        for (int f = 0; f < LY::kNF; ++f) {
+            const int32_t P = E.rw + (f == 0 ? LY::kLit : zat(E, f - 1) - 2);
             const uint32_t L = S.L[f] & 0xffffu;
             const int32_t lo = P > lo_all ? P : lo_all;
             const int32_t hi = P + 2 < hi_all ? P + 2 : hi_all;
@@ -998,25 +1066,26 @@ __device__ __forceinline__ void literal_pass(lds_u8* wout, lds_i32* rt, const Ti
     }
 }
 
-__device__ __forceinline__ void pack_window(lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk, uint64_t* sbase,
-                                            const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
-                                            int lane) {
-    const bool outside = build_tables(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
+template <class LY>
+__device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk,
+                                            uint64_t* sbase, const TileSt& S, int32_t wrel, int32_t wlen,
+                                            uintptr_t swb, int32_t nb, int lane) {
+    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
     wsync();
 #ifndef SBE_ABL_NO_CHUNK
     chunk_pass(wout, inb, rt, bk, wlen, nb, lane);
-    if (outside) chunk_pass_global(wout, rt, bk, (const lds_u64*)sbase, wlen, lane);
+    if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, lane);
 #endif
     wsync();
 #ifndef SBE_ABL_NO_FIXUP
-    fixup_pass(wout, inb, rt, sbase, S, wlen, nb, lane);
+    fixup_pass<LY>(wout, inb, rt, sbase, S, wlen, nb, lane);
 #endif
 #ifndef SBE_ABL_NO_LITERAL
-    literal_pass(wout, rt, S, wlen, lane);
+    literal_pass<LY>(ea, wout, rt, S, wlen, lane);
 #endif
 }
 
-template <bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, bool kTrunc>
 __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
@@ -1034,14 +1103,14 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
     if (t >= ntiles) return;
 
     uint64_t sb_next = 0, sp_out = 0, sp_in = 0;
-    TileIn x = tile_load<kPacked>(a, t, lane, sb_next);
-    TileSt S = tile_prepare<kPacked, kTrunc>(a, x, t, lane, sp_out, sp_in);
+    TileIn x = tile_load<LY, kPacked>(a, t, lane, sb_next);
+    TileSt S = tile_prepare<LY, kPacked, kTrunc>(a, x, t, lane, sp_out, sp_in);
     uint4 I[kStageRegs];
     uintptr_t swb = 0;
     int32_t nb = 0;
     bool fast = kPacked && single_window(S);
     if (fast) {
-        stage_range(S, -(int32_t)(S.T0 & 15), lane, swb, nb);
+        stage_range<LY>(S, -(int32_t)(S.T0 & 15), lane, swb, nb);
     } else {
         swb = reinterpret_cast<uintptr_t>(a.sink);
         nb = 0;
@@ -1051,7 +1120,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         stage_write(win_in, nb, lane, I);
     }
     uint64_t tn = t + G;
-    x = tile_load<kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane, sb_next);
+    x = tile_load<LY, kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane, sb_next);
 
     // Steady state, per tile: [next tile: prepare, lengths of the one after, staging loads]
     // [compose + store this tile] [next tile's staged input → LDS].  The staging registers are
@@ -1063,12 +1132,12 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         const bool have_next = tn < ntiles;
         TileSt Sn;
         if (have_next) {
-            Sn = tile_prepare<kPacked, kTrunc>(a, x, tn, lane, sp_out, sp_in);
+            Sn = tile_prepare<LY, kPacked, kTrunc>(a, x, tn, lane, sp_out, sp_in);
             const uint64_t t2 = tn + G;
-            x = tile_load<kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
+            x = tile_load<LY, kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
             fast = kPacked && single_window(Sn);
             if (fast) {
-                stage_range(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
+                stage_range<LY>(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
             } else {
                 swb = reinterpret_cast<uintptr_t>(a.sink);
                 nb = 0;
@@ -1079,10 +1148,10 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         const int32_t wrel0 = -(int32_t)(S.T0 & 15);
         if (cur_fast) {
             if (kPacked) {
-                pack_window(wout, win_in, rt, bk, sbase, S, wrel0, (int32_t)S.len - wrel0, cur_swb, cur_nb, lane);
+                pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, wrel0, (int32_t)S.len - wrel0, cur_swb, cur_nb, lane);
             } else {
                 wsync();
-                compose<false>(wout, win_in, S, wrel0, (int32_t)S.len, cur_swb, cur_nb);
+                compose<LY, false>(a, wout, win_in, S, wrel0, (int32_t)S.len, cur_swb, cur_nb);
             }
             wsync();
 #ifndef SBE_ABL_NO_STORE
@@ -1095,7 +1164,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                 uintptr_t sw = 0;
                 int32_t nbw = 0;
                 if (kPacked) {
-                    stage_range(S, wrel, lane, sw, nbw);
+                    stage_range<LY>(S, wrel, lane, sw, nbw);
                     // I holds the next tile's prefetch: stage this window in batches of 3 chunks
                     for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
                         uint4 J[3];
@@ -1112,10 +1181,10 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                     }
                 }
                 if (kPacked) {
-                    pack_window(wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
+                    pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
                 } else {
                     wsync();
-                    compose<false>(wout, win_in, S, wrel, we_rel, sw, nbw);
+                    compose<LY, false>(a, wout, win_in, S, wrel, we_rel, sw, nbw);
                 }
                 wsync();
                 store_window(a.out, a.sink, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
@@ -1483,6 +1552,49 @@ __device__ void dec_on_egress(const R_t& R, uint32_t len, Desc& d) {
     d.status = SBE_ST_EG_TM;
 }
 
+// The Lite templates' generated decode flyweights in field order (CommitOffsetLite.h:240-276,
+// :337-420, :528-540; OrderRequestLite.h / OrderNotificationLite.h likewise): wrapForDecode(buf,
+// 8, blockLength, version, len), topicId @8, sequence @12, getXAsString per var field (E100 past
+// len).  The 12 fixed bytes must lie inside the record (the flyweight reads them unchecked).
+template <typename R_t>
+__device__ void dec_lite(const R_t& R, uint32_t len, Desc& d) {
+    d.clear();
+    if (len < 8) { d.status = SBE_ST_LITE_NOT_LITE; return; }
+    const uint32_t h0 = R.u32(0), h1 = R.u32(4);
+    const uint32_t blk = h0 & 0xffffu, tmpl = h0 >> 16, schema = h1 & 0xffffu;
+    d.set_hdr(R, 0);
+    const uint32_t nf = tmpl == SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID ? 2u
+                      : (tmpl == SBE_ORDER_REQUEST_LITE_TEMPLATE_ID || tmpl == SBE_ORDER_NOTIFICATION_LITE_TEMPLATE_ID) ? 3u
+                                                                                                                   : 0u;
+    if (schema != 1 || nf == 0) { d.status = SBE_ST_LITE_NOT_LITE; return; }
+    uint32_t pos = 8u + blk;
+    if (pos > len || len < 20) { d.status = SBE_ST_LITE_E100; return; }
+#pragma unroll
+    for (uint32_t f = 0; f < 3; ++f) {
+        if (f >= nf) break;
+        if (pos + 2 > len) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) d.off[k] = d.len[k] = 0;
+            d.status = SBE_ST_LITE_E100;
+            return;
+        }
+        const uint32_t L = R.u16(pos);
+        pos += 2;
+        if (pos + L > len) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) d.off[k] = d.len[k] = 0;
+            d.status = SBE_ST_LITE_E100;
+            return;
+        }
+        d.off[f] = pos;
+        d.len[f] = L;
+        pos += L;
+    }
+    d.status = SBE_ST_LITE;
+    d.ts = R.u64(12);
+    d.off[4] = R.u32(8);
+}
+
 #ifndef SBE_DEC_PERSIST
 #define SBE_DEC_PERSIST 0  // measured: the persistent form was 6-10 % slower (hardware WG dispatch overlaps better)
 #endif
@@ -1557,17 +1669,23 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint32_t* win, const 
     if (!valid) {
     } else if (rl > 0xffffffffull) {  // records beyond u32 sizes are not SBE frames we can bound-check in 32 bits
         d.clear();
-        d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE : SBE_ST_ERR_TM_E100;
+        d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE
+                 : kMode == SBE_DEC_LITE    ? SBE_ST_LITE_E100
+                                            : SBE_ST_ERR_TM_E100;
     } else if (rs >= wb && rs + rl <= we) {
         const LdsRec R{win, (uint32_t)(rs - wb)};
         if (kMode == SBE_DEC_ON_EGRESS)
             dec_on_egress(R, (uint32_t)rl, d);
+        else if (kMode == SBE_DEC_LITE)
+            dec_lite(R, (uint32_t)rl, d);
         else
             dec_parse_message(R, (uint32_t)rl, d);
     } else {
         const GlbRec R{reinterpret_cast<uintptr_t>(a.in) + rs};
         if (kMode == SBE_DEC_ON_EGRESS)
             dec_on_egress(R, (uint32_t)rl, d);
+        else if (kMode == SBE_DEC_LITE)
+            dec_lite(R, (uint32_t)rl, d);
         else
             dec_parse_message(R, (uint32_t)rl, d);
     }
@@ -1740,6 +1858,67 @@ void prof_commit(int which, hipEvent_t start) {
     if (R.count < ProfRing::kCap) ++R.count;
 }
 
+// One encode request, whatever the layout (the C entry points fill it).
+struct EncReq {
+    const uint8_t* arena;
+    const uint32_t* str_off;
+    const uint32_t* str_len;
+    const uint64_t* ts;   // timestamp / sequence
+    const uint32_t* tid;  // Lite topicId
+    uint32_t tmpl;
+    int64_t term_id, sess_id;
+};
+
+size_t enc_workspace_size(uint64_t n) {
+    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
+    const uint64_t tiles = sbs * kTilesPerSb;
+    return (size_t)(16 * (tiles + sbs) + kSinkBytes + 16);
+}
+
+template <class LY, bool kPacked, bool kTrunc>
+void enc_launch_k(const EncArgs& a, uint64_t sbs, uint64_t tiles, hipStream_t s) {
+    const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<LY, kPacked, kTrunc>), tiles);
+    hipLaunchKernelGGL((sbe_enc_sums<LY, kPacked, kTrunc>), dim3((uint32_t)sbs), dim3(kSbThreads), 0, s, a);
+    hipEvent_t e0, e1;
+    prof_slot(0, &e0, &e1);
+    hipExtLaunchKernelGGL((sbe_enc_pack<LY, kPacked, kTrunc>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a);
+    prof_commit(0, e0);
+}
+
+// Argument checks, workspace carving and the two launches (sums, pack) of one encode call.
+template <class LY>
+int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out, uint64_t out_capacity,
+               uint64_t* out_off, uint8_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!out_off) return SBE_EINVAL;
+    if (flags & ~SBE_ENC_REF_TRUNCATE8) return SBE_EINVAL;
+    if (!LY::kTM && flags) return SBE_EINVAL;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
+    if (!q.str_len || !q.ts || !q.arena || !out) return SBE_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
+    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
+    const uint64_t tiles = (n + kRpt - 1) / kRpt;
+    if (tiles > kMaxTiles) return SBE_EINVAL;
+    if (!workspace || workspace_bytes < enc_workspace_size(n)) return SBE_ENOSPC;
+    if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
+    uint64_t* ws = static_cast<uint64_t*>(workspace);
+    EncArgs a{q.arena, q.str_off, q.str_len, q.ts, q.tid, q.tmpl, q.term_id, q.sess_id, n, ts_default,
+              out,     out_capacity, out_off, status, ws, ws + 2 * sbs * kTilesPerSb,
+              reinterpret_cast<uint8_t*>(ws + 2 * sbs * (kTilesPerSb + 1))};
+    const bool packed = q.str_off == nullptr;
+    const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
+    if (LY::kTM) {
+        if (packed && !trunc) enc_launch_k<LY, true, false>(a, sbs, tiles, s);
+        else if (packed && trunc) enc_launch_k<LY, true, true>(a, sbs, tiles, s);
+        else if (!packed && !trunc) enc_launch_k<LY, false, false>(a, sbs, tiles, s);
+        else enc_launch_k<LY, false, true>(a, sbs, tiles, s);
+    } else {
+        if (packed) enc_launch_k<LY, true, false>(a, sbs, tiles, s);
+        else enc_launch_k<LY, false, false>(a, sbs, tiles, s);
+    }
+    return record_hip(hipGetLastError());
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -1763,15 +1942,11 @@ int sbe_device_ready(void) {
     return 0;
 }
 
-size_t sbe_encode_workspace_size(uint64_t n) {
-    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
-    const uint64_t tiles = sbs * kTilesPerSb;
-    return (size_t)(16 * (tiles + sbs) + kSinkBytes + 16);
-}
+size_t sbe_encode_workspace_size(uint64_t n) { return enc_workspace_size(n); }
 
 uint64_t sbe_encode_output_bound(uint64_t n, uint64_t string_bytes, uint32_t flags) {
-    (void)flags;
-    return string_bytes + (uint64_t)SBE_TM_WIRE_OVERHEAD * n;
+    (void)flags;  // the wire length bounds the truncated one; session framing adds 32 B a record
+    return string_bytes + (uint64_t)(SBE_TM_WIRE_OVERHEAD + SBE_SESSION_HDR_LEN) * n;
 }
 
 int sbe_encode_workspace_init(void* workspace, size_t workspace_bytes, void* stream) {
@@ -1782,43 +1957,51 @@ int sbe_encode_workspace_init(void* workspace, size_t workspace_bytes, void* str
 int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
                            uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
                            void* workspace, size_t workspace_bytes, void* stream) {
-    if (!in || !out_off) return SBE_EINVAL;
-    if (flags & ~SBE_ENC_REF_TRUNCATE8) return SBE_EINVAL;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
-    if (!in->str_len || !in->timestamp || !in->arena || !out) return SBE_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
-    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
-    const uint64_t tiles = (n + kRpt - 1) / kRpt;
-    if (tiles > kMaxTiles) return SBE_EINVAL;
-    if (!workspace || workspace_bytes < sbe_encode_workspace_size(n)) return SBE_ENOSPC;
-    if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
-    uint64_t* ws = static_cast<uint64_t*>(workspace);
-    EncArgs a{in->arena, in->str_off, in->str_len, in->timestamp, n,  ts_default,
-              out,       out_capacity, out_off,   status,        ws, ws + 2 * sbs * kTilesPerSb,
-              reinterpret_cast<uint8_t*>(ws + 2 * sbs * (kTilesPerSb + 1))};
-    const bool packed = in->str_off == nullptr;
-    const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
-#define SBE_ENC_LAUNCH(P, T)                                                                          \
-    do {                                                                                              \
-        const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<P, T>), tiles);   \
-        hipLaunchKernelGGL((sbe_enc_sums<P, T>), dim3((uint32_t)sbs), dim3(kSbThreads), 0, s, a);     \
-        hipEvent_t e0, e1;                                                                            \
-        prof_slot(0, &e0, &e1);                                                                       \
-        hipExtLaunchKernelGGL((sbe_enc_pack<P, T>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a); \
-        prof_commit(0, e0);                                                                               \
-    } while (0)
-    if (packed && !trunc) SBE_ENC_LAUNCH(true, false);
-    else if (packed && trunc) SBE_ENC_LAUNCH(true, true);
-    else if (!packed && !trunc) SBE_ENC_LAUNCH(false, false);
-    else SBE_ENC_LAUNCH(false, true);
-#undef SBE_ENC_LAUNCH
-    return record_hip(hipGetLastError());
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, 0, 0};
+    return enc_launch<LayTM>(q, n, ts_default, flags, out, out_capacity, out_off, status, workspace,
+                             workspace_bytes, stream);
+}
+
+int sbe_encode_session_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
+                             int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, leadership_term_id, cluster_session_id};
+    return enc_launch<LayTMS>(q, n, ts_default, flags, out, out_capacity, out_off, status, workspace,
+                              workspace_bytes, stream);
+}
+
+uint32_t sbe_lite_fields(uint32_t template_id) {
+    switch (template_id) {
+        case SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID: return 2;
+        case SBE_ORDER_REQUEST_LITE_TEMPLATE_ID:
+        case SBE_ORDER_NOTIFICATION_LITE_TEMPLATE_ID: return 3;
+        default: return 0;
+    }
+}
+
+uint64_t sbe_lite_output_bound(uint64_t n, uint64_t string_bytes, uint32_t template_id) {
+    const uint32_t nf = sbe_lite_fields(template_id);
+    return string_bytes + (uint64_t)SBE_LITE_OVERHEAD(nf ? nf : 3) * n;
+}
+
+int sbe_encode_lite_batch(const sbe_lite_batch* in, uint64_t n, uint32_t template_id, uint8_t* out,
+                          uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+    const uint32_t nf = sbe_lite_fields(template_id);
+    if (!in || nf == 0) return SBE_EINVAL;
+    if (n && !in->topic_id) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->sequence, in->topic_id, template_id, 0, 0};
+    if (nf == 2)
+        return enc_launch<LayL2>(q, n, 0, 0, out, out_capacity, out_off, status, workspace, workspace_bytes, stream);
+    return enc_launch<LayL3>(q, n, 0, 0, out, out_capacity, out_off, status, workspace, workspace_bytes, stream);
 }
 
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream) {
-    if (mode != SBE_DEC_PARSE_MESSAGE && mode != SBE_DEC_ON_EGRESS) return SBE_EINVAL;
+    if (mode != SBE_DEC_PARSE_MESSAGE && mode != SBE_DEC_ON_EGRESS && mode != SBE_DEC_LITE) return SBE_EINVAL;
     if (n == 0) return SBE_OK;
     if (!in || !rec_off || !out || !out->status || !out->flags || !out->hdr || !out->ts || !out->view_off ||
         !out->view_len)
@@ -1843,6 +2026,8 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     prof_slot(1, &e0, &e1);
     if (mode == SBE_DEC_ON_EGRESS)
         hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_ON_EGRESS>), grid, block, 0, s, e0, e1, 0, a);
+    else if (mode == SBE_DEC_LITE)
+        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_LITE>), grid, block, 0, s, e0, e1, 0, a);
     else
         hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, e0, e1, 0, a);
     prof_commit(1, e0);

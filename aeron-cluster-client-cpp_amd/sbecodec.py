@@ -6,6 +6,11 @@ module without the built library, or calling it without a gfx950 device, raises.
 
 Reference surface mirrored (paths relative to the reference tree):
   encode_topic_batch  ~ SBEEncoder::encode_topic_message   src/sbe_encoder.cpp:131-167
+  encode_session_batch~ SessionManager create_topic_message + send_combined_message framing
+                        src/session_manager.cpp:936-967, :1050-1144
+  encode_lite_batch   ~ CommitManager::build_commit_offset_message (CommitOffsetLite)
+                        src/commit_manager.cpp:107-132; OrderRequestLite / OrderNotificationLite
+  decode_batch(LITE)  ~ the Lite templates' generated decode flyweights
   decode_batch(PARSE) ~ MessageParser::parse_message        src/sbe_encoder.cpp:513-551
   decode_batch(EGRESS)~ decode_ack + MessageHandler::on_egress
                         src/ack_decoder.cpp:29-105, include/aeron_cluster/message_handler.hpp:35-68
@@ -22,11 +27,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 1
+ABI_VERSION = 2
 ENC_REF_TRUNCATE8 = 0x1
 ENC_OK, ENC_OVERFLOW = 0, 6
-DEC_PARSE_MESSAGE, DEC_ON_EGRESS = 0, 1
+DEC_PARSE_MESSAGE, DEC_ON_EGRESS, DEC_LITE = 0, 1, 2
 TM_WIRE_OVERHEAD, TM_REF_OVERHEAD = 34, 26
+SESSION_HDR_LEN = 32
+COMMIT_OFFSET_LITE, ORDER_REQUEST_LITE, ORDER_NOTIFICATION_LITE = 301, 201, 202
+LITE_FIELDS = {COMMIT_OFFSET_LITE: 2, ORDER_REQUEST_LITE: 3, ORDER_NOTIFICATION_LITE: 3}
+ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
 
 ST_TM, ST_ACK, ST_SESSION_EVENT = 0, 1, 2
 ST_ERR_NULL_EMPTY, ST_ERR_HEADER, ST_ERR_UNKNOWN_TYPE = 16, 17, 18
@@ -46,6 +55,11 @@ class SbeError(RuntimeError):
 class _TmBatch(ctypes.Structure):
     _fields_ = [("arena", ctypes.c_void_p), ("str_off", ctypes.c_void_p),
                 ("str_len", ctypes.c_void_p), ("timestamp", ctypes.c_void_p)]
+
+
+class _LiteBatch(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("str_off", ctypes.c_void_p), ("str_len", ctypes.c_void_p),
+                ("topic_id", ctypes.c_void_p), ("sequence", ctypes.c_void_p)]
 
 
 class _Decoded(ctypes.Structure):
@@ -72,6 +86,22 @@ def _load():
         ctypes.POINTER(_TmBatch), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    if not hasattr(lib, "sbe_encode_session_batch"):  # an older build loaded for A/B timing only
+        return lib if lib.sbe_abi_version() == ABI_VERSION else _abi_mismatch()
+    lib.sbe_encode_session_batch.restype = ctypes.c_int
+    lib.sbe_encode_session_batch.argtypes = [
+        ctypes.POINTER(_TmBatch), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.sbe_lite_fields.restype = ctypes.c_uint32
+    lib.sbe_lite_fields.argtypes = [ctypes.c_uint32]
+    lib.sbe_lite_output_bound.restype = ctypes.c_uint64
+    lib.sbe_lite_output_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+    lib.sbe_encode_lite_batch.restype = ctypes.c_int
+    lib.sbe_encode_lite_batch.argtypes = [
+        ctypes.POINTER(_LiteBatch), ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.POINTER(_Decoded), ctypes.c_void_p]
@@ -80,8 +110,12 @@ def _load():
     lib.sbe_profile_read.restype = ctypes.c_int
     lib.sbe_profile_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     if lib.sbe_abi_version() != ABI_VERSION:
-        raise SbeError("libsbecodec.so ABI version mismatch")
+        _abi_mismatch()
     return lib
+
+
+def _abi_mismatch():
+    raise SbeError("libsbecodec.so ABI version mismatch")
 
 
 _lib = None
@@ -199,6 +233,72 @@ def encode_topic_batch(arena, str_len, timestamp, str_off=None, flags=0, ts_defa
                                       _ptr(out), out.numel(), _ptr(out_off), _ptr(status),
                                       _ptr(workspace), workspace.numel(), _stream(stream))
     _check(rc, "sbe_encode_topic_batch")
+    return Encoded(out, out_off, None if status is None else status[:n], workspace)
+
+
+def _enc_outputs(n, cap, dev, out, out_off, status, workspace, stream):
+    if out is None:
+        out = torch.empty(max(cap, 16), dtype=torch.uint8, device=dev)
+    if out_off is None:
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    elif status is False:
+        status = None
+    if workspace is None:
+        workspace = alloc_workspace(n, dev, stream)
+    elif workspace.numel() < workspace_size(n):
+        raise SbeError("workspace too small")
+    return out, out_off, status, workspace
+
+
+def encode_session_batch(arena, str_len, timestamp, leadership_term_id, cluster_session_id, str_off=None,
+                         flags=ENC_REF_TRUNCATE8, ts_default=0, out=None, out_off=None, status=None,
+                         workspace=None, stream=None) -> Encoded:
+    """Session-framed TopicMessages: each record is the 32-B SessionMessageHeader followed by the
+    TopicMessage (26+Σlen bytes with ENC_REF_TRUNCATE8, as the live publish path sends it)."""
+    arena = _dev(arena, torch.uint8, "arena")
+    str_len = _dev(str_len, torch.int32, "str_len")
+    timestamp = _dev(timestamp, torch.int64, "timestamp")
+    str_off = _dev(str_off, torch.int32, "str_off")
+    n = int(timestamp.numel())
+    if str_len.numel() != 5 * n:
+        raise SbeError("str_len must have 5 entries per record")
+    out, out_off, status, workspace = _enc_outputs(n, output_bound(n, int(arena.numel()), flags), arena.device,
+                                                   out, out_off, status, workspace, stream)
+    batch = _TmBatch(arena.data_ptr(), None if str_off is None else str_off.data_ptr(),
+                     str_len.data_ptr(), timestamp.data_ptr())
+    rc = lib().sbe_encode_session_batch(ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                        int(leadership_term_id), int(cluster_session_id),
+                                        _ptr(out), out.numel(), _ptr(out_off), _ptr(status),
+                                        _ptr(workspace), workspace.numel(), _stream(stream))
+    _check(rc, "sbe_encode_session_batch")
+    return Encoded(out, out_off, None if status is None else status[:n], workspace)
+
+
+def encode_lite_batch(template_id, arena, str_len, topic_id, sequence, str_off=None, out=None, out_off=None,
+                      status=None, workspace=None, stream=None) -> Encoded:
+    """Lite records (301 CommitOffsetLite, 201 OrderRequestLite, 202 OrderNotificationLite):
+    str_len int32 [n, nf] (u32), topic_id int32 [n] (u32), sequence int64 [n] (u64)."""
+    nf = LITE_FIELDS.get(int(template_id))
+    if nf is None:
+        raise SbeError(f"not a Lite template: {template_id}")
+    arena = _dev(arena, torch.uint8, "arena")
+    str_len = _dev(str_len, torch.int32, "str_len")
+    topic_id = _dev(topic_id, torch.int32, "topic_id")
+    sequence = _dev(sequence, torch.int64, "sequence")
+    str_off = _dev(str_off, torch.int32, "str_off")
+    n = int(sequence.numel())
+    if str_len.numel() != nf * n or topic_id.numel() != n:
+        raise SbeError(f"str_len must have {nf} entries and topic_id one per record")
+    cap = int(lib().sbe_lite_output_bound(n, int(arena.numel()), int(template_id)))
+    out, out_off, status, workspace = _enc_outputs(n, cap, arena.device, out, out_off, status, workspace, stream)
+    batch = _LiteBatch(arena.data_ptr(), None if str_off is None else str_off.data_ptr(), str_len.data_ptr(),
+                       topic_id.data_ptr(), sequence.data_ptr())
+    rc = lib().sbe_encode_lite_batch(ctypes.byref(batch), n, int(template_id), _ptr(out), out.numel(),
+                                     _ptr(out_off), _ptr(status), _ptr(workspace), workspace.numel(),
+                                     _stream(stream))
+    _check(rc, "sbe_encode_lite_batch")
     return Encoded(out, out_off, None if status is None else status[:n], workspace)
 
 

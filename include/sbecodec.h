@@ -18,6 +18,18 @@
  *                                  output records are what ClusterClient::offer_ingress
  *                                  (include/aeron_cluster/cluster_client.hpp:409,
  *                                  src/cluster_client_offer.cpp:11-20) receives one by one.
+ * sbe_encode_session_batch()      SessionManager::Impl::publish_message's frame: create_topic_message
+ *                                  src/session_manager.cpp:1050-1115 behind the 32-B
+ *                                  SessionMessageHeader that send_combined_message prepends
+ *                                  (:936-967 build, :1018-1046 update, :1118-1144 combine).
+ * sbe_encode_lite_batch()         CommitManager::build_commit_offset_message's CommitOffsetLite
+ *                                  encoder src/commit_manager.cpp:107-132 (template 301) and the
+ *                                  OrderRequestLite / OrderNotificationLite flyweights (201 / 202,
+ *                                  include/model/OrderRequestLite.h:114-118, :1020-1050).
+ * sbe_decode_batch(LITE)          the Lite templates' generated decode flyweights
+ *                                  (wrapForDecode + fixed fields + getXAsString in order,
+ *                                  include/model/CommitOffsetLite.h, OrderRequestLite.h,
+ *                                  OrderNotificationLite.h).
  * sbe_decode_batch(PARSE_MESSAGE) MessageParser::parse_message      src/sbe_encoder.cpp:513-551
  *                                  (+ parse_topic_message :724-831, decode_acknowledgment_with_sbe
  *                                  :833-954, decode_topic_message_with_sbe :957-1143,
@@ -37,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 1
+#define SBECODEC_ABI_VERSION 2
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -59,6 +71,15 @@ extern "C" {
 #define SBE_TM_WIRE_OVERHEAD 34u   /* 8 header + 16 block + 5 x u16 length */
 #define SBE_TM_REF_OVERHEAD 26u    /* reference encode_topic_message emits 8 B less */
 #define SBE_VAR_MAX_LEN 65534u     /* TopicMessage.h:1396-1428 (E109 above this) */
+#define SBE_SESSION_HDR_LEN 32u    /* SessionMessageHeader {24,1,111,8} + termId, sessionId, ts=0
+                                      (src/session_manager.cpp:936-967) */
+#define SBE_SESSION_BLOCK_LEN 24u
+#define SBE_SESSION_TEMPLATE_ID 1u
+#define SBE_CLUSTER_SCHEMA_VERSION 8u
+#define SBE_LITE_BLOCK_LEN 12u     /* u32 topicId @0, u64 sequence @4 (CommitOffsetLite.h:114, :337-420) */
+#define SBE_ORDER_REQUEST_LITE_TEMPLATE_ID 201u      /* uuid, messageIdentifier, payload */
+#define SBE_ORDER_NOTIFICATION_LITE_TEMPLATE_ID 202u /* uuid, messageIdentifier, payload */
+#define SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID 301u      /* messageId, messageIdentifier */
 
 /* ===================================== encode ===================================== */
 
@@ -66,6 +87,11 @@ extern "C" {
 #define SBE_ENC_REF_TRUNCATE8 0x1u /* emit exactly what SBEEncoder::encode_topic_message returns:
                                       buffer.resize(encodedLength()) keeps only the first
                                       26+Σlen bytes of the wire record (src/sbe_encoder.cpp:163-164) */
+
+/* Lite records: 8 header {12, template, 1, 1} + 12 block + nf x (u16 length + bytes), nf = 2
+ * (301) or 3 (201, 202).  Wire overhead 20 + 2 nf; no truncation (8 + encodedLength() is the
+ * whole record, src/commit_manager.cpp:129-130). */
+#define SBE_LITE_OVERHEAD(nf) (20u + 2u * (nf))
 
 /* per-record encode status */
 #define SBE_ENC_OK 0u
@@ -75,6 +101,8 @@ extern "C" {
 #define SBE_ENC_E109_PAYLOAD 4u      /* "payloadLength too long for length type [E109]" */
 #define SBE_ENC_E109_HEADERS 5u      /* "headersLength too long for length type [E109]" */
 #define SBE_ENC_OVERFLOW 6u          /* record does not fit in out_capacity (nothing written) */
+/* Lite templates: status 1 + f = "<field f>Length too long for length type [E109]" with the
+ * template's field names in wire order (computeLength, e.g. CommitOffsetLite.h:839-870). */
 
 /* A batch of TopicMessages in struct-of-arrays form.  Field order per record is the wire order
  * topic, messageType, uuid, payload, headers (TopicMessage.h:515-1231).
@@ -112,10 +140,47 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
                            uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* Session-framed encode: every record is the 32-B SessionMessageHeader
+ *   {blockLength 24, templateId 1, schemaId 111, version 8, i64 leadershipTermId,
+ *    i64 clusterSessionId, i64 timestamp 0}
+ * followed by the TopicMessage exactly as sbe_encode_topic_batch emits it under `flags`
+ * (SBE_ENC_REF_TRUNCATE8: the 26+Σlen bytes create_topic_message returns, which is what the live
+ * publish path sends; 0: the wire-correct 34+Σlen).  Record i = out[out_off[i]..out_off[i+1]) is
+ * one Publication::offer of send_combined_message.  Workspace, alignment and status as for
+ * sbe_encode_topic_batch. */
+int sbe_encode_session_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
+                             int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/* A batch of Lite records (struct of arrays):
+ *   arena, str_off ([n][nf] or NULL = packed), str_len [n][nf]: the var strings in wire order;
+ *   topic_id [n]: u32 topicId; sequence [n]: u64 sequence. */
+typedef struct sbe_lite_batch {
+    const uint8_t* arena;
+    const uint32_t* str_off;
+    const uint32_t* str_len;
+    const uint32_t* topic_id;
+    const uint64_t* sequence;
+} sbe_lite_batch;
+
+/* Fields per record of a Lite template (2 or 3), 0 if template_id is not one of them. */
+uint32_t sbe_lite_fields(uint32_t template_id);
+
+/* Upper bound of the encoded stream of a Lite batch whose strings total `string_bytes`. */
+uint64_t sbe_lite_output_bound(uint64_t n, uint64_t string_bytes, uint32_t template_id);
+
+/* Encode n Lite records of template_id (201, 202 or 301).  Outputs, workspace and alignment as
+ * for sbe_encode_topic_batch (the same workspace size). */
+int sbe_encode_lite_batch(const sbe_lite_batch* in, uint64_t n, uint32_t template_id, uint8_t* out,
+                          uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 /* ===================================== decode ===================================== */
 
 #define SBE_DEC_PARSE_MESSAGE 0u /* MessageParser::parse_message semantics → ParseResult */
 #define SBE_DEC_ON_EGRESS 1u     /* MessageHandler::on_egress semantics (decode_ack first) */
+#define SBE_DEC_LITE 2u          /* Lite-template flyweight decode (201 / 202 / 301) */
 
 /* per-record decode status.  Parse mode (0..31): */
 #define SBE_ST_TM 0u                 /* TopicMessage: views topic,type,uuid,payload,headers */
@@ -139,6 +204,13 @@ int sbe_encode_topic_batch(const sbe_tm_batch* in, uint64_t n, uint64_t ts_defau
 #define SBE_ST_EG_TM 34u             /* topic-message callback; views topic,type,uuid,payload,headers */
 #define SBE_ST_EG_NONE 35u           /* on_egress returns without a callback */
 #define SBE_ST_EG_THROW_E100 36u     /* on_egress throws std::runtime_error("buffer too short [E100]") */
+/* Lite mode (48..): the generated flyweight sequence MessageHeader::wrap, wrapForDecode(buf, 8,
+ * blockLength, version, len), topicId(), sequence(), getXAsString() per var field in order. */
+#define SBE_ST_LITE 48u              /* decoded: ts = sequence, view_off[4] = topicId, views 0..nf-1 */
+#define SBE_ST_LITE_E100 49u         /* a flyweight bounds check threw "buffer too short [E100]" (also:
+                                         the 12 fixed bytes lie past the record) */
+#define SBE_ST_LITE_NOT_LITE 50u     /* len < 8, schema != 1 or template not 201/202/301 (hdr kept
+                                         when len >= 8) */
 
 /* per-record decode flags */
 #define SBE_FL_ID_DEFAULT 0x1u      /* ack: message_id = "ack_" + decimal(ts) */

@@ -17,7 +17,10 @@
 #include <string>
 
 #include "model/Acknowledgment.h"
+#include "model/CommitOffsetLite.h"
 #include "model/MessageHeader.h"
+#include "model/OrderNotificationLite.h"
+#include "model/OrderRequestLite.h"
 #include "model/TopicMessage.h"
 
 namespace {
@@ -37,9 +40,138 @@ void put_out(uint8_t* buf, uint64_t& at, uint32_t* flen, int f, const std::strin
     at += s.size();
 }
 
+// Lite encode in CommitManager::build_commit_offset_message's call order
+// (src/commit_manager.cpp:114-130): computeLength, wrapAndApplyHeader, topicId, sequence, putX
+// per var field, 8 + encodedLength().
+template <class M>
+int lite_encode(const std::string* f, uint32_t tid, uint64_t seq, uint8_t* out, uint64_t cap, uint64_t* out_len);
+
+int lite_e109(const std::runtime_error& e, const char* const* names, int nf) {
+    const std::string w = e.what();
+    for (int k = 0; k < nf; ++k)
+        if (w.rfind(names[k], 0) == 0) return k + 1;
+    return 99;
+}
+
+template <>
+int lite_encode<sbe::CommitOffsetLite>(const std::string* f, uint32_t tid, uint64_t seq, uint8_t* out, uint64_t cap,
+                                       uint64_t* out_len) {
+    static const char* names[2] = {"messageIdLength", "messageIdentifierLength"};
+    size_t total;
+    try {
+        total = sbe::MessageHeader::encodedLength() + sbe::CommitOffsetLite::computeLength(f[0].size(), f[1].size());
+    } catch (const std::runtime_error& e) {
+        *out_len = 0;
+        return lite_e109(e, names, 2);
+    }
+    std::string buf(total, '\0');
+    sbe::CommitOffsetLite m;
+    m.wrapAndApplyHeader(&buf[0], 0, buf.size());
+    m.topicId(tid);
+    m.sequence(seq);
+    m.putMessageId(f[0].c_str(), static_cast<std::uint16_t>(f[0].size()));
+    m.putMessageIdentifier(f[1].c_str(), static_cast<std::uint16_t>(f[1].size()));
+    const uint64_t n = sbe::MessageHeader::encodedLength() + m.encodedLength();
+    if (n > cap) return 98;
+    std::memcpy(out, buf.data(), n);
+    *out_len = n;
+    return 0;
+}
+
+template <class M>
+int lite3_encode(const std::string* f, uint32_t tid, uint64_t seq, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    static const char* names[3] = {"uuidLength", "messageIdentifierLength", "payloadLength"};
+    size_t total;
+    try {
+        total = sbe::MessageHeader::encodedLength() + M::computeLength(f[0].size(), f[1].size(), f[2].size());
+    } catch (const std::runtime_error& e) {
+        *out_len = 0;
+        return lite_e109(e, names, 3);
+    }
+    std::string buf(total, '\0');
+    M m;
+    m.wrapAndApplyHeader(&buf[0], 0, buf.size());
+    m.topicId(tid);
+    m.sequence(seq);
+    m.putUuid(f[0].c_str(), static_cast<std::uint16_t>(f[0].size()));
+    m.putMessageIdentifier(f[1].c_str(), static_cast<std::uint16_t>(f[1].size()));
+    m.putPayload(f[2].c_str(), static_cast<std::uint16_t>(f[2].size()));
+    const uint64_t n = sbe::MessageHeader::encodedLength() + m.encodedLength();
+    if (n > cap) return 98;
+    std::memcpy(out, buf.data(), n);
+    *out_len = n;
+    return 0;
+}
+
+// Lite decode with the generated flyweights: wrapForDecode(buf, 8, blockLength, version, len),
+// topicId(), sequence(), getXAsString() in field order.
+template <class M>
+int lite_decode(char* p, uint64_t len, const sbe::MessageHeader& h, uint32_t* tid, uint64_t* seq, uint32_t* flen,
+                uint8_t* fbuf);
+
+template <>
+int lite_decode<sbe::CommitOffsetLite>(char* p, uint64_t len, const sbe::MessageHeader& h, uint32_t* tid,
+                                       uint64_t* seq, uint32_t* flen, uint8_t* fbuf) {
+    sbe::CommitOffsetLite m;
+    uint64_t at = 0;
+    m.wrapForDecode(p, 8, h.blockLength(), h.version(), len);
+    *tid = m.topicId();
+    *seq = m.sequence();
+    put_out(fbuf, at, flen, 0, m.getMessageIdAsString());
+    put_out(fbuf, at, flen, 1, m.getMessageIdentifierAsString());
+    return 0;
+}
+
+template <class M>
+int lite3_decode(char* p, uint64_t len, const sbe::MessageHeader& h, uint32_t* tid, uint64_t* seq, uint32_t* flen,
+                 uint8_t* fbuf) {
+    M m;
+    uint64_t at = 0;
+    m.wrapForDecode(p, 8, h.blockLength(), h.version(), len);
+    *tid = m.topicId();
+    *seq = m.sequence();
+    put_out(fbuf, at, flen, 0, m.getUuidAsString());
+    put_out(fbuf, at, flen, 1, m.getMessageIdentifierAsString());
+    put_out(fbuf, at, flen, 2, m.getPayloadAsString());
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Lite encode (template 301, 201 or 202).  Returns 0, 1..nf = E109 on that field, 97 = unknown
+// template, 98 = capacity.
+int ref_lite_encode(uint32_t tmpl, const uint8_t* const* s, const uint32_t* len, uint32_t tid, uint64_t seq,
+                    uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    std::string f[3];
+    const int nf = tmpl == 301 ? 2 : 3;
+    for (int i = 0; i < nf; ++i) f[i].assign(reinterpret_cast<const char*>(s[i]), len[i]);
+    switch (tmpl) {
+        case 301: return lite_encode<sbe::CommitOffsetLite>(f, tid, seq, out, cap, out_len);
+        case 201: return lite3_encode<sbe::OrderRequestLite>(f, tid, seq, out, cap, out_len);
+        case 202: return lite3_encode<sbe::OrderNotificationLite>(f, tid, seq, out, cap, out_len);
+        default: return 97;
+    }
+}
+
+// Lite decode of a record whose header says template 301 / 201 / 202, schema 1 (the caller
+// checks the header; len >= 20).  Returns 0 (fields out) or 1 (E100 thrown).
+int ref_lite_decode(const uint8_t* rec, uint64_t len, uint32_t* tid, uint64_t* seq, uint32_t* flen, uint8_t* fbuf) {
+    char* p = const_cast<char*>(reinterpret_cast<const char*>(rec));
+    try {
+        sbe::MessageHeader h;
+        h.wrap(p, 0, 1, len);
+        switch (h.templateId()) {
+            case 301: return lite_decode<sbe::CommitOffsetLite>(p, len, h, tid, seq, flen, fbuf);
+            case 201: return lite3_decode<sbe::OrderRequestLite>(p, len, h, tid, seq, flen, fbuf);
+            case 202: return lite3_decode<sbe::OrderNotificationLite>(p, len, h, tid, seq, flen, fbuf);
+            default: return 2;
+        }
+    } catch (const std::exception&) {
+        return 1;
+    }
+}
 
 // The sequence of SBEEncoder::encode_topic_message (src/sbe_encoder.cpp:141-164) when wire == 0;
 // wire == 1 returns the same record at its wire length (8 + encodedLength(), the length

@@ -74,17 +74,101 @@ uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len[5], uint64
     return emit;
 }
 
-int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
-                     const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
-                     uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads) {
-    const uint64_t ovh = (flags & SBE_ENC_REF_TRUNCATE8) ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD;
-    /* pass 1: record sizes (0 for E109) and, in packed mode, string offsets */
+/* One record of any layout: `lit` (nlit bytes: session header, SBE header, fixed block), then
+ * nf u16-length-prefixed strings; the last `cut` bytes of the wire record are dropped
+ * (REF_TRUNCATE8).  E109 on the first field above 65534 in wire order (computeLength). */
+static uint64_t enc_record(const uint8_t* lit, uint32_t nlit, int nf, const uint8_t* const* s,
+                           const uint32_t* len, uint32_t cut, uint8_t* out, uint8_t* status) {
+    for (int f = 0; f < nf; ++f) {
+        if (len[f] > SBE_VAR_MAX_LEN) {
+            if (status) *status = (uint8_t)(SBE_ENC_E109_TOPIC + f);
+            return 0;
+        }
+    }
+    uint64_t total = nlit + 2u * (uint64_t)nf;
+    for (int f = 0; f < nf; ++f) total += len[f];
+    const uint64_t emit = total - cut;
+    uint64_t pos = 0;
+#define PUT(src, n)                                        \
+    do {                                                   \
+        uint64_t n_ = (n);                                 \
+        uint64_t k_ = pos + n_ <= emit ? n_ : emit - pos;  \
+        if (pos < emit && k_) memcpy(out + pos, (src), k_); \
+        pos += n_;                                         \
+    } while (0)
+    PUT(lit, nlit);
+    for (int f = 0; f < nf; ++f) {
+        uint8_t l2[2];
+        wr16(l2, (uint16_t)len[f]);
+        PUT(l2, 2);
+        if (len[f]) PUT(s[f], len[f]);
+    }
+#undef PUT
+    if (status) *status = SBE_ENC_OK;
+    return emit;
+}
+
+enum { LAY_TM = 0, LAY_TM_SESSION = 1, LAY_LITE = 2 };
+typedef struct {
+    int kind, nf;
+    uint32_t cut, tmpl;
+    int64_t term, sess;
+    uint64_t ts_default;
+    const uint64_t* ts;   /* timestamp / sequence */
+    const uint32_t* tid;
+} layout_t;
+
+/* the literal prefix of record i; returns its length */
+static uint32_t lay_prefix(const layout_t* L, uint64_t i, uint8_t* lit) {
+    uint32_t o = 0;
+    if (L->kind == LAY_TM_SESSION) {
+        /* SessionManager::Impl::create_session_message_header_buffer / update_session_header
+         * (src/session_manager.cpp:936-967, :1018-1046), prepended by send_combined_message
+         * (:1118-1144) */
+        wr16(lit + 0, SBE_SESSION_BLOCK_LEN);
+        wr16(lit + 2, SBE_SESSION_TEMPLATE_ID);
+        wr16(lit + 4, SBE_CLUSTER_SCHEMA_ID);
+        wr16(lit + 6, SBE_CLUSTER_SCHEMA_VERSION);
+        wr64(lit + 8, (uint64_t)L->term);
+        wr64(lit + 16, (uint64_t)L->sess);
+        wr64(lit + 24, 0);
+        o = 32;
+    }
+    if (L->kind == LAY_LITE) {
+        /* wrapAndApplyHeader {12, T, 1, 1}; topicId @0, sequence @4 (src/commit_manager.cpp:120-124,
+         * include/model/CommitOffsetLite.h:114-118, :337-420) */
+        wr16(lit + 0, SBE_LITE_BLOCK_LEN);
+        wr16(lit + 2, (uint16_t)L->tmpl);
+        wr16(lit + 4, 1);
+        wr16(lit + 6, 1);
+        const uint32_t t = L->tid[i];
+        lit[8] = (uint8_t)t; lit[9] = (uint8_t)(t >> 8); lit[10] = (uint8_t)(t >> 16); lit[11] = (uint8_t)(t >> 24);
+        wr64(lit + 12, L->ts[i]);
+        return 20;
+    }
+    /* TopicMessage: header {16,1,1,1}, timestamp (0 → the caller's clock), sequenceNumber 0 */
+    wr16(lit + o + 0, SBE_TM_BLOCK_LEN);
+    wr16(lit + o + 2, SBE_TM_TEMPLATE_ID);
+    wr16(lit + o + 4, SBE_TOPIC_SCHEMA_ID);
+    wr16(lit + o + 6, 1);
+    wr64(lit + o + 8, L->ts[i] ? L->ts[i] : L->ts_default);
+    wr64(lit + o + 16, 0);
+    return o + 24;
+}
+
+static int encode_batch_lay(const layout_t* Ly, const uint8_t* arena, const uint32_t* str_off,
+                            const uint32_t* str_len, uint64_t n, uint8_t* out, uint64_t* out_off,
+                            uint8_t* status, int nthreads) {
+    const int nf = Ly->nf;
+    const uint64_t nlit = Ly->kind == LAY_LITE ? 20u : (Ly->kind == LAY_TM_SESSION ? 56u : 24u);
+    const uint64_t ovh = nlit + 2u * (uint64_t)nf - Ly->cut;
+    /* pass 1: record sizes (0 for E109) */
     uint64_t acc = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t* L = str_len + 5 * i;
+        const uint32_t* L = str_len + (uint64_t)nf * i;
         uint64_t sum = 0;
         int bad = 0;
-        for (int f = 0; f < 5; ++f) {
+        for (int f = 0; f < nf; ++f) {
             sum += L[f];
             if (L[f] > SBE_VAR_MAX_LEN) bad = 1;
         }
@@ -93,51 +177,64 @@ int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32
     }
     out_off[n] = acc;
     if (nthreads < 1) nthreads = 1;
-    if (str_off) {
-#ifdef _OPENMP
-#pragma omp parallel for schedule(static) num_threads(nthreads)
-#endif
-        for (int64_t i = 0; i < (int64_t)n; ++i) {
-            const uint8_t* s[5];
-            for (int f = 0; f < 5; ++f) s[f] = arena + str_off[5 * i + f];
-            uint64_t ts = timestamp[i] ? timestamp[i] : ts_default;
-            uint8_t st;
-            orc_encode_one(s, str_len + 5 * i, ts, flags, out + out_off[i], &st);
-            if (status) status[i] = st;
-        }
-    } else {
-        /* packed: string bytes of record i start at Σ_{j<i} Σlen_j (E109 records included).
-         * Split into nthreads contiguous chunks; each chunk first sums its predecessors'
-         * string bytes. */
-        int nt = nthreads;
-        uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
+    /* packed: string bytes of record i start at Σ_{j<i} Σlen_j (E109 records included).  Split
+     * into nthreads contiguous chunks; each chunk first sums its predecessors' string bytes. */
+    int nt = nthreads;
+    uint64_t chunk = (n + (uint64_t)nt - 1) / (uint64_t)nt;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static, 1) num_threads(nt)
 #endif
-        for (int t = 0; t < nt; ++t) {
-            uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk < n ? lo + chunk : n;
-            if (lo >= hi) continue;
-            /* string bytes before record lo = out_off-free recomputation over lengths */
-            uint64_t ib = 0;
-            for (uint64_t j = 0; j < lo; ++j)
-                for (int f = 0; f < 5; ++f) ib += str_len[5 * j + f];
-            for (uint64_t i = lo; i < hi; ++i) {
-                const uint32_t* L = str_len + 5 * i;
-                const uint8_t* s[5];
-                uint64_t o = ib;
-                for (int f = 0; f < 5; ++f) {
-                    s[f] = arena + o;
-                    o += L[f];
-                }
-                uint64_t ts = timestamp[i] ? timestamp[i] : ts_default;
-                uint8_t st;
-                orc_encode_one(s, L, ts, flags, out + out_off[i], &st);
-                if (status) status[i] = st;
-                ib = o;
+    for (int t = 0; t < nt; ++t) {
+        uint64_t lo = (uint64_t)t * chunk, hi = lo + chunk < n ? lo + chunk : n;
+        if (lo >= hi) continue;
+        uint64_t ib = 0;
+        if (!str_off)
+            for (uint64_t j = 0; j < lo * (uint64_t)nf; ++j) ib += str_len[j];
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t* L = str_len + (uint64_t)nf * i;
+            const uint8_t* s[5];
+            for (int f = 0; f < nf; ++f) {
+                s[f] = arena + (str_off ? str_off[(uint64_t)nf * i + f] : ib);
+                if (!str_off) ib += L[f];
             }
+            uint8_t lit[64], st;
+            const uint32_t nlit = lay_prefix(Ly, i, lit);
+            enc_record(lit, nlit, nf, s, L, Ly->cut, out + out_off[i], &st);
+            if (status) status[i] = st;
         }
     }
     return 0;
+}
+
+int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                     const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
+                     uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads) {
+    layout_t Ly = {LAY_TM, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0, 0, 0, ts_default, timestamp, NULL};
+    return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
+}
+
+int orc_encode_session_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                             const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
+                             int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t* out_off, uint8_t* status, int nthreads) {
+    layout_t Ly = {LAY_TM_SESSION, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0,
+                   leadership_term_id, cluster_session_id, ts_default, timestamp, NULL};
+    return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
+}
+
+static int lite_fields(uint32_t t) {
+    return t == SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID ? 2
+         : (t == SBE_ORDER_REQUEST_LITE_TEMPLATE_ID || t == SBE_ORDER_NOTIFICATION_LITE_TEMPLATE_ID) ? 3 : 0;
+}
+
+int orc_encode_lite_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                          const uint32_t* topic_id, const uint64_t* sequence, uint64_t n,
+                          uint32_t template_id, uint8_t* out, uint64_t* out_off, uint8_t* status,
+                          int nthreads) {
+    const int nf = lite_fields(template_id);
+    if (!nf) return -1;
+    layout_t Ly = {LAY_LITE, nf, 0, template_id, 0, 0, 0, sequence, topic_id};
+    return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -376,8 +473,40 @@ static void dec_on_egress(const uint8_t* rec, uint64_t len, desc_t* d) {
     d->status = SBE_ST_EG_TM;
 }
 
+/* The Lite templates' generated decode flyweights, in field order: MessageHeader::wrap,
+ * wrapForDecode(buf, 8, blockLength, version, len) → sbeCheckPosition(8 + blockLength)
+ * (CommitOffsetLite.h:240-254, :268-276), topicId() @8, sequence() @12 (:337-420: no bounds
+ * check; records shorter than 20 B would read past the buffer, reported as E100 here), then
+ * getXAsString() per var field: sbePosition(pos + 2), then sbePosition(pos + 2 + L)
+ * (:528-540), each throwing "buffer too short [E100]" past len. */
+static void dec_lite(const uint8_t* rec, uint64_t len, desc_t* d) {
+    memset(d, 0, sizeof(*d));
+    if (!rec || len < 8) { d->status = SBE_ST_LITE_NOT_LITE; return; }
+    set_hdr(d, rec);
+    const uint16_t blk = rd16(rec + 0), tmpl = rd16(rec + 2), schema = rd16(rec + 4);
+    const int nf = lite_fields(tmpl);
+    if (schema != 1 || !nf) { d->status = SBE_ST_LITE_NOT_LITE; return; }
+    uint64_t pos = 8u + blk;
+    if (pos > len || len < 20) { d->status = SBE_ST_LITE_E100; return; }
+    for (int f = 0; f < nf; ++f) {
+        if (pos + 2 > len) { memset(d->off, 0, sizeof d->off); memset(d->len, 0, sizeof d->len);
+                             d->status = SBE_ST_LITE_E100; return; }
+        const uint64_t L = rd16(rec + pos);
+        pos += 2;
+        if (pos + L > len) { memset(d->off, 0, sizeof d->off); memset(d->len, 0, sizeof d->len);
+                             d->status = SBE_ST_LITE_E100; return; }
+        set_view(d, f, pos, L);
+        pos += L;
+    }
+    d->status = SBE_ST_LITE;
+    d->ts = rd64(rec + 12);
+    d->off[4] = rd32(rec + 8);
+}
+
 static void decode_into(const uint8_t* rec, uint64_t len, uint32_t mode, desc_t* d) {
-    if (mode == SBE_DEC_ON_EGRESS)
+    if (mode == SBE_DEC_LITE)
+        dec_lite(rec, len, d);
+    else if (mode == SBE_DEC_ON_EGRESS)
         dec_on_egress(rec, len, d);
     else
         dec_parse_message(rec, len, d);

@@ -35,7 +35,21 @@ int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32
                      const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
                      uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads);
 
-/* One record, MessageParser::parse_message (mode 0) or MessageHandler::on_egress (mode 1).
+/* Session-framed batch encode, the semantics/outputs of sbe_encode_session_batch. */
+int orc_encode_session_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                             const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
+                             int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t* out_off, uint8_t* status, int nthreads);
+
+/* Lite-template batch encode (201 / 202 / 301), the semantics/outputs of sbe_encode_lite_batch.
+ * str_off / str_len are [n][nf].  Returns -1 for an unknown template. */
+int orc_encode_lite_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                          const uint32_t* topic_id, const uint64_t* sequence, uint64_t n,
+                          uint32_t template_id, uint8_t* out, uint64_t* out_off, uint8_t* status,
+                          int nthreads);
+
+/* One record, MessageParser::parse_message (mode 0), MessageHandler::on_egress (mode 1) or the
+ * Lite flyweight decode (mode 2).
  * Writes the descriptor fields of record slot 0 of the given arrays. */
 void orc_decode_one(const uint8_t* rec, uint64_t len, uint32_t mode, uint8_t* status,
                     uint8_t* flags, uint16_t hdr[4], uint64_t* ts, uint32_t view_off[5],

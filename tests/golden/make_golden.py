@@ -110,6 +110,70 @@ def main():
     json.dump({"source": src + " (MessageHandler::on_egress TopicMessage sequence, message_handler.hpp:47-60)",
                "cases": eg}, open(os.path.join(HERE, "egress_tm_ref.json"), "w"), indent=1)
     print(f"encode {len(out)}, tm {len(tm)}, ack {len(ack)}, egress {len(eg)}")
+    lite = lite_cases()
+    json.dump({"source": src + " (CommitOffsetLite / OrderRequestLite / OrderNotificationLite: "
+                               "build_commit_offset_message call order src/commit_manager.cpp:114-130 for encode; "
+                               "wrapForDecode + topicId + sequence + getXAsString for decode)",
+               **lite}, open(os.path.join(HERE, "lite_ref.json"), "w"), indent=1)
+    print(f"lite encode {len(lite['encode'])}, lite decode {len(lite['decode'])}")
+
+
+def lite_encode_inputs():
+    """(template, fields, topic_id, sequence) encode cases: typical, empty, non-printable, the
+    65534 boundary and E109 on every field."""
+    cases = []
+    for t in (301, 201, 202):
+        nf = T.LITE_NF[t]
+        base = [b"msg_1760000000000000000_00042", b"orders:17", b'{"symbol":"BTC-USD","qty":"1"}'][:nf]
+        cases.append((t, base, 1, 1))
+        cases.append((t, [b""] * nf, 0, 0))
+        cases.append((t, [b"\x00\xff\n", b"x", b"\x7f" * 3][:nf], 2**32 - 1, 2**64 - 1))
+        cases.append((t, [b"\x41" * 65534] + [b"y"] * (nf - 1), 3, 12345))
+        for k in range(nf):
+            f = [b"a", b"b", b"c"][:nf]
+            f[k] = b"\x5a" * 65535
+            cases.append((t, f, 4, 9))
+    return cases
+
+
+def lite_decode_records():
+    """Valid Lite records and mutations of them: every truncation length >= 20, blockLength and
+    version variants, a corrupted length field, trailing slack."""
+    recs = []
+    for t in (301, 201, 202):
+        nf = T.LITE_NF[t]
+        f = [b"m_7", b"orders:3", b'{"q":1}'][:nf]
+        rc, r = T.ref_lite_encode(t, f, 7, 0x0102030405060708)
+        assert rc == 0
+        recs.append((f"t{t}_ok", r))
+        recs.append((f"t{t}_slack", r + b"\x00" * 5))
+        for cut in range(20, len(r)):
+            recs.append((f"t{t}_cut{cut}", r[:cut]))
+        for blk in (0, 4, 11, 13, 16, 40):
+            recs.append((f"t{t}_blk{blk}", blk.to_bytes(2, "little") + r[2:]))
+        recs.append((f"t{t}_ver9", r[:6] + b"\x09\x00" + r[8:]))
+        bad = bytearray(r)
+        bad[20:22] = (len(r)).to_bytes(2, "little")
+        recs.append((f"t{t}_badlen", bytes(bad)))
+        empty = T.ref_lite_encode(t, [b""] * nf, 0, 0)[1]
+        recs.append((f"t{t}_empty", empty))
+    return recs
+
+
+def lite_cases():
+    enc = []
+    for t, fields, tid, seq in lite_encode_inputs():
+        rc, r = T.ref_lite_encode(t, fields, tid, seq)
+        enc.append({"template": t, "fields": [field_spec(x) for x in fields], "topic_id": tid, "sequence": str(seq),
+                    "status": rc, "record": blob(r)})
+    dec = []
+    for name, r in lite_decode_records():
+        rc, tid, seq, f = T.ref_lite_decode(r)
+        nf = T.LITE_NF[int.from_bytes(r[2:4], "little")]
+        dec.append({"name": name, "rec": blob(r), "e100": rc, "topic_id": tid if rc == 0 else None,
+                    "sequence": str(seq) if rc == 0 else None,
+                    "fields": [blob(x) for x in f[:nf]] if rc == 0 else None})
+    return {"encode": enc, "decode": dec}
 
 
 if __name__ == "__main__":

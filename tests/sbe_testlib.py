@@ -25,7 +25,9 @@ if PKG not in sys.path:
 
 # status / flag constants (include/sbecodec.h)
 ENC_REF_TRUNCATE8 = 1
-DEC_PARSE, DEC_EGRESS = 0, 1
+DEC_PARSE, DEC_EGRESS, DEC_LITE = 0, 1, 2
+ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
+LITE_NF = {301: 2, 201: 3, 202: 3}
 ST_TM, ST_ACK, ST_SESSION_EVENT = 0, 1, 2
 ST_ERR_NULL_EMPTY, ST_ERR_HEADER, ST_ERR_UNKNOWN_TYPE = 16, 17, 18
 ST_ERR_SESSION_EVENT, ST_ERR_SESSION_SHORT, ST_ERR_EMBEDDED_SHORT = 19, 20, 21
@@ -54,7 +56,10 @@ def oracle():
             build_oracle()
         L = ctypes.CDLL(ORACLE_LIB)
         vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        i64 = ctypes.c_int64
         L.orc_encode_batch.argtypes = [vp, vp, vp, vp, u64, u64, u32, vp, vp, vp, i]
+        L.orc_encode_session_batch.argtypes = [vp, vp, vp, vp, u64, u64, u32, i64, i64, vp, vp, vp, i]
+        L.orc_encode_lite_batch.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp, vp, vp, i]
         L.orc_decode_batch.argtypes = [vp, vp, u64, u32, vp, vp, vp, vp, vp, vp, i]
         L.orc_to_nanos_auto.restype = u64
         L.orc_to_nanos_auto.argtypes = [u64]
@@ -80,6 +85,47 @@ def oracle_encode(arena, str_len, ts, str_off=None, flags=0, ts_default=0, nthre
     status = np.zeros(max(n, 1), dtype=np.uint8)
     oracle().orc_encode_batch(_p(arena if arena.size else np.zeros(1, np.uint8)), _p(str_off), _p(str_len),
                               _p(ts), n, ts_default, flags, _p(out), _p(out_off), _p(status), nthreads)
+    return out[: int(out_off[n])], out_off, status[:n]
+
+
+def oracle_encode_session(arena, str_len, ts, term_id, session_id, str_off=None, flags=0, ts_default=0,
+                          nthreads=1):
+    """Session-framed TopicMessages (32-B SessionMessageHeader + record) → (out, out_off, status)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    str_len = np.ascontiguousarray(str_len, dtype=np.uint32).reshape(-1, 5)
+    ts = np.ascontiguousarray(ts, dtype=np.uint64)
+    n = ts.size
+    if str_off is not None:
+        str_off = np.ascontiguousarray(str_off, dtype=np.uint32).reshape(-1, 5)
+    cap = int(str_len.sum(dtype=np.uint64)) + 66 * n + 16
+    out = np.zeros(cap, dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    oracle().orc_encode_session_batch(_p(arena if arena.size else np.zeros(1, np.uint8)), _p(str_off), _p(str_len),
+                                      _p(ts), n, ts_default, flags, term_id, session_id, _p(out), _p(out_off),
+                                      _p(status), nthreads)
+    return out[: int(out_off[n])], out_off, status[:n]
+
+
+def oracle_encode_lite(template_id, arena, str_len, topic_id, sequence, str_off=None, nthreads=1):
+    """Lite records (201 / 202 / 301): str_len uint32[n, nf] → (out, out_off, status)."""
+    nf = LITE_NF[template_id]
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    str_len = np.ascontiguousarray(str_len, dtype=np.uint32).reshape(-1, nf)
+    topic_id = np.ascontiguousarray(topic_id, dtype=np.uint32)
+    sequence = np.ascontiguousarray(sequence, dtype=np.uint64)
+    n = sequence.size
+    if str_off is not None:
+        str_off = np.ascontiguousarray(str_off, dtype=np.uint32).reshape(-1, nf)
+    cap = int(str_len.sum(dtype=np.uint64)) + (20 + 2 * nf) * n + 16
+    out = np.zeros(cap, dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    rc = oracle().orc_encode_lite_batch(_p(arena if arena.size else np.zeros(1, np.uint8)), _p(str_off),
+                                        _p(str_len), _p(topic_id if n else np.zeros(1, np.uint32)),
+                                        _p(sequence if n else np.zeros(1, np.uint64)), n, template_id,
+                                        _p(out), _p(out_off), _p(status), nthreads)
+    assert rc == 0
     return out[: int(out_off[n])], out_off, status[:n]
 
 
@@ -115,6 +161,8 @@ def ref():
         L.ref_tm_decode_parse.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.ref_ack_decode.argtypes = [vp, u64, vp, vp, vp]
         L.ref_egress_tm.argtypes = [vp, u64, vp, vp]
+        L.ref_lite_encode.argtypes = [ctypes.c_uint32, vp, vp, ctypes.c_uint32, u64, vp, u64, vp]
+        L.ref_lite_decode.argtypes = [vp, u64, vp, vp, vp, vp]
         _ref = L
     return _ref
 
@@ -128,6 +176,29 @@ def ref_encode(fields, ts, wire):
     n = ctypes.c_uint64(0)
     rc = ref().ref_tm_encode(ptrs, lens, ts, 1 if wire else 0, out, cap, ctypes.byref(n))
     return rc, out.raw[: n.value]
+
+
+def ref_lite_encode(template_id, fields, topic_id, sequence):
+    nf = LITE_NF[template_id]
+    assert len(fields) == nf
+    bufs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in fields]
+    ptrs = (ctypes.c_void_p * nf)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint32 * nf)(*[len(f) for f in fields])
+    cap = 20 + 2 * nf + sum(len(f) for f in fields) + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_uint64(0)
+    rc = ref().ref_lite_encode(template_id, ptrs, lens, topic_id, sequence, out, cap, ctypes.byref(n))
+    return rc, out.raw[: n.value]
+
+
+def ref_lite_decode(rec: bytes):
+    """(rc, topic_id, sequence, fields): rc 0 ok, 1 E100 (header must name a Lite template)."""
+    b = _rec_buf(rec)
+    tid, seq = ctypes.c_uint32(), ctypes.c_uint64()
+    flen = (ctypes.c_uint32 * 3)()
+    fbuf = ctypes.create_string_buffer(len(rec) * 3 + 16)
+    rc = ref().ref_lite_decode(b, len(rec), ctypes.byref(tid), ctypes.byref(seq), flen, fbuf)
+    return rc, tid.value, seq.value, _split(fbuf.raw, flen, 3)
 
 
 def _rec_buf(rec: bytes):
@@ -392,6 +463,29 @@ def var_orders(n: int, seed: int = 0x5EED0004):
     pb = ub + 29
     arena[pb[:, None] + np.arange(10)] = np.frombuffer(b'{"symbol":', np.uint8)
     return arena, str_len, ts
+
+
+def lite_records(n: int, template_id: int, seed: int = 0x5EED0301):
+    """Lite records in packed SoA form: 301 CommitOffsetLite (messageId = uuid 29 B,
+    messageIdentifier 8–40 B); 201 / 202 (uuid 29 B, messageIdentifier 8–40 B, payload 32–480 B).
+    Returns (arena, str_len [n, nf], topic_id [n], sequence [n])."""
+    nf = LITE_NF[template_id]
+    r = splitmix64(seed ^ template_id, 4 * n).reshape(n, 4)
+    lens = [np.full(n, 29, np.int64), (U64(8) + r[:, 0] % U64(33)).astype(np.int64)]
+    if nf == 3:
+        lens.append((U64(32) + r[:, 1] % U64(449)).astype(np.int64))
+    str_len = np.stack(lens, axis=1).astype(np.uint32)
+    tot = str_len.astype(np.int64).sum(1)
+    starts = np.zeros(n + 1, np.int64)
+    starts[1:] = np.cumsum(tot)
+    fill = splitmix64(seed ^ 0x5151, (int(starts[-1]) + 7) // 8 + 1).view(np.uint8)[: int(starts[-1])]
+    arena = ((fill % 94) + 32).astype(np.uint8)
+    seq = U64(1_000_000) + np.arange(n, dtype=U64)
+    ub = starts[:-1]
+    arena[ub[:, None] + np.arange(4)] = np.frombuffer(b"msg_", np.uint8)
+    arena[ub[:, None] + 4 + np.arange(19)] = _digits(U64(1_760_000_000_000_000_000) + np.arange(n, dtype=U64), 19)
+    topic_id = (U64(1) + r[:, 2] % U64(3)).astype(np.uint32)
+    return arena, str_len, topic_id, seq
 
 
 def mixed_records(n: int, seed: int = 0x5EED0003):

@@ -38,13 +38,20 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_side_entry_points(lib):
     lib.sbe_abi_version.restype = ctypes.c_int
-    assert lib.sbe_abi_version() == 1
+    assert lib.sbe_abi_version() == 2
     lib.sbe_encode_workspace_size.restype = ctypes.c_size_t
     lib.sbe_encode_workspace_size.argtypes = [ctypes.c_uint64]
     assert lib.sbe_encode_workspace_size(1_000_000) >= 16 * (1_000_000 // 256)
     lib.sbe_encode_output_bound.restype = ctypes.c_uint64
     lib.sbe_encode_output_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
-    assert lib.sbe_encode_output_bound(10, 222 * 10, 0) == 2560
+    assert lib.sbe_encode_output_bound(10, 222 * 10, 0) == 2220 + (34 + 32) * 10  # covers session framing
+    lib.sbe_lite_fields.restype = ctypes.c_uint32
+    lib.sbe_lite_fields.argtypes = [ctypes.c_uint32]
+    assert [lib.sbe_lite_fields(t) for t in (301, 201, 202, 1, 0)] == [2, 3, 3, 0, 0]
+    lib.sbe_lite_output_bound.restype = ctypes.c_uint64
+    lib.sbe_lite_output_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+    assert lib.sbe_lite_output_bound(10, 500, 301) == 500 + 24 * 10
+    assert lib.sbe_lite_output_bound(10, 500, 201) == 500 + 26 * 10
     lib.sbe_last_error.restype = ctypes.c_char_p
     assert lib.sbe_last_error() == b""
 
@@ -55,6 +62,17 @@ def test_invalid_arguments_are_rejected_before_any_launch(lib):
     lib.sbe_encode_topic_batch.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp,
                                            ctypes.c_uint64, vp, vp, vp, ctypes.c_size_t, vp]
     assert lib.sbe_encode_topic_batch(None, 1, 0, 0, None, 0, None, None, None, 0, None) == -1
+    lib.sbe_encode_lite_batch.restype = ctypes.c_int
+    lib.sbe_encode_lite_batch.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp, vp, vp,
+                                          ctypes.c_size_t, vp]
+    dummy = (ctypes.c_uint64 * 8)()
+    assert lib.sbe_encode_lite_batch(ctypes.addressof(dummy), 1, 7, None, 0, None, None, None, 0, None) == -1
+    lib.sbe_encode_session_batch.restype = ctypes.c_int
+    lib.sbe_encode_session_batch.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64,
+                                             ctypes.c_int64, vp, ctypes.c_uint64, vp, vp, vp, ctypes.c_size_t, vp]
+    assert lib.sbe_encode_session_batch(None, 1, 0, 0, 1, 2, None, 0, None, None, None, 0, None) == -1
+    assert lib.sbe_encode_session_batch(ctypes.addressof(dummy), 1, 0, 0x80, 1, 2, None, 0,
+                                        ctypes.addressof(dummy), None, None, 0, None) == -1  # unknown flag
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp]
     assert lib.sbe_decode_batch(None, None, 5, 7, None, None) == -1      # unknown mode
