@@ -1332,9 +1332,9 @@ __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte 
 
 // Staged records: every key dword contains 'q' (key[3]), so a 16-byte chunk (one ds_read_b128; the
 // in-chunk swizzle permutes dwords, which a membership test does not care about) without a 'q'
-// byte holds no candidate.  Only flagged chunks run the exact per-dword test.
-template <>
-__device__ bool has_seq_key<LdsRec>(const LdsRec& R, uint32_t p, uint32_t n) {
+// byte holds no candidate.  Only flagged chunks run the exact per-dword test.  Per lane: the
+// fallback of the window-wide scan below (more hits in one window than its list holds).
+__device__ bool has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
     if (n < 16) return false;
     const uint32_t a0 = R.base + p, a1 = a0 + n;  // window byte range
     const uint32_t c1 = (a1 + 15) >> 4;
@@ -1354,6 +1354,62 @@ __device__ bool has_seq_key<LdsRec>(const LdsRec& R, uint32_t p, uint32_t n) {
         }
     }
     return false;
+}
+
+// Staged records are not scanned while parsing: the wave scans the whole window once
+// (window_seq_scan) and each lane then looks its payload up in the hit list.
+// per-lane scans cost the longest payload of the wave (divergence), the window-wide scan a fixed
+// 16 chunks per lane: payloads up to kSeqLaneMax bytes are scanned per lane
+constexpr uint32_t kSeqLaneMax = 256;
+// _sequence_number flag of a payload: SBE_FL_SEQ_KEY or 0; staged payloads return kFlSeqPending
+// (dec_window resolves them: per lane, or with one window-wide scan when some payload of the
+// window is longer than kSeqLaneMax)
+constexpr uint32_t kFlSeqPending = 0x80u;
+template <typename R_t>
+__device__ __forceinline__ uint32_t seq_key_state(const R_t& R, uint32_t p, uint32_t n) {
+    return has_seq_key(R, p, n) ? SBE_FL_SEQ_KEY : 0u;
+}
+template <>
+__device__ __forceinline__ uint32_t seq_key_state<LdsRec>(const LdsRec&, uint32_t, uint32_t n) {
+    return n >= 16 ? kFlSeqPending : 0u;
+}
+
+// Window-wide "_sequence_number" scan: lane l takes 16-byte chunks l, l+64, ... of the staged
+// window (coalesced, no divergence between records); a chunk with a 'q' byte has its aligned
+// dwords tested against the four key slices, and a candidate start is verified (16 bytes at that
+// window offset, inside the window).  Each lane keeps the start of its first hit in `hit`
+// (~0u: none) and sets `more` if it found a second one.
+__device__ __forceinline__ uint32_t win_bytes4(const uint32_t* win, uint32_t s) {  // 4 bytes at window offset s
+    const uint32_t lo = lds_dw(win, s >> 2), sh = s & 3u;
+    return sh ? __builtin_amdgcn_alignbyte(lds_dw(win, (s >> 2) + 1), lo, sh) : lo;
+}
+__device__ __forceinline__ void window_seq_scan(const uint32_t* win, uint32_t nbytes, int lane, uint32_t& hit,
+                                                bool& more) {
+    hit = ~0u;
+    more = false;
+    const uint32_t nch = nbytes >> 4;
+#pragma unroll 4
+    for (int k = 0; k < kWin / 16 / kWave; ++k) {
+        const uint32_t c = lane + kWave * k;
+        const uint4 v = c < nch ? lds_read_chunk_raw(win, c) : make_uint4(0, 0, 0, 0);
+        const uint32_t t = (q_bytes(v.x) | q_bytes(v.y) | q_bytes(v.z) | q_bytes(v.w)) & 0x80808080u;
+        if (t) {
+#pragma nounroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t A = 16 * c + 4 * j;
+                const uint32_t w = lds_dw(win, A >> 2);
+                if (!(w == kSeqK0 || w == kSeqS1 || w == kSeqS2 || w == kSeqS3)) continue;
+                const uint32_t off = w == kSeqK0 ? 0u : w == kSeqS1 ? 1u : w == kSeqS2 ? 2u : 3u;
+                if (A < off || A - off + 16 > nbytes) continue;
+                const uint32_t st = A - off;
+                if (win_bytes4(win, st) == kSeqK0 && win_bytes4(win, st + 4) == kSeqK1 &&
+                    win_bytes4(win, st + 8) == kSeqK2 && win_bytes4(win, st + 12) == kSeqK3) {
+                    if (hit == ~0u) hit = st;
+                    else more = true;
+                }
+            }
+        }
+    }
 }
 
 // decode_topic_message_with_sbe (src/sbe_encoder.cpp:957-1143); record bytes [b, b+len)
@@ -1381,7 +1437,7 @@ __device__ void dec_tm_parse(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
     d.ts = R.u64(b + 8);
     if (b) d.flags |= SBE_FL_WRAPPED;
 #ifndef SBE_DABL_NOSEQ
-    if (has_seq_key(R, d.off[3], d.len[3])) d.flags |= SBE_FL_SEQ_KEY;
+    d.flags |= seq_key_state(R, d.off[3], d.len[3]);
 #endif
     if (pos + 2 > len || pos + 2 + (uint64_t)R.u16(b + pos) > len) {
         d.flags |= SBE_FL_HEADERS_E100;
@@ -1405,6 +1461,24 @@ __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& 
     for (uint64_t i = 16; i < len && nruns < 3; i += 4) {
         const uint32_t nb = (len - i) < 4 ? (uint32_t)(len - i) : 4u;
         const uint32_t w = R.bytes(b + i, nb);
+        // printable bytes [32, 126], four at a time: bit 8k+7 set for a printable byte k
+        const uint32_t lo7 = w & 0x7f7f7f7fu;
+        const uint32_t pr = ((lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u) &
+                            (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u);
+        const uint32_t full = nb == 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * nb)) - 1u);
+        if (pr == full) {  // every byte printable: the run goes on
+            if (run_len == 0) run_start = i;
+            run_len += nb;
+            continue;
+        }
+        if (pr == 0) {  // none printable: the run (if any) ends here
+            if (run_len >= 3 && nruns < 3) {
+                d.set_view(nruns, (uint32_t)(b + run_start), (uint32_t)run_len);
+                ++nruns;
+            }
+            run_len = 0;
+            continue;
+        }
         for (uint32_t k = 0; k < nb; ++k) {
             const uint32_t c = (w >> (8 * k)) & 0xffu;
             if (c >= 32 && c <= 126) {
@@ -1595,41 +1669,43 @@ __device__ void dec_lite(const R_t& R, uint32_t len, Desc& d) {
     d.off[4] = R.u32(8);
 }
 
-#ifndef SBE_DEC_PERSIST
-#define SBE_DEC_PERSIST 0  // measured: the persistent form was 6-10 % slower (hardware WG dispatch overlaps better)
+constexpr int kDecRegs = kWin / 16 / kWave;  // uint4 staging registers per lane (one window)
+
+
+template <uint32_t kMode, typename R_t>
+__device__ __forceinline__ void dec_record(const R_t& R, uint32_t len, Desc& d) {
+    if (kMode == SBE_DEC_ON_EGRESS)
+        dec_on_egress(R, len, d);
+    else if (kMode == SBE_DEC_LITE)
+        dec_lite(R, len, d);
+    else
+        dec_parse_message(R, len, d);
+}
+
+// a record parsed straight from HBM (rare: see sbe_decode_kernel); not inlined, so its register
+// needs stay out of the window loop's
+#ifndef SBE_DEC_GLB_INLINE
+#define SBE_DEC_GLB_INLINE 0
 #endif
-constexpr int kDecRegs = kWin / 16 / kWave;  // uint4 staging registers per lane (one tile)
-
-// One 64-record tile: its byte range and this lane's record.
-struct DecTile {
-    uint64_t T0, T1;  // rec_off[first], rec_off[last] (uniform)
-    uint64_t rs, re;  // this lane's record [rs, re) (clamped to the last record past the end)
-};
-
-__device__ __forceinline__ DecTile dec_tile_load(const DecArgs& a, uint64_t tile, int lane) {
-    DecTile x;
-    const uint64_t t0 = tile * kTile;
-    const uint64_t last = t0 + kTile < a.n ? t0 + kTile : a.n;
-    x.T0 = a.rec_off[t0];
-    x.T1 = a.rec_off[last];
-    uint64_t r = t0 + (uint64_t)lane;
-    r = r < a.n ? r : a.n - 1;
-    x.rs = a.rec_off[r];
-    x.re = a.rec_off[r + 1];
-    return x;
+template <uint32_t kMode>
+#if SBE_DEC_GLB_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint32_t rl) {
+    Desc d;
+    d.clear();
+    dec_record<kMode>(GlbRec{reinterpret_cast<uintptr_t>(in) + rs}, rl, d);
+    return d;
 }
 
-// staged window [wb, we) of a tile: from its first byte (16-B aligned down) for kWin bytes at most
-__device__ __forceinline__ void dec_window(const DecTile& x, uint64_t& wb, uint64_t& we) {
-    wb = uniform64(x.T0) & ~15ull;
-    const uint64_t end = (uniform64(x.T1) + 15) & ~15ull;
-    we = (wb + kWin) < end ? wb + kWin : end;
-}
-
-__device__ __forceinline__ void dec_stage_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane,
-                                                uint4 (&I)[kDecRegs]) {
+// Stage window [wb, we) (16-B aligned, <= kWin bytes) into LDS: every 16-B load issued before
+// the first LDS write, one HBM round trip per window.
+__device__ __forceinline__ void dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, int lane) {
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
     const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
+    uint4 I[kDecRegs];
 #pragma unroll
     for (int k = 0; k < kDecRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -1639,11 +1715,6 @@ __device__ __forceinline__ void dec_stage_issue(const DecArgs& a, uint64_t wb, u
         I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
 #endif
     }
-}
-
-__device__ __forceinline__ void dec_stage_write(uint32_t* win, uint64_t wb, uint64_t we, int lane,
-                                                const uint4 (&I)[kDecRegs]) {
-    const uint32_t nch = (uint32_t)((we - wb) >> 4);
 #pragma unroll
     for (int k = 0; k < kDecRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -1651,43 +1722,112 @@ __device__ __forceinline__ void dec_stage_write(uint32_t* win, uint64_t wb, uint
     }
 }
 
-// Parse the tile's records (staged in win as [wb, we)) and write their descriptors.  The
-// workgroup is one wave, whose LDS accesses execute in issue order: phase changes are compiler
-// barriers (a __syncthreads() would wait vmcnt(0) and drain the next tile's staging loads).
+// One workgroup (one wave) per 64-record tile.  The tile's bytes are staged window by window:
+// the first window starts at the tile's first byte, each later one at the first record not yet
+// parsed; every lane parses its record from LDS in the window that holds it whole.  A record
+// that no window can hold (larger than the window, or outside the tile's byte range when
+// rec_off is not monotonic) is parsed from HBM.  Fixed 256-B records take one window per tile.
+// The workgroup is one wave, whose LDS accesses execute in issue order: phase changes are
+// compiler barriers.
+// 3 waves per SIMD (<= 168 VGPRs): with 16 KiB of LDS per workgroup the CU holds 10 workgroups,
+// which 3 waves/SIMD still allow.
+// Parse the records that lie whole in the staged window [wb, we); in parse mode, then resolve the
+// _sequence_number flags left pending (long payloads) with one window-wide scan.
 template <uint32_t kMode>
-__device__ __forceinline__ void dec_tile(const DecArgs& a, uint32_t* win, const DecTile& x, uint64_t wb,
-                                         uint64_t we, uint64_t tile, int lane) {
-    const uint64_t t0 = tile * kTile;
-    const uint64_t r = t0 + lane;
+__device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uint64_t we, uint64_t rs, uint64_t rl,
+                                           bool& done, Desc& d, int lane) {
+    bool here = false;
+    if (!done && rs >= wb && rs + rl <= we) {
+        dec_record<kMode>(LdsRec{win, (uint32_t)(rs - wb)}, (uint32_t)rl, d);
+        done = true;
+        here = true;
+    }
+    if (kMode == SBE_DEC_PARSE_MESSAGE) {
+        const bool pend = here && (d.flags & kFlSeqPending);
+        if (__ballot(pend) && !__ballot(pend && d.len[3] > kSeqLaneMax)) {
+            if (pend)
+                d.flags = (d.flags & ~kFlSeqPending) |
+                          (has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]) ? SBE_FL_SEQ_KEY : 0u);
+        } else if (__ballot(pend)) {
+            uint32_t hpos;
+            bool more;
+            window_seq_scan(win, (uint32_t)(we - wb), lane, hpos, more);
+            const uint32_t p0 = (uint32_t)(rs - wb) + d.off[3], p1 = p0 + d.len[3];
+            bool hit = false;
+            if (__ballot(more)) {  // two hits among one lane's chunks: pending lanes scan themselves
+                if (pend) hit = has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
+            } else {
+                for (uint64_t m = __ballot(hpos != ~0u); m; m &= m - 1) {  // broadcast each hit
+                    const uint32_t x = __builtin_amdgcn_readlane(hpos, __builtin_ctzll(m));
+                    hit |= x >= p0 && x + 16 <= p1;
+                }
+            }
+            if (pend) d.flags = (d.flags & ~kFlSeqPending) | (hit ? SBE_FL_SEQ_KEY : 0u);
+        }
+    }
+}
+
+#ifndef SBE_DEC_MINW
+#define SBE_DEC_MINW 3
+#endif
+template <uint32_t kMode>
+__global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
+    __shared__ uint32_t win[kWinDw];
+    const int lane = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t r = t0 + (uint64_t)lane;
     const bool valid = r < a.n;
-    const uint64_t last = (t0 + kTile < a.n ? t0 + kTile : a.n);
-    const uint64_t rs = valid ? x.rs : 0;
-    const uint64_t rl = valid ? x.re - x.rs : 0;
+    const uint64_t last = t0 + kTile < a.n ? t0 + kTile : a.n;
+    const uint64_t T0 = uniform64(a.rec_off[t0]);
+    const uint64_t end = (uniform64(a.rec_off[last]) + 15) & ~15ull;
+    const uint64_t rc = r < a.n ? r : a.n - 1;
+    const uint64_t rs = a.rec_off[rc];
+    const uint64_t rl = valid ? a.rec_off[rc + 1] - rs : 0;
 
     Desc d;
     d.clear();
-    if (!valid) {
-    } else if (rl > 0xffffffffull) {  // records beyond u32 sizes are not SBE frames we can bound-check in 32 bits
-        d.clear();
+    bool done = !valid;
+    if (valid && rl > 0xffffffffull) {  // beyond 32-bit record sizes: not an SBE frame we bound-check
         d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE
                  : kMode == SBE_DEC_LITE    ? SBE_ST_LITE_E100
                                             : SBE_ST_ERR_TM_E100;
-    } else if (rs >= wb && rs + rl <= we) {
-        const LdsRec R{win, (uint32_t)(rs - wb)};
-        if (kMode == SBE_DEC_ON_EGRESS)
-            dec_on_egress(R, (uint32_t)rl, d);
-        else if (kMode == SBE_DEC_LITE)
-            dec_lite(R, (uint32_t)rl, d);
-        else
-            dec_parse_message(R, (uint32_t)rl, d);
-    } else {
-        const GlbRec R{reinterpret_cast<uintptr_t>(a.in) + rs};
-        if (kMode == SBE_DEC_ON_EGRESS)
-            dec_on_egress(R, (uint32_t)rl, d);
-        else if (kMode == SBE_DEC_LITE)
-            dec_lite(R, (uint32_t)rl, d);
-        else
-            dec_parse_message(R, (uint32_t)rl, d);
+        done = true;
+    }
+    // first window: the whole tile when its records are at most 256 B on average
+    uint64_t wb = T0 & ~15ull;
+    uint64_t we = wb + kWin < end ? wb + kWin : (end > wb ? end : wb);
+    dec_stage(a, win, wb, we, lane);
+    wsync();
+    dec_window<kMode>(win, wb, we, rs, rl, done, d, lane);
+    if (__ballot(!done)) {
+        // later windows start at the first record still to parse; records no window can hold are
+        // parsed from HBM
+#pragma nounroll
+        for (;;) {
+            bool again = false;
+            for (;;) {
+                const uint64_t m = __ballot(!done);
+                if (m == 0) break;
+                const int f = __builtin_ctzll(m);
+                const uint64_t rsf = uniform64(__shfl(rs, f, kWave));
+                const uint64_t rlf = uniform64(__shfl(rl, f, kWave));
+                if ((rsf & 15) + rlf <= kWin && rsf + rlf <= end && rsf >= (T0 & ~15ull)) {
+                    wb = rsf & ~15ull;
+                    again = true;
+                    break;
+                }
+                if (lane == f) {
+                    d = dec_record_glb<kMode>(a.in, rs, (uint32_t)rl);
+                    done = true;
+                }
+            }
+            if (!again) break;
+            we = wb + kWin < end ? wb + kWin : end;
+            wsync();
+            dec_stage(a, win, wb, we, lane);
+            wsync();
+            dec_window<kMode>(win, wb, we, rs, rl, done, d, lane);
+        }
     }
     if (valid) {
         dst_store(a.status + r, (uint8_t)d.status);
@@ -1717,69 +1857,6 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint32_t* win, const 
         }
     }
 }
-
-#if SBE_DEC_PERSIST
-// Persistent: one wave per workgroup loops over tiles t = blockIdx.x, += gridDim.x.  While it
-// parses tile t it holds tile t+G's 16 KiB of staging loads in flight (registers) and tile
-// t+2G's record offsets, so a tile's two dependent HBM round trips hide behind the previous
-// tile's parse.
-template <uint32_t kMode>
-__global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
-    __shared__ uint32_t win[kWinDw];
-    const int lane = threadIdx.x;
-    const uint64_t ntiles = (a.n + kTile - 1) / kTile;
-    const uint64_t G = gridDim.x;
-    uint64_t t = blockIdx.x;
-    if (t >= ntiles) return;
-    DecTile cur = dec_tile_load(a, t, lane);
-    uint64_t wb, we;
-    dec_window(cur, wb, we);
-    uint4 I[kDecRegs];
-    dec_stage_issue(a, wb, we, lane, I);
-    uint64_t tn = t + G;
-    DecTile nxt = dec_tile_load(a, tn < ntiles ? tn : ntiles - 1, lane);
-    dec_stage_write(win, wb, we, lane, I);
-    for (;;) {
-        const bool have_next = tn < ntiles;
-        uint64_t nwb = 0, nwe = 0;
-        DecTile after = nxt;
-        if (have_next) {
-            dec_window(nxt, nwb, nwe);
-            dec_stage_issue(a, nwb, nwe, lane, I);
-            const uint64_t t2 = tn + G;
-            after = dec_tile_load(a, t2 < ntiles ? t2 : ntiles - 1, lane);
-        }
-        wsync();
-        dec_tile<kMode>(a, win, cur, wb, we, t, lane);
-        if (!have_next) break;
-        wsync();
-        dec_stage_write(win, nwb, nwe, lane, I);
-        wsync();
-        cur = nxt;
-        nxt = after;
-        wb = nwb;
-        we = nwe;
-        t = tn;
-        tn += G;
-    }
-}
-#else
-// one workgroup per tile
-template <uint32_t kMode>
-__global__ __launch_bounds__(kWave) void sbe_decode_kernel(DecArgs a) {
-    __shared__ uint32_t win[kWinDw];
-    const int lane = threadIdx.x;
-    const uint64_t t = blockIdx.x;
-    const DecTile cur = dec_tile_load(a, t, lane);
-    uint64_t wb, we;
-    dec_window(cur, wb, we);
-    uint4 I[kDecRegs];
-    dec_stage_issue(a, wb, we, lane, I);
-    dec_stage_write(win, wb, we, lane, I);
-    __syncthreads();
-    dec_tile<kMode>(a, win, cur, wb, we, t, lane);
-}
-#endif
 
 thread_local char g_last_error[256] = "";
 
@@ -2014,14 +2091,7 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     if (tiles > kMaxTiles) return SBE_EINVAL;
     DecArgs a{in, rec_off, n, out->status, out->flags, out->hdr, out->ts, out->view_off, out->view_len};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#if SBE_DEC_PERSIST
-    const void* kfn = mode == SBE_DEC_ON_EGRESS
-                          ? reinterpret_cast<const void*>(&sbe_decode_kernel<SBE_DEC_ON_EGRESS>)
-                          : reinterpret_cast<const void*>(&sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>);
-    const dim3 grid((uint32_t)pack_grid(kfn, tiles)), block(kWave);
-#else
     const dim3 grid((uint32_t)tiles), block(kWave);
-#endif
     hipEvent_t e0, e1;
     prof_slot(1, &e0, &e1);
     if (mode == SBE_DEC_ON_EGRESS)

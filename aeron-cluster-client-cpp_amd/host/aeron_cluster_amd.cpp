@@ -226,54 +226,54 @@ bool ParseResult::is_topic_message() const {
 
 bool gpu_codec_available() { return sbe_device_ready() == 1; }
 
-EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) {
+namespace {
+// Stage a batch of records (nf strings, a u64 and a u32 each) in pinned memory, copy it to HBM,
+// run `launch` (one sbe_encode_*_batch call) and copy the encoded stream back.
+template <class Launch>
+EncodedBatch run_encode(size_t n, int nf, const std::function<std::string_view(size_t, int)>& field,
+                        const std::function<uint64_t(size_t)>& u64, const std::function<uint32_t(size_t)>& u32,
+                        uint64_t bound_per_record, Launch launch) {
     Ctx& c = ctx();
     EncodedBatch b;
-    const size_t n = msgs.size();
     b.offsets.assign(n + 1, 0);
     b.status.assign(n, 0);
     if (n == 0) return b;
     size_t arena = 0;
-    for (const auto& m : msgs) arena += m.topic.size() + m.message_type.size() + m.uuid.size() + m.payload.size() + m.headers.size();
+    for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < nf; ++k) arena += field(i, k).size();
     c.h_arena.need(arena + 16);
-    c.h_len.need(n * 20);
-    c.h_ts.need(n * 8);
+    c.h_len.need(n * 4 * nf);
+    c.h_ts.need(n * 12);
     uint8_t* ap = static_cast<uint8_t*>(c.h_arena.p);
     uint32_t* lp = static_cast<uint32_t*>(c.h_len.p);
     uint64_t* tp = static_cast<uint64_t*>(c.h_ts.p);
+    uint32_t* ip = reinterpret_cast<uint32_t*>(tp + n);
     size_t at = 0;
     for (size_t i = 0; i < n; ++i) {
-        const std::string_view f[5] = {msgs[i].topic, msgs[i].message_type, msgs[i].uuid, msgs[i].payload, msgs[i].headers};
-        for (int k = 0; k < 5; ++k) {
-            std::memcpy(ap + at, f[k].data(), f[k].size());
-            at += f[k].size();
-            lp[5 * i + k] = (uint32_t)f[k].size();
+        for (int k = 0; k < nf; ++k) {
+            const std::string_view f = field(i, k);
+            std::memcpy(ap + at, f.data(), f.size());
+            at += f.size();
+            lp[(size_t)nf * i + k] = (uint32_t)f.size();
         }
-        tp[i] = (uint64_t)msgs[i].timestamp;
+        tp[i] = u64(i);
+        ip[i] = u32(i);
     }
-    // timestamp 0 → the clock the reference reads (src/sbe_encoder.cpp:134-138)
-    const uint64_t now_ms = (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
-                                std::chrono::system_clock::now().time_since_epoch())
-                                .count();
-    const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8 : 0u;
-    const uint64_t cap = sbe_encode_output_bound(n, arena, flags) + 16;
+    const uint64_t cap = arena + bound_per_record * n + 16;
     c.d_arena.need(arena + 16);
-    c.d_len.need(n * 20);
-    c.d_ts.need(n * 8);
+    c.d_len.need(n * 4 * nf);
+    c.d_ts.need(n * 12);
     c.d_out.need(cap);
     c.d_off.need((n + 1) * 8);
     c.d_st.need(n);
-    const size_t wsb = sbe_encode_workspace_size(n);
-    c.d_ws.need(wsb);
+    c.d_ws.need(sbe_encode_workspace_size(n));
     hip_check(hipMemcpyAsync(c.d_arena.p, ap, arena, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_len.p, lp, n * 20, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_ts.p, tp, n * 8, hipMemcpyHostToDevice, c.stream), "H2D");
-    sbe_tm_batch in{static_cast<uint8_t*>(c.d_arena.p), nullptr, static_cast<uint32_t*>(c.d_len.p),
-                    static_cast<uint64_t*>(c.d_ts.p)};
-    if (sbe_encode_topic_batch(&in, n, now_ms, flags, static_cast<uint8_t*>(c.d_out.p), cap,
-                               static_cast<uint64_t*>(c.d_off.p), static_cast<uint8_t*>(c.d_st.p), c.d_ws.p, c.d_ws.cap,
-                               c.stream) != SBE_OK)
-        fail("sbe_encode_topic_batch");
+    hip_check(hipMemcpyAsync(c.d_len.p, lp, n * 4 * nf, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_ts.p, tp, n * 12, hipMemcpyHostToDevice, c.stream), "H2D");
+    const uint64_t* d_u64 = static_cast<const uint64_t*>(c.d_ts.p);
+    launch(static_cast<const uint8_t*>(c.d_arena.p), static_cast<const uint32_t*>(c.d_len.p), d_u64,
+           reinterpret_cast<const uint32_t*>(d_u64 + n), static_cast<uint8_t*>(c.d_out.p), cap,
+           static_cast<uint64_t*>(c.d_off.p), static_cast<uint8_t*>(c.d_st.p), c.d_ws.p, c.d_ws.cap, c.stream);
     hip_check(hipMemcpyAsync(b.offsets.data(), c.d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
     hip_check(hipMemcpyAsync(b.status.data(), c.d_st.p, n, hipMemcpyDeviceToHost, c.stream), "D2H");
     hip_check(hipStreamSynchronize(c.stream), "sync");
@@ -283,6 +283,113 @@ EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields
         hip_check(hipStreamSynchronize(c.stream), "sync");
     }
     return b;
+}
+
+std::string_view tm_field(const TopicMessageFields& m, int k) {
+    switch (k) {
+        case 0: return m.topic;
+        case 1: return m.message_type;
+        case 2: return m.uuid;
+        case 3: return m.payload;
+        default: return m.headers;
+    }
+}
+
+uint64_t clock_ms() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+uint64_t clock_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::high_resolution_clock::now().time_since_epoch())
+        .count();
+}
+
+EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength length, bool session, int64_t term,
+                       int64_t sess, uint64_t ts_default) {
+    const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8 : 0u;
+    return run_encode(
+        msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
+        [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; },
+        SBE_TM_WIRE_OVERHEAD + SBE_SESSION_HDR_LEN,
+        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, uint8_t* out, uint64_t cap,
+            uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+            sbe_tm_batch in{arena, nullptr, len, ts};
+            const int rc = session ? sbe_encode_session_batch(&in, msgs.size(), ts_default, flags, term, sess, out, cap,
+                                                              off, st, ws, wsb, s)
+                                   : sbe_encode_topic_batch(&in, msgs.size(), ts_default, flags, out, cap, off, st, ws,
+                                                            wsb, s);
+            if (rc != SBE_OK) fail(session ? "sbe_encode_session_batch" : "sbe_encode_topic_batch");
+        });
+}
+}  // namespace
+
+EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) {
+    // timestamp 0 → the clock the reference reads (src/sbe_encoder.cpp:134-138)
+    return encode_tm(msgs, length, false, 0, 0, clock_ms());
+}
+
+EncodedBatch SessionFrameEncoder::encode_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) const {
+    // create_topic_message stamps high_resolution_clock nanoseconds (src/session_manager.cpp:1075-1076)
+    return encode_tm(msgs, length, true, leadership_term_id_, cluster_session_id_, clock_ns());
+}
+
+std::vector<std::uint8_t> SessionFrameEncoder::create_combined_message(const std::string& topic,
+                                                                       const std::string& message_type,
+                                                                       const std::string& message_id,
+                                                                       const std::string& payload,
+                                                                       const std::string& headers) const {
+    TopicMessageFields f{topic, message_type, message_id, payload, headers, 0};
+    EncodedBatch b = encode_batch({f}, EncodeLength::Reference);
+    const uint8_t st = b.status[0];
+    if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
+    if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
+    return b.bytes;
+}
+
+std::uint32_t CommitManager::topic_to_id(const std::string& topic) {
+    if (topic == "order_request_topic") return 1;
+    if (topic == "order_notification_topic") return 2;
+    if (topic == "orders") return 3;
+    if (topic == "order_status_request_topic") return 4;
+    return 0;
+}
+
+EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOffset>& offsets) const {
+    std::vector<uint32_t> ids(offsets.size());
+    for (size_t i = 0; i < offsets.size(); ++i) {
+        ids[i] = topic_to_id(offsets[i].topic);
+        if (ids[i] == 0)
+            throw std::runtime_error("sbecodec: commit offset for unknown topic '" + offsets[i].topic +
+                                     "' needs the jsoncpp TopicMessage fallback (not built)");
+    }
+    return run_encode(
+        offsets.size(), 2,
+        [&](size_t i, int k) { return std::string_view(k == 0 ? offsets[i].message_id : offsets[i].message_identifier); },
+        [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; },
+        SBE_LITE_OVERHEAD(2),
+        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid, uint8_t* out,
+            uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+            sbe_lite_batch in{arena, nullptr, len, tid, seq};
+            if (sbe_encode_lite_batch(&in, offsets.size(), SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
+                                      wsb, s) != SBE_OK)
+                fail("sbe_encode_lite_batch");
+        });
+}
+
+std::vector<std::uint8_t> CommitManager::build_commit_offset_message(const std::string& topic,
+                                                                     const std::string& client_id,
+                                                                     const CommitOffset& offset) const {
+    (void)topic;  // the reference keys the template on offset.topic (src/commit_manager.cpp:110)
+    (void)client_id;
+    EncodedBatch b = build_commit_offset_batch({offset});
+    static const char* kLiteE109[2] = {"messageIdLength too long for length type [E109]",
+                                       "messageIdentifierLength too long for length type [E109]"};
+    const uint8_t st = b.status[0];
+    if (st == 1 || st == 2) throw std::runtime_error(kLiteE109[st - 1]);
+    if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
+    return b.bytes;
 }
 
 std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
@@ -337,6 +444,20 @@ std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len) {
     const uint64_t off[2] = {0, len};
     Desc d = run_decode(data, off, 1, SBE_DEC_ON_EGRESS);
     return ack_from(data, d, 0);
+}
+
+std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len) {
+    if (!data || len < 8) return std::nullopt;
+    const uint64_t off[2] = {0, len};
+    Desc d = run_decode(data, off, 1, SBE_DEC_LITE);
+    if (d.status[0] != SBE_ST_LITE) return std::nullopt;
+    LiteRecord r;
+    r.template_id = d.hdr[1];
+    r.topic_id = d.off[4];
+    r.sequence = d.ts[0];
+    const int nf = (int)sbe_lite_fields(r.template_id);
+    for (int k = 0; k < nf; ++k) r.fields.emplace_back(reinterpret_cast<const char*>(data) + d.off[k], d.len[k]);
+    return r;
 }
 
 MessageHandler::MessageHandler() = default;

@@ -9,6 +9,11 @@
 //   decode_ack / AckInfo               include/aeron_cluster/ack_decoder.hpp:9-19, src/ack_decoder.cpp:29-105
 //   MessageHandler::on_egress          include/aeron_cluster/message_handler.hpp:35-89 (E100 escapes
 //                                      as std::runtime_error("buffer too short [E100]"))
+//   SessionManager frame               create_topic_message + send_combined_message,
+//                                      src/session_manager.cpp:936-967, :1018-1046, :1050-1144
+//   CommitManager                      build_commit_offset_message (CommitOffsetLite),
+//                                      src/commit_manager.cpp:16-22, :107-132; CommitOffset
+//                                      include/aeron_cluster/commit_manager.hpp:17-24
 //   ClusterClient::offer_ingress       include/aeron_cluster/cluster_client.hpp:409 — the sink the
 //                                      encoded records are handed to (OfferFn below)
 // plus batched overloads, which are the point of the GPU path: one launch per batch.
@@ -140,6 +145,62 @@ private:
     TopicMessageCallback tm_cb_;
     AckCallback ack_cb_;
 };
+
+// The frame SessionManager::Impl publishes (src/session_manager.cpp:1050-1144): the 32-B
+// SessionMessageHeader {24, 1, 111, 8, leadershipTermId, clusterSessionId, 0} followed by
+// create_topic_message's record (26+Σlen bytes, timestamp = high_resolution_clock nanoseconds).
+class SessionFrameEncoder {
+public:
+    // update_session_header (:1018-1046)
+    void update_session_header(std::int64_t leadership_term_id, std::int64_t cluster_session_id) {
+        leadership_term_id_ = leadership_term_id;
+        cluster_session_id_ = cluster_session_id;
+    }
+    // One frame as send_combined_message builds it (:1118-1144); throws E109 like
+    // create_topic_message (:1111-1114).
+    std::vector<std::uint8_t> create_combined_message(const std::string& topic, const std::string& message_type,
+                                                      const std::string& message_id, const std::string& payload,
+                                                      const std::string& headers) const;
+    // Batch: one GPU launch.  A message's timestamp 0 → the nanosecond clock.
+    EncodedBatch encode_batch(const std::vector<TopicMessageFields>& msgs,
+                              EncodeLength length = EncodeLength::Reference) const;
+
+private:
+    std::int64_t leadership_term_id_ = 0, cluster_session_id_ = 0;
+};
+
+// include/aeron_cluster/commit_manager.hpp:17-24
+struct CommitOffset {
+    std::string topic;
+    std::string message_identifier;
+    std::string message_id;
+    std::uint64_t timestamp_nanos = 0;
+    std::uint64_t sequence_number = 0;
+};
+
+class CommitManager {
+public:
+    // src/commit_manager.cpp:16-22
+    static std::uint32_t topic_to_id(const std::string& topic);
+    // src/commit_manager.cpp:107-132: a known topic → CommitOffsetLite (template 301) with topicId,
+    // sequence, messageId, messageIdentifier; E109 → std::runtime_error.  The unknown-topic
+    // fallback (a jsoncpp-formatted TopicMessage, :134-160) is not built: it throws.
+    std::vector<std::uint8_t> build_commit_offset_message(const std::string& topic, const std::string& client_id,
+                                                          const CommitOffset& offset) const;
+    // Batch (one GPU launch); every offset's topic must be known.
+    EncodedBatch build_commit_offset_batch(const std::vector<CommitOffset>& offsets) const;
+};
+
+// A decoded Lite record (CommitOffsetLite / OrderRequestLite / OrderNotificationLite flyweights).
+struct LiteRecord {
+    std::uint16_t template_id = 0;
+    std::uint32_t topic_id = 0;
+    std::uint64_t sequence = 0;
+    std::vector<std::string> fields;  // var strings in wire order (2 or 3)
+};
+// Decoded with the generated flyweights' semantics; nullopt when the record is not a Lite
+// template or a bounds check throws E100.
+std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len);
 
 // The raw ingress sink (ClusterClient::offer_ingress signature).  Feeds every encoded record of a
 // batch to it in order; returns the number accepted before the first refusal.

@@ -1,0 +1,153 @@
+"""Per-row measurement of the SURVEY §8 rows beyond the headline bench: one JSON line per workload
+with records/s (whole calls, device-resident), each dominant kernel's HIP-event duration, its
+algorithmic bytes per launch (computed from the actual record sizes) and its fraction of the
+8 TB/s HBM peak.  Rows:
+  config3_mixed_decode   1 M mixed TopicMessage / Ack records, parse_message
+  config4_var_roundtrip  16 M variable-length TopicMessages, encode + parse decode (config 4)
+  session_fixed256       1 M session-framed Order TopicMessages (32-B SessionMessageHeader + 248 B)
+  lite301 / lite201      1 M CommitOffsetLite / OrderRequestLite records, encode + Lite decode
+Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...]  (GPU only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "aeron-cluster-client-cpp_amd"), os.path.join(ROOT, "tests")]
+import sbe_testlib as T  # noqa: E402
+import sbecodec  # noqa: E402
+
+PEAK = 8000.0
+DESC = 1 + 1 + 8 + 8 + 40  # decode descriptor bytes written per record
+
+
+def dev(a, dt):
+    return torch.from_numpy(np.ascontiguousarray(a).view({torch.uint8: np.uint8, torch.int32: np.int32,
+                                                           torch.int64: np.int64}[dt])).to("cuda")
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    sbecodec.profile_enable(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pack = sbecodec.profile_read(sbecodec.PROF_PACK)
+    deck = sbecodec.profile_read(sbecodec.PROF_DECODE)
+    sbecodec.profile_enable(0)
+    return el / steps, (float(np.mean(pack)) if pack else None), (float(np.mean(deck)) if deck else None)
+
+
+def line(row, n, step_s, kernels):
+    out = {"row": row, "records": n, "records_per_s": n / step_s, "ms_per_step": step_s * 1e3, "kernels": {}}
+    for name, (ms, nbytes) in kernels.items():
+        if ms is None:
+            continue
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out["kernels"][name] = {"ms": ms, "alg_bytes": nbytes, "GBps": gbs, "frac": gbs / PEAK}
+    print(json.dumps(out), flush=True)
+
+
+def row_mixed(steps, warmup):
+    n = 1_000_000
+    data, off = T.mixed_records(n)
+    d, o = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
+    out = sbecodec.alloc_decoded(n, "cuda")
+    s, _, dk = timed(lambda: sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out), steps, warmup)
+    line("config3_mixed_decode", n, s, {"sbe_decode_kernel<parse_message>": (dk, int(off[-1]) + 8 * n + DESC * n)})
+
+
+def row_var(steps, warmup):
+    n = 16_777_216
+    arena, L, ts = T.var_orders(n)
+    a, l, t = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32), dev(ts.view(np.int64), torch.int64)
+    cap = sbecodec.output_bound(n, arena.size)
+    ob = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ws = sbecodec.alloc_workspace(n, "cuda")
+    dec = sbecodec.alloc_decoded(n, "cuda")
+
+    def step():
+        sbecodec.encode_topic_batch(a, l, t, out=ob, out_off=oo, status=st, workspace=ws)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec)
+
+    s, pk, dk = timed(step, steps, warmup)
+    outb = int(arena.size) + 34 * n
+    line("config4_var_roundtrip", n, s, {"sbe_enc_pack<packed,wire>": (pk, arena.size + 28 * n + outb + 9 * n),
+                                         "sbe_decode_kernel<parse_message>": (dk, outb + 8 * n + DESC * n)})
+
+
+def row_session(steps, warmup):
+    n = 1_000_000
+    arena, L, ts = T.fixed256_orders(n)
+    a, l, t = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32), dev(ts.view(np.int64), torch.int64)
+    ob = torch.empty(sbecodec.output_bound(n, arena.size), dtype=torch.uint8, device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ws = sbecodec.alloc_workspace(n, "cuda")
+    dec = sbecodec.alloc_decoded(n, "cuda")
+
+    def step():
+        sbecodec.encode_session_batch(a, l, t, 7, 8, out=ob, out_off=oo, status=st, workspace=ws)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec)
+
+    s, pk, dk = timed(step, steps, warmup)
+    rec = 32 + 248
+    line("session_fixed256", n, s, {"sbe_enc_pack<session,packed,ref>": (pk, n * (222 + 28 + rec + 9)),
+                                    "sbe_decode_kernel<parse_message>": (dk, n * (rec + 8 + DESC))})
+
+
+def row_lite(t_id, steps, warmup):
+    n = 1_000_000
+    nf = T.LITE_NF[t_id]
+    arena, L, tid, seq = T.lite_records(n, t_id)
+    a, l = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32)
+    ti, sq = dev(tid.view(np.int32), torch.int32), dev(seq.view(np.int64), torch.int64)
+    cap = arena.size + (20 + 2 * nf) * n + 16
+    ob = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ws = sbecodec.alloc_workspace(n, "cuda")
+    dec = sbecodec.alloc_decoded(n, "cuda")
+
+    def step():
+        sbecodec.encode_lite_batch(t_id, a, l, ti, sq, out=ob, out_off=oo, status=st, workspace=ws)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_LITE, out=dec)
+
+    s, pk, dk = timed(step, steps, warmup)
+    outb = arena.size + (20 + 2 * nf) * n
+    line(f"lite{t_id}", n, s, {f"sbe_enc_pack<lite{nf},packed>": (pk, arena.size + (4 * nf + 12) * n + outb + 9 * n),
+                               "sbe_decode_kernel<lite>": (dk, outb + 8 * n + DESC * n)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201")
+    args = ap.parse_args()
+    sbecodec.require_device()
+    for r in args.rows.split(","):
+        if r == "mixed":
+            row_mixed(args.steps, args.warmup)
+        elif r == "var":
+            row_var(max(args.steps // 2, 5), args.warmup)
+        elif r == "session":
+            row_session(args.steps, args.warmup)
+        elif r.startswith("lite"):
+            row_lite(int(r[4:]), args.steps, args.warmup)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -181,6 +181,69 @@ int main() {
             if (failures > 20) break;
         }
     }
+    // ---- session frames (src/session_manager.cpp:936-967, :1050-1144) ----
+    {
+        SessionFrameEncoder sf;
+        sf.update_session_header(0x0102030405060708LL, -2);
+        auto fr = sf.create_combined_message("orders", "CREATE_ORDER", "msg_1", "{\"a\":1}", "{\"h\":2}");
+        CHECK(fr.size() == 32 + 63);
+        CHECK(hex(fr).rfind("180001006f000800" "0807060504030201" "feffffffffffffff" "0000000000000000" "1000010001000100", 0) == 0);
+        uint64_t ns = 0;
+        std::memcpy(&ns, fr.data() + 40, 8);
+        CHECK(ns > 1700000000000000000ULL);  // high_resolution_clock nanoseconds (:1075-1076)
+        auto pr = MessageParser::parse_message(fr.data(), fr.size());
+        CHECK(pr.success && pr.message_id == "msg_1" && pr.payload == "{\"a\":1}" && pr.block_length == 16);
+        try {
+            sf.create_combined_message(std::string(65535, 'x'), "", "", "", "");
+            CHECK(false);
+        } catch (const std::runtime_error& ex) {
+            CHECK(std::string(ex.what()) == "topicLength too long for length type [E109]");
+        }
+        std::vector<TopicMessageFields> msgs;
+        for (size_t i = 0; i < recs.size(); ++i)
+            msgs.push_back({recs[i][0], recs[i][1], recs[i][2], recs[i][3], recs[i][4], (int64_t)tss[i]});
+        EncodedBatch b = sf.encode_batch(msgs, EncodeLength::Wire);
+        std::vector<uint8_t> eo(arena.size() + 66 * recs.size() + 16);
+        std::vector<uint64_t> eoff(recs.size() + 1);
+        std::vector<uint8_t> est(recs.size());
+        orc_encode_session_batch(reinterpret_cast<const uint8_t*>(arena.data()), nullptr, lens.data(), tss.data(),
+                                 recs.size(), 0, 0, 0x0102030405060708LL, -2, eo.data(), eoff.data(), est.data(), 1);
+        CHECK(b.offsets == eoff);
+        CHECK(b.bytes.size() == eoff.back() && std::memcmp(b.bytes.data(), eo.data(), b.bytes.size()) == 0);
+    }
+    // ---- CommitOffsetLite (src/commit_manager.cpp:107-132) ----
+    {
+        CommitManager cm;
+        CommitOffset o;
+        o.topic = "orders";
+        o.message_identifier = "orders:17";
+        o.message_id = "msg_42";
+        o.sequence_number = 0x1122334455667788ULL;
+        auto m = cm.build_commit_offset_message("orders", "client", o);
+        CHECK(m.size() == 24 + 6 + 9);
+        CHECK(hex(m) == "0c002d0101000100" "03000000" "8877665544332211" "0600" + hex(std::vector<uint8_t>(o.message_id.begin(), o.message_id.end())) +
+                            "0900" + hex(std::vector<uint8_t>(o.message_identifier.begin(), o.message_identifier.end())));
+        auto lr = decode_lite(m.data(), m.size());
+        CHECK(lr && lr->template_id == 301 && lr->topic_id == 3 && lr->sequence == o.sequence_number &&
+              lr->fields.size() == 2 && lr->fields[0] == "msg_42" && lr->fields[1] == "orders:17");
+        CHECK(!decode_lite(m.data(), m.size() - 1));  // E100
+        o.topic = "nope";
+        bool threw = false;
+        try {
+            cm.build_commit_offset_message("nope", "c", o);
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+        CHECK(threw);
+        o.topic = "order_request_topic";
+        o.message_id = std::string(65535, 'q');
+        try {
+            cm.build_commit_offset_message("x", "c", o);
+            CHECK(false);
+        } catch (const std::runtime_error& ex) {
+            CHECK(std::string(ex.what()) == "messageIdLength too long for length type [E109]");
+        }
+    }
     std::printf("host api test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -171,6 +171,45 @@ def test_decode_seq_key_positions(codec, mode):
         assert_same_decode(gpu_decode(codec, data, off, mode), exp)
 
 
+def long_seq_key_records(seed):
+    """Payloads longer than the per-lane scan limit (the window-wide scan path): keys at random
+    positions and alignments, keys in the other fields only (never flagged), several keys per
+    record (a lane's chunks with two hits: the per-lane fallback), split keys, near misses."""
+    key = b"_sequence_number"
+    rng = np.random.default_rng(seed)
+    recs = []
+    for k in range(700):
+        plen = int(rng.integers(257, 700)) if k % 5 else int(rng.integers(16, 256))
+        pay = bytearray(rng.choice(np.frombuffer(b"q_sequnbr{}:,", np.uint8), plen).tobytes())
+        kind = k % 7
+        if kind in (0, 1, 2):
+            at = int(rng.integers(0, plen - 15))
+            pay[at:at + 16] = key
+        if kind == 2 and plen > 80:
+            at = int(rng.integers(0, plen - 15))
+            pay[at:at + 16] = key
+        if kind == 3:
+            at = int(rng.integers(0, plen - 15))
+            pay[at:at + 16] = key[:9] + b"X" + key[10:]
+        other = key if kind == 4 else b"id"
+        if kind == 5:  # split between payload and headers
+            pay[-5:] = key[:5]
+            recs.append(T.tm_wire([b"orders", b"T", other, bytes(pay), key[5:] + b"zz"], k))
+            continue
+        recs.append(T.tm_wire([b"orders", other, b"u" * (k % 5), bytes(pay), b"{}"], k))
+    return recs
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_decode_seq_key_long_payloads(codec, seed):
+    recs = long_seq_key_records(seed)
+    for lead in (0, 3, 8):
+        data, off = T.pack_records([b"\0" * lead] + recs)
+        exp = T.oracle_decode(data, off, T.DEC_PARSE)
+        assert 100 < int((exp["flags"] & T.FL_SEQ_KEY != 0).sum()) < len(recs)
+        assert_same_decode(gpu_decode(codec, data, off, T.DEC_PARSE), exp)
+
+
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
 def test_decode_mixed(codec, mode):
     data, off = T.mixed_records(50000)
