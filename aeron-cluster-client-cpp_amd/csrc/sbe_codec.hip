@@ -578,8 +578,6 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     return S;
 }
 
-// one output window covers the tile: the pipelined path
-__device__ __forceinline__ bool single_window(const TileSt& S) { return S.len + (uint32_t)(S.T0 & 15) <= (uint32_t)kEW; }
 
 // Staged input range for the output window starting wrel bytes from T0: from the first string
 // byte at/after max(wrel, 0) (input offset >= p - kOvh within the record holding it) for kEWIn
@@ -865,20 +863,23 @@ __device__ __forceinline__ void put_clip(lds_u8* wout, int32_t d, uint32_t v, in
 // (wave-uniform) when some record of the window has strings outside the staged input.
 template <class LY>
 __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t* sbase, const TileSt& S,
-                                             int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int lane) {
+                                             int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int ra, int rb,
+                                             int lane) {
     const int q = lane % kLpr, r = lane / kLpr;
-    bk[lane] = 0;
+    bk[lane] = ra;
     bool outside = false;
     if (q == 0) {
+        // records outside [ra, rb) compose nothing in this window
+        const bool live = S.rec_out && r >= ra && r < rb;
         const int32_t rw = (int32_t)S.rs - wrel;
-        const int32_t rend = (S.rec_out ? (int32_t)S.pe_rec : (int32_t)S.rs) - wrel;
+        const int32_t rend = (live ? (int32_t)S.pe_rec : (int32_t)S.rs) - wrel;
         const uint64_t s0 = S.in_tile + S.in0;                 // absolute address of string 0
         const int64_t src0 = (int64_t)s0 - (int64_t)swb;       // its staged position
         uint32_t nstr = 0;
 #pragma unroll
         for (int f = 0; f < 5; ++f) nstr += S.L[f];
         const bool staged = src0 >= 0 && src0 + (int64_t)nstr <= (int64_t)nb;
-        outside = S.rec_out && !staged && rend > (rw > 0 ? rw : 0) && (rw < wlen);
+        outside = live && !staged && rend > (rw > 0 ? rw : 0) && (rw < wlen);
         i32x4 a, b;
         a.x = rw;
         a.y = rend;
@@ -905,7 +906,7 @@ __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t*
         // buckets bb with bb*kLaneBytes inside [rw, rend) ∩ [0, wlen)
         const int32_t s1 = rw > 0 ? rw : 0;
         const int32_t e1 = rend < wlen ? rend : wlen;
-        if (S.rec_out && s1 < e1) {
+        if (live && s1 < e1) {
             for (int32_t bb = (s1 + kLaneBytes - 1) / kLaneBytes; bb * kLaneBytes < e1; ++bb) bk[bb] = r;
         }
     }
@@ -1069,8 +1070,8 @@ __device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, ld
 template <class LY>
 __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk,
                                             uint64_t* sbase, const TileSt& S, int32_t wrel, int32_t wlen,
-                                            uintptr_t swb, int32_t nb, int lane) {
-    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, lane);
+                                            uintptr_t swb, int32_t nb, int lane, int ra = 0, int rb = kRpt) {
+    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lane);
     wsync();
 #ifndef SBE_ABL_NO_CHUNK
     chunk_pass(wout, inb, rt, bk, wlen, nb, lane);
@@ -1083,6 +1084,44 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
 #ifndef SBE_ABL_NO_LITERAL
     literal_pass<LY>(ea, wout, rt, S, wlen, lane);
 #endif
+}
+
+// A tile whose output exceeds the window is split at record boundaries: window [ra, rb) holds
+// whole records only (none straddles, so all of them are staged), output bytes [wrel, wrel+wlen)
+// relative to T0 with wrel the 16-B aligned start below record ra's first byte A, and staged
+// input [swb, swb+nb) = the strings of records [ra, rb).  A tile with a record longer than the
+// window minus 16 bytes takes the byte-window path instead (tile_big).
+struct Win {
+    int ra, rb;
+    int32_t wrel, wlen;
+    uint32_t A;
+    uintptr_t swb;
+    int32_t nb;
+};
+
+__device__ __forceinline__ bool tile_big(const TileSt& S, int lane) {
+    return __ballot(lane % kLpr == 0 && S.rec_out > (uint32_t)(kEW - 16)) != 0;
+}
+
+__device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, uintptr_t sink) {
+    Win W;
+    const int q = lane % kLpr, r = lane / kLpr;
+    W.ra = ra;
+    W.A = __builtin_amdgcn_readfirstlane(__shfl(S.rs, ra * kLpr, kWave));
+    W.wrel = (int32_t)W.A - (int32_t)((S.T0 + W.A) & 15u);
+    // records from ra whose (capacity-clipped) end fits: ends are non-decreasing, so a prefix
+    const bool fits = q == 0 && r >= ra && (int32_t)S.pe_rec - W.wrel <= kEW;
+    const int cnt = __builtin_popcountll(__ballot(fits));
+    W.rb = ra + (cnt > 0 ? cnt : 1);
+    const uint32_t B = __builtin_amdgcn_readfirstlane(__shfl(S.pe_rec, (W.rb - 1) * kLpr, kWave));
+    W.wlen = (int32_t)B - W.wrel;
+    const uint64_t ia = uniform64(__shfl(S.in0, ra * kLpr, kWave));
+    const uint64_t ib = W.rb < kRpt ? uniform64(__shfl(S.in0, W.rb * kLpr, kWave)) : (uint64_t)S.agg_in;
+    W.swb = (S.in_tile + ia) & ~(uintptr_t)15;
+    const uintptr_t end = (S.in_tile + ib + 15) & ~(uintptr_t)15;
+    W.nb = (int32_t)(end - W.swb < (uintptr_t)kEWIn ? end - W.swb : (uintptr_t)kEWIn);
+    if (W.nb == 0) W.swb = sink;  // stage_issue reads 16 bytes at swb even then
+    return W;
 }
 
 template <class LY, bool kPacked, bool kTrunc>
@@ -1106,66 +1145,56 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
     TileIn x = tile_load<LY, kPacked>(a, t, lane, sb_next);
     TileSt S = tile_prepare<LY, kPacked, kTrunc>(a, x, t, lane, sp_out, sp_in);
     uint4 I[kStageRegs];
-    uintptr_t swb = 0;
-    int32_t nb = 0;
-    bool fast = kPacked && single_window(S);
-    if (fast) {
-        stage_range<LY>(S, -(int32_t)(S.T0 & 15), lane, swb, nb);
-    } else {
-        swb = reinterpret_cast<uintptr_t>(a.sink);
-        nb = 0;
-    }
+    const uintptr_t sink = reinterpret_cast<uintptr_t>(a.sink);
+    Win W{0, kRpt, 0, 0, 0, sink, 0};
+    bool fast = kPacked && !tile_big(S, lane);
+    if (fast) W = tile_window(S, 0, lane, sink);
     if (kPacked) {
-        stage_issue(swb, nb, lane, I);
-        stage_write(win_in, nb, lane, I);
+        stage_issue(W.swb, W.nb, lane, I);
+        stage_write(win_in, W.nb, lane, I);
     }
     uint64_t tn = t + G;
     x = tile_load<LY, kPacked>(a, tn < ntiles ? tn : ntiles - 1, lane, sb_next);
 
-    // Steady state, per tile: [next tile: prepare, lengths of the one after, staging loads]
-    // [compose + store this tile] [next tile's staged input → LDS].  The staging registers are
-    // written to LDS after this tile's stores, so that wait leaves exactly those stores in flight.
+    // Steady state, per window: [next window of this tile, or the next tile (prepare, lengths of
+    // the one after): staging loads] [compose + store this window] [next window's staged input →
+    // LDS].  The staging registers are written to LDS after this window's stores, so that wait
+    // leaves exactly those stores in flight.
     for (;;) {
-        const uintptr_t cur_swb = swb;
-        const int32_t cur_nb = nb;
-        const bool cur_fast = fast;
-        const bool have_next = tn < ntiles;
+        const bool more_win = fast && W.rb < kRpt && W.wrel + W.wlen < (int32_t)S.len;
+        const bool have_next = more_win || tn < ntiles;
         TileSt Sn;
-        if (have_next) {
+        Win Wn{0, kRpt, 0, 0, 0, sink, 0};
+        bool fast_n = false;
+        if (more_win) {
+            Wn = tile_window(S, W.rb, lane, sink);
+            fast_n = true;
+        } else if (have_next) {
             Sn = tile_prepare<LY, kPacked, kTrunc>(a, x, tn, lane, sp_out, sp_in);
             const uint64_t t2 = tn + G;
             x = tile_load<LY, kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
-            fast = kPacked && single_window(Sn);
-            if (fast) {
-                stage_range<LY>(Sn, -(int32_t)(Sn.T0 & 15), lane, swb, nb);
-            } else {
-                swb = reinterpret_cast<uintptr_t>(a.sink);
-                nb = 0;
-            }
-            if (kPacked) stage_issue(swb, nb, lane, I);
+            fast_n = kPacked && !tile_big(Sn, lane);
+            if (fast_n) Wn = tile_window(Sn, 0, lane, sink);
         }
-        // current tile: compose + store, one window (fast) or window by window
-        const int32_t wrel0 = -(int32_t)(S.T0 & 15);
-        if (cur_fast) {
-            if (kPacked) {
-                pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, wrel0, (int32_t)S.len - wrel0, cur_swb, cur_nb, lane);
-            } else {
-                wsync();
-                compose<LY, false>(a, wout, win_in, S, wrel0, (int32_t)S.len, cur_swb, cur_nb);
-            }
+        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
+        // current window (fast) or the whole tile window by window
+        if (fast) {
+            pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
 #ifndef SBE_ABL_NO_STORE
-            store_window(a.out, a.sink, wout, S.T0, S.T0 & ~15ull, S.T0 + S.len, lane);
+            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, S.T0 + (int64_t)(W.wrel + W.wlen),
+                         lane);
 #endif
             wsync();
         } else {
+            const int32_t wrel0 = -(int32_t)(S.T0 & 15);
             for (int32_t wrel = wrel0; wrel < (int32_t)S.len; wrel += kEW) {
                 const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
                 uintptr_t sw = 0;
                 int32_t nbw = 0;
                 if (kPacked) {
                     stage_range<LY>(S, wrel, lane, sw, nbw);
-                    // I holds the next tile's prefetch: stage this window in batches of 3 chunks
+                    // I holds the next item's prefetch: stage this window in batches of 3 chunks
                     for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
                         uint4 J[3];
 #pragma unroll
@@ -1192,10 +1221,14 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
             }
         }
         if (!have_next) break;
-        if (kPacked) stage_write(win_in, nb, lane, I);  // after the compose above read win_in
+        if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in
         wsync();
-        S = Sn;
-        tn += G;
+        if (!more_win) {
+            S = Sn;
+            tn += G;
+        }
+        W = Wn;
+        fast = fast_n;
     }
 }
 

@@ -25,6 +25,7 @@ if PKG not in sys.path:
 
 # status / flag constants (include/sbecodec.h)
 ENC_REF_TRUNCATE8 = 1
+ENC_OVERFLOW = 6
 DEC_PARSE, DEC_EGRESS, DEC_LITE = 0, 1, 2
 ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
 LITE_NF = {301: 2, 201: 3, 202: 3}

@@ -245,3 +245,38 @@ def test_roundtrip_materialized(codec, flags):
         assert pr["timestamp"] == int(ts[i]) and pr["block_length"] == 16
         # wire form keeps headers; the reference-truncated form loses them to E100
         assert pr["headers"] == (b"" if flags else f[4])
+
+
+@pytest.mark.parametrize("kind", ["fixed", "var", "session"])
+def test_encode_capacity_overflow(codec, kind):
+    """out_capacity smaller than the stream: records ending past it get SBE_ENC_OVERFLOW, offsets
+    are unchanged, every record that fits is bit-exact, and nothing is written past the capacity."""
+    if kind == "var":
+        arena, L, ts = T.var_orders(3000, seed=21)
+    else:
+        arena, L, ts = T.fixed256_orders(3000)
+    if kind == "session":
+        eo, eoff, est = T.oracle_encode_session(arena, L, ts, 5, 6)
+    else:
+        eo, eoff, est = T.oracle_encode(arena, L, ts)
+    for cap in (int(eoff[-1]) // 3 + 5, int(eoff[-1]) - 1, 4096 + 7):
+        guard = 8192
+        big = torch.full((cap + guard,), 0xAB, dtype=torch.uint8, device="cuda")
+        a = to_dev(arena, torch.uint8)
+        l = to_dev(L.view(np.int32), torch.int32)
+        t = to_dev(ts.view(np.int64), torch.int64)
+        if kind == "session":
+            enc = codec.encode_session_batch(a, l, t, 5, 6, flags=0, out=big[:cap])
+        else:
+            enc = codec.encode_topic_batch(a, l, t, out=big[:cap])
+        torch.cuda.synchronize()
+        off = enc.out_off.cpu().numpy().view(np.uint64)
+        st = enc.status.cpu().numpy()
+        np.testing.assert_array_equal(off, eoff)
+        fits = eoff[1:] <= cap
+        np.testing.assert_array_equal(st[fits], est[fits])
+        assert (st[~fits] == T.ENC_OVERFLOW).all()
+        got = big.cpu().numpy()
+        assert (got[cap:] == 0xAB).all(), "write past out_capacity"
+        last = int(eoff[1:][fits][-1]) if fits.any() else 0
+        np.testing.assert_array_equal(got[:last], eo[:last])
