@@ -14,10 +14,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
-KERNELS = {"sbe_enc_pack<true, false>": "sbe_enc_pack<packed,wire>",
+# rocprof kernel names (TopicMessage layout Lay<0, 16, 5, true>, packed input, wire length)
+KERNELS = {"sbe_enc_pack<(anonymous namespace)::Lay<0, 16, 5, true>, true, false>": "sbe_enc_pack<packed,wire>",
            "sbe_decode_kernel<0u>": "sbe_decode_kernel<parse_message>",
-           "sbe_enc_sums<true, false>": "sbe_enc_sums<packed,wire>",
-           "sbe_enc_scan": "sbe_enc_scan"}
+           "sbe_enc_sums<(anonymous namespace)::Lay<0, 16, 5, true>, true, false>": "sbe_enc_sums<packed,wire>"}
 
 
 def short(name):
