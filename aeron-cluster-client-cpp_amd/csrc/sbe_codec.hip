@@ -145,7 +145,7 @@ __device__ __forceinline__ void dst_store(T* p, T v) {
 #ifndef SBE_ENC_RPT
 #define SBE_ENC_RPT 32
 #endif
-constexpr int kSbRec = 4096;                          // records per superblock (one K1 workgroup)
+constexpr int kSbRec = 2 * 64 * SBE_ENC_RPT;          // records per superblock (one K1 workgroup): 128 tiles
 constexpr int kSbThreads = 1024;
 constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
 constexpr int kLpr = kWave / kRpt;                    // lanes per record in K3
@@ -1358,6 +1358,16 @@ __device__ bool has_seq_key(const R_t& R, uint32_t p, uint32_t n) {
     return false;
 }
 
+// 0 iff some dword of v equals one of the four key slices (the candidates of seq_key_at); the
+// in-chunk swizzle only permutes dwords, which this membership test does not care about
+__device__ __forceinline__ uint32_t slice_dist(uint32_t w) {
+    const uint32_t a = min(w ^ kSeqK0, w ^ kSeqS1), b = min(w ^ kSeqS2, w ^ kSeqS3);
+    return min(a, b);
+}
+__device__ __forceinline__ bool has_slice(uint4 v) {
+    return min(min(slice_dist(v.x), slice_dist(v.y)), min(slice_dist(v.z), slice_dist(v.w))) == 0u;
+}
+
 __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte of w equal to 'q' (plus borrow noise above a hit)
     const uint32_t x = w ^ 0x71717171u;
     return (x - 0x01010101u) & ~x;
@@ -1376,7 +1386,7 @@ __device__ bool has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
         const uint4 v1 = c + 1 < c1 ? lds_read_chunk_raw(R.win, c + 1) : make_uint4(0, 0, 0, 0);
         const uint32_t t0 = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w)) & 0x80808080u;
         const uint32_t t1 = (q_bytes(v1.x) | q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
-        if (t0 | t1) {
+        if ((t0 | t1) && (has_slice(v0) || has_slice(v1))) {
 #pragma nounroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t A = 16 * c + 4 * k;  // window offset of an aligned dword
@@ -1426,7 +1436,7 @@ __device__ __forceinline__ void window_seq_scan(const uint32_t* win, uint32_t nb
         const uint32_t c = lane + kWave * k;
         const uint4 v = c < nch ? lds_read_chunk_raw(win, c) : make_uint4(0, 0, 0, 0);
         const uint32_t t = (q_bytes(v.x) | q_bytes(v.y) | q_bytes(v.z) | q_bytes(v.w)) & 0x80808080u;
-        if (t) {
+        if (t && has_slice(v)) {
 #pragma nounroll
             for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t A = 16 * c + 4 * j;
