@@ -55,11 +55,17 @@ def parse_args():
     return p.parse_args()
 
 
+def launched_distributed():
+    """Started by torch.distributed.run (even at one process): RCCL is initialised, so a one-GPU
+    run exercises the same barrier / max-over-ranks path the multi-GPU runs take."""
+    return "LOCAL_RANK" in os.environ and "MASTER_ADDR" in os.environ
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or launched_distributed():
         torch.cuda.set_device(local)
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -68,14 +74,19 @@ def setup_dist(args):
     return world, rank, local
 
 
+def dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(x: float, world: int) -> float:
-    if world == 1:
+    if not dist_on():
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
@@ -224,7 +235,7 @@ def main():
         if gather is not None:
             line["gather"] = gather
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 
