@@ -20,6 +20,7 @@
 //       descriptor SoA; bytes outside the window are read from global memory.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <hipcub/device/device_scan.hpp>
 
 #include <cstdint>
 #include <cstring>
@@ -1978,6 +1979,163 @@ void prof_commit(int which, hipEvent_t start) {
     if (R.count < ProfRing::kCap) ++R.count;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Aeron fragment reassembly (LocalFragmentReassembler::onFragment, src/cluster_client.cpp:39-82)
+//   1. frag_classify: per fragment a scan element (delivery-point count, last BEGIN, last END,
+//      non-single bytes, singles); message sizes zeroed
+//   2. one device-wide inclusive scan of the elements (hipCUB / rocPRIM, tuple operator)
+//   3. frag_messages: every delivery point (a BEGIN|END single, or an END) sizes its message:
+//      the END's group is the non-single fragments since the last BEGIN or END before it; the
+//      open group at the end of the batch is the carry
+//   4. exclusive scan of the sizes → msg_off
+//   5. frag_copy: one wave per message, realigning dword copy (fragment by fragment only when a
+//      single sits inside a group)
+// ------------------------------------------------------------------------------------------
+struct FragScan {
+    uint64_t dp;   // delivery points (singles + ENDs) so far
+    int64_t lb;    // last BEGIN (non-single) index so far, -1 none
+    int64_t le;    // last END (non-single) index so far, -1 none
+    uint64_t ns;   // bytes of non-single fragments so far
+    uint64_t sg;   // singles so far
+};
+struct FragScanOp {
+    __host__ __device__ FragScan operator()(const FragScan& a, const FragScan& b) const {
+        return FragScan{a.dp + b.dp, a.lb > b.lb ? a.lb : b.lb, a.le > b.le ? a.le : b.le, a.ns + b.ns, a.sg + b.sg};
+    }
+};
+
+struct FragArgs {
+    const uint8_t* in;
+    const uint64_t* frag_off;
+    const uint8_t* flags;
+    uint64_t n;
+    uint8_t* out;
+    uint64_t* msg_off;
+    uint64_t* counts;
+    FragScan* el;      // [n] scan elements
+    FragScan* sc;      // [n] their inclusive scan
+    uint64_t* msize;   // [n + 1]
+    uint64_t* mfirst;  // [n + 1] first fragment of message j
+    uint64_t* mlast;   // [n + 1] last fragment (bit 63: a single sits inside the group)
+};
+
+__device__ __forceinline__ bool frag_single(uint8_t f) {
+    return (f & (SBE_FRAG_BEGIN | SBE_FRAG_END)) == (SBE_FRAG_BEGIN | SBE_FRAG_END);
+}
+
+__global__ __launch_bounds__(256) void frag_classify(FragArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= a.n) a.msize[i] = 0;
+    if (i >= a.n) return;
+    const uint8_t f = a.flags[i];
+    const bool single = frag_single(f);
+    const uint64_t len = a.frag_off[i + 1] - a.frag_off[i];
+    FragScan e;
+    e.dp = (single || (f & SBE_FRAG_END)) ? 1u : 0u;
+    e.lb = (!single && (f & SBE_FRAG_BEGIN)) ? (int64_t)i : -1;
+    e.le = (!single && (f & SBE_FRAG_END)) ? (int64_t)i : -1;
+    e.ns = single ? 0u : len;
+    e.sg = single ? 1u : 0u;
+    a.el[i] = e;
+}
+
+// group of non-single fragments ending at i (inclusive): from the later of the last BEGIN at or
+// before i and the fragment after the last END before i
+__device__ __forceinline__ void frag_group(const FragArgs& a, uint64_t i, int64_t le_before, uint64_t& s,
+                                          uint64_t& bytes, bool& gap) {
+    const FragScan& e = a.sc[i];
+    int64_t st = e.lb > le_before + 1 ? e.lb : le_before + 1;
+    if (st < 0) st = 0;
+    s = (uint64_t)st;
+    const uint64_t ns0 = s ? a.sc[s - 1].ns : 0u, sg0 = s ? a.sc[s - 1].sg : 0u;
+    bytes = e.ns - ns0;
+    gap = e.sg != sg0;
+}
+
+__global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t f = a.flags[i];
+    const FragScan e = a.sc[i];
+    const bool single = frag_single(f);
+    if ((single || (f & SBE_FRAG_END)) && e.dp >= 1 && e.dp <= a.n) {
+        const uint64_t j = e.dp - 1;
+        if (single) {
+            a.msize[j] = a.frag_off[i + 1] - a.frag_off[i];
+            a.mfirst[j] = i;
+            a.mlast[j] = i;
+        } else {
+            uint64_t s, bytes;
+            bool gap;
+            frag_group(a, i, i ? a.sc[i - 1].le : -1, s, bytes, gap);
+            a.msize[j] = bytes;
+            a.mfirst[j] = s;
+            a.mlast[j] = i | (gap ? (1ull << 63) : 0ull);
+        }
+    }
+    if (i == a.n - 1) {  // the open accumulator after the last fragment: the carry
+        const uint64_t m = e.dp <= a.n ? e.dp : a.n;
+        uint64_t s, bytes;
+        bool gap;
+        frag_group(a, i, e.le, s, bytes, gap);
+        const bool open = (int64_t)s <= (int64_t)i && bytes > 0;
+        a.msize[m] = open ? bytes : 0u;
+        a.mfirst[m] = s;
+        a.mlast[m] = i | (gap ? (1ull << 63) : 0ull);
+        a.counts[0] = m;
+        a.counts[1] = open ? bytes : 0u;
+    }
+}
+
+// copy src[0, len) to dst with dword stores where dst is aligned (lanes stride dwords); source
+// dwords are read aligned and joined with v_alignbyte (never past the source's last dword)
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
+    if (len == 0) return;
+    const uint64_t head = ((4u - ((uintptr_t)dst & 3u)) & 3u) < len ? ((4u - ((uintptr_t)dst & 3u)) & 3u) : len;
+    if ((uint64_t)lane < head) dst[lane] = src[lane];
+    const uint64_t nd = (len - head) >> 2;
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + head;
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+    for (uint64_t k = lane; k < nd; k += kWave) {
+        const uintptr_t p = s0 + 4 * k;
+        const uint32_t lo = gload32(p & ~(uintptr_t)3), hi = gload32((p + 3) & ~(uintptr_t)3);
+        d32[k] = (p & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(p & 3)) : lo;
+    }
+    const uint64_t tail0 = head + 4 * nd;
+    if ((uint64_t)lane < len - tail0) dst[tail0 + lane] = src[tail0 + lane];
+}
+
+__global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    const uint64_t m = a.counts[0];
+    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; j <= m; j += waves) {
+        const uint64_t len = a.msize[j];
+        if (len == 0) continue;
+        const uint64_t first = a.mfirst[j], last = a.mlast[j] & ~(1ull << 63);
+        uint8_t* dst = a.out + a.msg_off[j];
+        if (!(a.mlast[j] >> 63)) {
+            wave_copy(dst, a.in + a.frag_off[first], len, lane);
+        } else {  // a single inside the group: fragment by fragment, skipping singles
+            uint64_t at = 0;
+            for (uint64_t f = first; f <= last; ++f) {
+                if (frag_single(a.flags[f])) continue;
+                const uint64_t l = a.frag_off[f + 1] - a.frag_off[f];
+                wave_copy(dst + at, a.in + a.frag_off[f], l, lane);
+                at += l;
+            }
+        }
+    }
+}
+
+size_t frag_scan_temp(uint64_t n, hipStream_t s) {
+    size_t t1 = 0, t2 = 0;
+    (void)hipcub::DeviceScan::InclusiveScan(nullptr, t1, (FragScan*)nullptr, (FragScan*)nullptr, FragScanOp{}, n, s);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, n + 1, s);
+    return (t1 > t2 ? t1 : t2) + 256;
+}
+
 // One encode request, whatever the layout (the C entry points fill it).
 struct EncReq {
     const uint8_t* arena;
@@ -2144,6 +2302,53 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     else
         hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, e0, e1, 0, a);
     prof_commit(1, e0);
+    return record_hip(hipGetLastError());
+}
+
+size_t sbe_reassemble_workspace_size(uint64_t n) {
+    // scan elements, sizes, first / last fragment per message, scan temporary storage
+    return (size_t)(2 * n * sizeof(FragScan) + 3 * 8 * (n + 1) + 5 * 16) + frag_scan_temp(n ? n : 1, nullptr);
+}
+
+int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
+                             uint8_t* out, uint64_t* msg_off, uint64_t* counts, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!msg_off || !counts) return SBE_EINVAL;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(counts, 0, 16, s);
+        if (e == hipSuccess) e = hipMemsetAsync(msg_off, 0, 8, s);
+        return record_hip(e);
+    }
+    if (!in || !frag_off || !flags || !out || !workspace) return SBE_EINVAL;
+    if (n > (1ull << 40)) return SBE_EINVAL;
+    if (workspace_bytes < sbe_reassemble_workspace_size(n)) return SBE_ENOSPC;
+    auto al = [](uintptr_t x) { return (x + 15) & ~(uintptr_t)15; };
+    uintptr_t w = al(reinterpret_cast<uintptr_t>(workspace));
+    FragScan* el = reinterpret_cast<FragScan*>(w);
+    w = al(w + n * sizeof(FragScan));
+    FragScan* sc = reinterpret_cast<FragScan*>(w);
+    w = al(w + n * sizeof(FragScan));
+    uint64_t* msize = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    uint64_t* mfirst = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    uint64_t* mlast = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    void* tmp = reinterpret_cast<void*>(w);
+    size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
+    FragArgs a{in, frag_off, flags, n, out, msg_off, counts, el, sc, msize, mfirst, mlast};
+    const uint32_t blocks = (uint32_t)((n + 1 + 255) / 256);
+    hipLaunchKernelGGL(frag_classify, dim3(blocks), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, el, sc, FragScanOp{}, n, s);
+    if (e != hipSuccess) return record_hip(e);
+    hipLaunchKernelGGL(frag_messages, dim3(blocks), dim3(256), 0, s, a);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, msize, msg_off, n + 1, s);
+    if (e != hipSuccess) return record_hip(e);
+    const uint64_t cb = (n + 1 + 3) / 4;  // four waves per 256-thread block
+    hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < 4096 ? cb : 4096)), dim3(256), 0, s, a);
     return record_hip(hipGetLastError());
 }
 

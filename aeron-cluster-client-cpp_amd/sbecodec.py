@@ -11,6 +11,7 @@ Reference surface mirrored (paths relative to the reference tree):
   encode_lite_batch   ~ CommitManager::build_commit_offset_message (CommitOffsetLite)
                         src/commit_manager.cpp:107-132; OrderRequestLite / OrderNotificationLite
   decode_batch(LITE)  ~ the Lite templates' generated decode flyweights
+  reassemble          ~ LocalFragmentReassembler::onFragment  src/cluster_client.cpp:39-82
   decode_batch(PARSE) ~ MessageParser::parse_message        src/sbe_encoder.cpp:513-551
   decode_batch(EGRESS)~ decode_ack + MessageHandler::on_egress
                         src/ack_decoder.cpp:29-105, include/aeron_cluster/message_handler.hpp:35-68
@@ -36,6 +37,7 @@ SESSION_HDR_LEN = 32
 COMMIT_OFFSET_LITE, ORDER_REQUEST_LITE, ORDER_NOTIFICATION_LITE = 301, 201, 202
 LITE_FIELDS = {COMMIT_OFFSET_LITE: 2, ORDER_REQUEST_LITE: 3, ORDER_NOTIFICATION_LITE: 3}
 ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
+FRAG_BEGIN, FRAG_END = 0x80, 0x40
 
 ST_TM, ST_ACK, ST_SESSION_EVENT = 0, 1, 2
 ST_ERR_NULL_EMPTY, ST_ERR_HEADER, ST_ERR_UNKNOWN_TYPE = 16, 17, 18
@@ -102,6 +104,12 @@ def _load():
         ctypes.POINTER(_LiteBatch), ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.sbe_reassemble_workspace_size.restype = ctypes.c_size_t
+    lib.sbe_reassemble_workspace_size.argtypes = [ctypes.c_uint64]
+    lib.sbe_reassemble_fragments.restype = ctypes.c_int
+    lib.sbe_reassemble_fragments.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_size_t, ctypes.c_void_p]
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.POINTER(_Decoded), ctypes.c_void_p]
@@ -341,3 +349,33 @@ def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = No
     if n < out.status.numel():
         out = Decoded(*(getattr(out, k)[:n] for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
     return out
+
+
+@dataclass
+class Reassembled:
+    out: torch.Tensor      # uint8: messages back to back, then the carry
+    msg_off: torch.Tensor  # int64 [n+1]: message j = out[msg_off[j]:msg_off[j+1]] for j < m
+    counts: torch.Tensor   # int64 [2]: m, carry bytes (carry = out[msg_off[m]:msg_off[m]+carry])
+
+
+def reassemble(data, frag_off, flags, out=None, msg_off=None, workspace=None, stream=None) -> Reassembled:
+    """Aeron BEGIN/END fragment reassembly of data[frag_off[i]:frag_off[i+1]] with flags[i]."""
+    data = _dev(data, torch.uint8, "data")
+    frag_off = _dev(frag_off, torch.int64, "frag_off")
+    flags = _dev(flags, torch.uint8, "flags")
+    n = int(flags.numel())
+    if frag_off.numel() != n + 1:
+        raise SbeError("frag_off must have n + 1 entries")
+    dev = data.device
+    if out is None:
+        out = torch.empty(max(int(data.numel()), 16), dtype=torch.uint8, device=dev)
+    if msg_off is None:
+        msg_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)
+    need = int(lib().sbe_reassemble_workspace_size(n))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+    rc = lib().sbe_reassemble_fragments(_ptr(data), _ptr(frag_off), _ptr(flags), n, _ptr(out), _ptr(msg_off),
+                                        _ptr(counts), _ptr(workspace), workspace.numel(), _stream(stream))
+    _check(rc, "sbe_reassemble_fragments")
+    return Reassembled(out, msg_off, counts)

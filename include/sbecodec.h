@@ -30,6 +30,8 @@
  *                                  (wrapForDecode + fixed fields + getXAsString in order,
  *                                  include/model/CommitOffsetLite.h, OrderRequestLite.h,
  *                                  OrderNotificationLite.h).
+ * sbe_reassemble_fragments()      LocalFragmentReassembler::onFragment src/cluster_client.cpp:39-82
+ *                                  (BEGIN / END flag reassembly of Aeron fragments, before parse).
  * sbe_decode_batch(PARSE_MESSAGE) MessageParser::parse_message      src/sbe_encoder.cpp:513-551
  *                                  (+ parse_topic_message :724-831, decode_acknowledgment_with_sbe
  *                                  :833-954, decode_topic_message_with_sbe :957-1143,
@@ -239,6 +241,26 @@ typedef struct sbe_decoded {
  * the SBE header carries no total length.  Alignment: in 16 B, rec_off/hdr/ts 8 B, views 4 B. */
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream);
+
+/* ============================ Aeron fragment reassembly ============================ */
+/* Replaces LocalFragmentReassembler::onFragment (src/cluster_client.cpp:39-82) for a batch of
+ * fragments, in arrival order:
+ *   flags[i] & (BEGIN|END) == BEGIN|END   the fragment is a whole message;
+ *   otherwise   BEGIN clears the accumulator, the fragment is appended, END delivers the
+ *               accumulator as one message and clears it.
+ * in[frag_off[i] .. frag_off[i+1]) is fragment i (frag_off: n + 1 device u64).
+ * Outputs: the delivered messages back to back in delivery order, out[msg_off[j] .. msg_off[j+1])
+ * for j < m; then the open accumulator ("carry", bytes of a message whose END has not arrived)
+ * at out[msg_off[m] .. msg_off[m] + carry).  counts (device u64[2]) = {m, carry}.  To continue
+ * with the next batch, pass the carry bytes as its first fragment with flags 0 (a middle
+ * fragment appends exactly as the accumulator would).
+ * out must hold frag_off[n] - frag_off[0] bytes, msg_off n + 1 entries. */
+#define SBE_FRAG_BEGIN 0x80u
+#define SBE_FRAG_END 0x40u
+size_t sbe_reassemble_workspace_size(uint64_t n);
+int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
+                             uint8_t* out, uint64_t* msg_off, uint64_t* counts, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* ================================== profiling ================================== */
 /* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every

@@ -545,3 +545,42 @@ int orc_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Aeron fragment reassembly: LocalFragmentReassembler::onFragment, src/cluster_client.cpp:39-82,
+ * one call per fragment in order:
+ *   BEGIN|END (0xC0)     deliver the fragment itself (the accumulator is untouched, :52-56);
+ *   otherwise            BEGIN clears the accumulator (:59-62), the fragment is appended (:63),
+ *                        END delivers the accumulator and clears it (:66-73).
+ * Outputs as sbe_reassemble_fragments: messages back to back, msg_off[0..m], then the open
+ * accumulator ("carry") right after the last message; counts = {m, carry bytes}.
+ * ------------------------------------------------------------------------------------------ */
+int orc_reassemble(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
+                   uint8_t* out, uint64_t* msg_off, uint64_t counts[2], uint8_t* acc_buf) {
+    uint64_t m = 0, at = 0, acc = 0;
+    msg_off[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t f = flags[i];
+        const uint8_t* src = in + frag_off[i];
+        const uint64_t len = frag_off[i + 1] - frag_off[i];
+        if ((f & (SBE_FRAG_BEGIN | SBE_FRAG_END)) == (SBE_FRAG_BEGIN | SBE_FRAG_END)) {
+            memcpy(out + at, src, len);
+            at += len;
+            msg_off[++m] = at;
+            continue;
+        }
+        if (f & SBE_FRAG_BEGIN) acc = 0;
+        memcpy(acc_buf + acc, src, len);
+        acc += len;
+        if (f & SBE_FRAG_END) {
+            memcpy(out + at, acc_buf, acc);
+            at += acc;
+            msg_off[++m] = at;
+            acc = 0;
+        }
+    }
+    memcpy(out + at, acc_buf, acc);
+    counts[0] = m;
+    counts[1] = acc;
+    return 0;
+}

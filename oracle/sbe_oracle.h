@@ -60,6 +60,11 @@ int orc_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
                      uint8_t* status, uint8_t* flags, uint16_t* hdr, uint64_t* ts,
                      uint32_t* view_off, uint32_t* view_len, int nthreads);
 
+/* Fragment reassembly with the semantics/outputs of sbe_reassemble_fragments (host arrays; out
+ * and acc_buf hold frag_off[n] - frag_off[0] bytes, msg_off n + 1 entries). */
+int orc_reassemble(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
+                   uint8_t* out, uint64_t* msg_off, uint64_t counts[2], uint8_t* acc_buf);
+
 /* protocol.hpp:37-42 */
 uint64_t orc_to_nanos_auto(uint64_t ts);
 

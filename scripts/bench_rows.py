@@ -6,6 +6,8 @@ algorithmic bytes per launch (computed from the actual record sizes) and its fra
   config4_var_roundtrip  16 M variable-length TopicMessages, encode + parse decode (config 4)
   session_fixed256       1 M session-framed Order TopicMessages (32-B SessionMessageHeader + 248 B)
   lite301 / lite201      1 M CommitOffsetLite / OrderRequestLite records, encode + Lite decode
+  reassemble             1 M Aeron fragments (90 % whole messages, the rest BEGIN..END groups),
+                         BEGIN/END reassembly (all five launches, torch events around the call)
 Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...]  (GPU only)
 """
 import argparse
@@ -130,11 +132,33 @@ def row_lite(t_id, steps, warmup):
                                "sbe_decode_kernel<lite>": (dk, outb + 8 * n + DESC * n)})
 
 
+def row_reassemble(steps, warmup):
+    n = 1_000_000
+    data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512)
+    d, o, f = dev(data, torch.uint8), dev(off.view(np.int64), torch.int64), dev(flags, torch.uint8)
+    out = torch.empty(max(data.size, 16), dtype=torch.uint8, device="cuda")
+    mo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    ws = torch.empty(int(sbecodec.lib().sbe_reassemble_workspace_size(n)), dtype=torch.uint8, device="cuda")
+    fn = lambda: sbecodec.reassemble(d, o, f, out=out, msg_off=mo, workspace=ws)  # noqa: E731
+    for _ in range(warmup):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = 2 * data.size + (8 + 1 + 8) * n  # payload read + written, frag_off + flags read, msg_off written
+    line("reassemble", n, ms * 1e-3, {"sbe_reassemble_fragments (5 launches)": (ms, nbytes)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201")
+    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble")
     args = ap.parse_args()
     sbecodec.require_device()
     for r in args.rows.split(","):
@@ -144,6 +168,8 @@ def main():
             row_var(max(args.steps // 2, 5), args.warmup)
         elif r == "session":
             row_session(args.steps, args.warmup)
+        elif r == "reassemble":
+            row_reassemble(args.steps, args.warmup)
         elif r.startswith("lite"):
             row_lite(int(r[4:]), args.steps, args.warmup)
         torch.cuda.empty_cache()

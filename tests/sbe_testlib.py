@@ -61,6 +61,7 @@ def oracle():
         L.orc_encode_batch.argtypes = [vp, vp, vp, vp, u64, u64, u32, vp, vp, vp, i]
         L.orc_encode_session_batch.argtypes = [vp, vp, vp, vp, u64, u64, u32, i64, i64, vp, vp, vp, i]
         L.orc_encode_lite_batch.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp, vp, vp, i]
+        L.orc_reassemble.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
         L.orc_decode_batch.argtypes = [vp, vp, u64, u32, vp, vp, vp, vp, vp, vp, i]
         L.orc_to_nanos_auto.restype = u64
         L.orc_to_nanos_auto.argtypes = [u64]
@@ -128,6 +129,56 @@ def oracle_encode_lite(template_id, arena, str_len, topic_id, sequence, str_off=
                                         _p(out), _p(out_off), _p(status), nthreads)
     assert rc == 0
     return out[: int(out_off[n])], out_off, status[:n]
+
+
+def oracle_reassemble(data, frag_off, flags):
+    """LocalFragmentReassembler restated → (messages list of bytes, carry bytes)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    frag_off = np.ascontiguousarray(frag_off, dtype=np.uint64)
+    flags = np.ascontiguousarray(flags, dtype=np.uint8)
+    n = flags.size
+    tot = max(int(frag_off[-1]) if n else 0, 1)
+    out = np.zeros(tot, np.uint8)
+    acc = np.zeros(tot, np.uint8)
+    msg_off = np.zeros(n + 1, np.uint64)
+    counts = np.zeros(2, np.uint64)
+    oracle().orc_reassemble(_p(data if data.size else np.zeros(1, np.uint8)), _p(frag_off),
+                            _p(flags if n else np.zeros(1, np.uint8)), n, _p(out), _p(msg_off), _p(counts), _p(acc))
+    m = int(counts[0])
+    msgs = [bytes(out[int(msg_off[j]):int(msg_off[j + 1])]) for j in range(m)]
+    carry = bytes(out[int(msg_off[m]):int(msg_off[m]) + int(counts[1])])
+    return msgs, carry
+
+
+def fragment_stream(n, seed, p_single=0.6, maxlen=300):
+    """Random Aeron fragment stream: lengths 0..maxlen, flags drawn from whole messages
+    (BEGIN|END), BEGIN … END sequences, and stray middle / END / BEGIN fragments."""
+    rng = np.random.default_rng(seed)
+    flags = np.zeros(n, np.uint8)
+    i = 0
+    while i < n:
+        r = rng.random()
+        if r < p_single:
+            flags[i] = 0xC0
+            i += 1
+        elif r < 0.9:
+            k = int(rng.integers(2, 6))
+            for t in range(k):
+                if i >= n:
+                    break
+                flags[i] = 0x80 if t == 0 else (0x40 if t == k - 1 else 0x00)
+                if 0 < t < k - 1 and rng.random() < 0.1:
+                    flags[i] = 0xC0  # a whole message inside a group
+                i += 1
+        else:
+            flags[i] = int(rng.choice([0x00, 0x40, 0x80]))
+            i += 1
+    lens = rng.integers(0, maxlen + 1, n)
+    lens[rng.random(n) < 0.05] = 0
+    frag_off = np.zeros(n + 1, np.uint64)
+    frag_off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, int(frag_off[-1]), dtype=np.uint8)
+    return data, frag_off, flags
 
 
 def oracle_decode(data, rec_off, mode=DEC_PARSE, nthreads=1):
