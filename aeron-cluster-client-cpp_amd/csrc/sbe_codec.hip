@@ -1992,16 +1992,16 @@ void prof_commit(int which, hipEvent_t start) {
 //   5. frag_copy: one wave per message, realigning dword copy (fragment by fragment only when a
 //      single sits inside a group)
 // ------------------------------------------------------------------------------------------
-struct FragScan {
-    uint64_t dp;   // delivery points (singles + ENDs) so far
-    int64_t lb;    // last BEGIN (non-single) index so far, -1 none
-    int64_t le;    // last END (non-single) index so far, -1 none
+struct FragScan {  // 24 bytes (batches of up to 2^31 fragments)
+    uint32_t dp;   // delivery points (singles + ENDs) so far
+    uint32_t sg;   // singles so far
+    int32_t lb;    // last BEGIN (non-single) index so far, -1 none
+    int32_t le;    // last END (non-single) index so far, -1 none
     uint64_t ns;   // bytes of non-single fragments so far
-    uint64_t sg;   // singles so far
 };
 struct FragScanOp {
     __host__ __device__ FragScan operator()(const FragScan& a, const FragScan& b) const {
-        return FragScan{a.dp + b.dp, a.lb > b.lb ? a.lb : b.lb, a.le > b.le ? a.le : b.le, a.ns + b.ns, a.sg + b.sg};
+        return FragScan{a.dp + b.dp, a.sg + b.sg, a.lb > b.lb ? a.lb : b.lb, a.le > b.le ? a.le : b.le, a.ns + b.ns};
     }
 };
 
@@ -2033,8 +2033,8 @@ __global__ __launch_bounds__(256) void frag_classify(FragArgs a) {
     const uint64_t len = a.frag_off[i + 1] - a.frag_off[i];
     FragScan e;
     e.dp = (single || (f & SBE_FRAG_END)) ? 1u : 0u;
-    e.lb = (!single && (f & SBE_FRAG_BEGIN)) ? (int64_t)i : -1;
-    e.le = (!single && (f & SBE_FRAG_END)) ? (int64_t)i : -1;
+    e.lb = (!single && (f & SBE_FRAG_BEGIN)) ? (int32_t)i : -1;
+    e.le = (!single && (f & SBE_FRAG_END)) ? (int32_t)i : -1;
     e.ns = single ? 0u : len;
     e.sg = single ? 1u : 0u;
     a.el[i] = e;
@@ -2045,7 +2045,7 @@ __global__ __launch_bounds__(256) void frag_classify(FragArgs a) {
 __device__ __forceinline__ void frag_group(const FragArgs& a, uint64_t i, int64_t le_before, uint64_t& s,
                                           uint64_t& bytes, bool& gap) {
     const FragScan& e = a.sc[i];
-    int64_t st = e.lb > le_before + 1 ? e.lb : le_before + 1;
+    int64_t st = (int64_t)e.lb > le_before + 1 ? (int64_t)e.lb : le_before + 1;
     if (st < 0) st = 0;
     s = (uint64_t)st;
     const uint64_t ns0 = s ? a.sc[s - 1].ns : 0u, sg0 = s ? a.sc[s - 1].sg : 0u;
@@ -2106,24 +2106,93 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
     if ((uint64_t)lane < len - tail0) dst[tail0 + lane] = src[tail0 + lane];
 }
 
+// the 16 bytes at src + 16c + sh from the aligned blocks b0 (at 16c) and b1 (the next one)
+__device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
+    const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const uint32_t ds = sh >> 2, bs = sh & 3u;
+    uint32_t v[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t)  // v[t] = w[t + ds] (selects keep w in registers)
+        v[t] = ds == 0 ? w[t] : ds == 1 ? w[t + 1] : ds == 2 ? w[t + 2] : w[t + 3 < 8 ? t + 3 : 7];
+    return make_uint4(__builtin_amdgcn_alignbyte(v[1], v[0], bs), __builtin_amdgcn_alignbyte(v[2], v[1], bs),
+                      __builtin_amdgcn_alignbyte(v[3], v[2], bs), __builtin_amdgcn_alignbyte(v[4], v[3], bs));
+}
+
+// wave copy of src[0, len) to dst with 16-byte stores once dst is aligned; each output chunk
+// joins the two aligned 16-byte source blocks it spans (never past the source's last block);
+// two chunks per lane in flight per step
+__device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
+    if (len == 0) return;
+    uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+    head = head < len ? head : len;
+    if ((uint64_t)lane < head) dst[lane] = src[lane];
+    const uint64_t nc = (len - head) >> 4;
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(src) + head;
+    const uint32_t sh = (uint32_t)(p0 & 15u);
+    const uintptr_t q0 = p0 & ~(uintptr_t)15;
+    uint4* d16 = reinterpret_cast<uint4*>(dst + head);
+    for (uint64_t c = lane; c < nc; c += 2 * kWave) {
+        const uint64_t c2 = c + kWave;
+        const uintptr_t qa = q0 + 16 * c, qb = q0 + 16 * (c2 < nc ? c2 : c);
+        const uint4 a0 = gload128(qa), a1 = sh ? gload128(qa + 16) : a0;
+        const uint4 b0 = gload128(qb), b1 = sh ? gload128(qb + 16) : b0;
+        d16[c] = sh ? join16(a0, a1, sh) : a0;
+        if (c2 < nc) d16[c2] = sh ? join16(b0, b1, sh) : b0;
+    }
+    const uint64_t t0 = head + 16 * nc;
+    if ((uint64_t)lane < len - t0) dst[t0 + lane] = src[t0 + lane];
+}
+
+// One wave per kFragGroup consecutive messages: lane l loads message (base + l)'s size, source
+// and destination (coalesced; small groups keep each wave's copy short, many waves in flight).  Consecutive messages whose sources are back to back (singles and
+// complete groups: the common case) form runs, each copied as one block; a message with a single
+// inside its group is copied fragment by fragment.
+constexpr int kFragGroup = 64;
 __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
     const uint64_t m = a.counts[0];
-    for (uint64_t j = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave; j <= m; j += waves) {
-        const uint64_t len = a.msize[j];
-        if (len == 0) continue;
-        const uint64_t first = a.mfirst[j], last = a.mlast[j] & ~(1ull << 63);
-        uint8_t* dst = a.out + a.msg_off[j];
-        if (!(a.mlast[j] >> 63)) {
-            wave_copy(dst, a.in + a.frag_off[first], len, lane);
-        } else {  // a single inside the group: fragment by fragment, skipping singles
-            uint64_t at = 0;
-            for (uint64_t f = first; f <= last; ++f) {
-                if (frag_single(a.flags[f])) continue;
-                const uint64_t l = a.frag_off[f + 1] - a.frag_off[f];
-                wave_copy(dst + at, a.in + a.frag_off[f], l, lane);
-                at += l;
+    for (uint64_t base = ((uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * kFragGroup; base <= m;
+         base += waves * kFragGroup) {
+        const uint64_t j = base + (uint64_t)lane;
+        uint64_t len = 0, src = 0, dst = 0, mlast = 0, first = 0;
+        if (lane < kFragGroup && j <= m) {
+            len = a.msize[j];
+            first = a.mfirst[j];
+            mlast = a.mlast[j];
+            dst = a.msg_off[j];
+            src = a.frag_off[first];
+        }
+        const bool valid = lane < kFragGroup && j <= m;
+        const bool gap = valid && (mlast >> 63);
+        // run membership: this message's source follows the previous one's (and neither is gapped)
+        const uint64_t pend = __shfl_up(src + len, 1, kWave);
+        const bool pgap = __shfl_up(gap ? 1 : 0, 1, kWave) != 0;
+        const bool cont = lane > 0 && valid && !gap && !pgap && src == pend;
+        const uint64_t starts = __ballot(valid && !gap && !cont);
+        const uint64_t vmask = __ballot(valid);
+        for (uint64_t mk = starts; mk; mk &= mk - 1) {
+            const int k = __builtin_ctzll(mk);
+            // the run ends before the next start, gapped message or invalid lane
+            const uint64_t stop = (starts | __ballot(gap) | ~vmask) & ~((2ull << k) - 1);
+            const int e = stop ? __builtin_ctzll(stop) : kWave;  // first lane after the run
+            const uint64_t D = uniform64(__shfl(dst, k, kWave));
+            const uint64_t De = uniform64(__shfl(dst + len, e - 1, kWave));
+            wave_copy16(a.out + D, a.in + uniform64(__shfl(src, k, kWave)), De - D, lane);
+        }
+        for (uint64_t mk = __ballot(gap && len > 0); mk; mk &= mk - 1) {
+            const int k = __builtin_ctzll(mk);
+            const uint64_t D = uniform64(__shfl(dst, (int)k, kWave));
+            const uint64_t ML = uniform64(__shfl(mlast, (int)k, kWave));
+            {  // a single inside the group: fragment by fragment, skipping singles
+                const uint64_t F = uniform64(__shfl(first, (int)k, kWave)), last = ML & ~(1ull << 63);
+                uint64_t at = 0;
+                for (uint64_t f = F; f <= last; ++f) {
+                    if (frag_single(a.flags[f])) continue;
+                    const uint64_t l = a.frag_off[f + 1] - a.frag_off[f];
+                    wave_copy16(a.out + D + at, a.in + a.frag_off[f], l, lane);
+                    at += l;
+                }
             }
         }
     }
@@ -2321,7 +2390,7 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
         return record_hip(e);
     }
     if (!in || !frag_off || !flags || !out || !workspace) return SBE_EINVAL;
-    if (n > (1ull << 40)) return SBE_EINVAL;
+    if (n >= (1ull << 31)) return SBE_EINVAL;
     if (workspace_bytes < sbe_reassemble_workspace_size(n)) return SBE_ENOSPC;
     auto al = [](uintptr_t x) { return (x + 15) & ~(uintptr_t)15; };
     uintptr_t w = al(reinterpret_cast<uintptr_t>(workspace));
@@ -2347,7 +2416,7 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     e = hipGetLastError();
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, msize, msg_off, n + 1, s);
     if (e != hipSuccess) return record_hip(e);
-    const uint64_t cb = (n + 1 + 3) / 4;  // four waves per 256-thread block
+    const uint64_t cb = (n + 1 + 4 * kFragGroup - 1) / (4 * kFragGroup);  // four waves per block
     hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < 4096 ? cb : 4096)), dim3(256), 0, s, a);
     return record_hip(hipGetLastError());
 }
