@@ -460,6 +460,69 @@ std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len)
     return r;
 }
 
+EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const std::uint64_t* frag_off,
+                                               const std::uint8_t* flags, std::size_t n) {
+    Ctx& c = ctx();
+    EncodedBatch b;
+    // the accumulator so far goes first as a middle fragment (flags 0): it is appended to exactly
+    // as the reference's acc_ would be, or cleared by a BEGIN
+    const size_t pre = acc_.empty() ? 0 : 1, nf = n + pre;
+    if (nf == 0) {
+        b.offsets.assign(1, 0);
+        return b;
+    }
+    const uint64_t base = n ? frag_off[0] : 0, body = n ? frag_off[n] - base : 0, total = acc_.size() + body;
+    c.h_in.need(total + 16);
+    uint8_t* hi = static_cast<uint8_t*>(c.h_in.p);
+    std::memcpy(hi, acc_.data(), acc_.size());
+    if (body) std::memcpy(hi + acc_.size(), data + base, body);
+    c.h_roff.need((nf + 1) * 8 + nf);
+    uint64_t* ho = static_cast<uint64_t*>(c.h_roff.p);
+    uint8_t* hf = reinterpret_cast<uint8_t*>(ho + nf + 1);
+    ho[0] = 0;
+    if (pre) {
+        ho[1] = acc_.size();
+        hf[0] = 0;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        ho[pre + i + 1] = acc_.size() + (frag_off[i + 1] - base);
+        hf[pre + i] = flags[i];
+    }
+    c.d_in.need(total + 16);
+    c.d_roff.need((nf + 1) * 8 + nf);
+    c.d_out.need(total + 16);
+    c.d_off.need((nf + 1) * 8 + 16);
+    const size_t wsb = sbe_reassemble_workspace_size(nf);
+    c.d_ws.need(wsb);
+    hip_check(hipMemcpyAsync(c.d_in.p, hi, total, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_roff.p, ho, (nf + 1) * 8 + nf, hipMemcpyHostToDevice, c.stream), "H2D");
+    uint64_t* d_off = static_cast<uint64_t*>(c.d_off.p);
+    uint64_t* d_counts = d_off + nf + 1;
+    if (sbe_reassemble_fragments(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p),
+                                 reinterpret_cast<uint8_t*>(static_cast<uint64_t*>(c.d_roff.p) + nf + 1), nf,
+                                 static_cast<uint8_t*>(c.d_out.p), d_off, d_counts, c.d_ws.p, c.d_ws.cap,
+                                 c.stream) != SBE_OK)
+        fail("sbe_reassemble_fragments");
+    uint64_t counts[2];
+    hip_check(hipMemcpyAsync(counts, d_counts, 16, hipMemcpyDeviceToHost, c.stream), "D2H");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    const uint64_t m = counts[0];
+    b.offsets.resize(m + 1);
+    b.status.assign(m, 0);
+    hip_check(hipMemcpyAsync(b.offsets.data(), d_off, (m + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
+    hip_check(hipStreamSynchronize(c.stream), "sync");
+    const uint64_t out_bytes = b.offsets[m] + counts[1];
+    std::vector<uint8_t> all(out_bytes);
+    if (out_bytes) {
+        hip_check(hipMemcpyAsync(all.data(), c.d_out.p, out_bytes, hipMemcpyDeviceToHost, c.stream), "D2H");
+        hip_check(hipStreamSynchronize(c.stream), "sync");
+    }
+    acc_.assign(all.begin() + b.offsets[m], all.end());
+    all.resize(b.offsets[m]);
+    b.bytes = std::move(all);
+    return b;
+}
+
 MessageHandler::MessageHandler() = default;
 MessageHandler::~MessageHandler() = default;
 

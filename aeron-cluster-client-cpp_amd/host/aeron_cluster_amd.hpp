@@ -14,6 +14,7 @@
 //   CommitManager                      build_commit_offset_message (CommitOffsetLite),
 //                                      src/commit_manager.cpp:16-22, :107-132; CommitOffset
 //                                      include/aeron_cluster/commit_manager.hpp:17-24
+//   LocalFragmentReassembler           src/cluster_client.cpp:39-82 (FragmentReassembler below)
 //   ClusterClient::offer_ingress       include/aeron_cluster/cluster_client.hpp:409 — the sink the
 //                                      encoded records are handed to (OfferFn below)
 // plus batched overloads, which are the point of the GPU path: one launch per batch.
@@ -201,6 +202,20 @@ struct LiteRecord {
 // Decoded with the generated flyweights' semantics; nullopt when the record is not a Lite
 // template or a bounds check throws E100.
 std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len);
+
+// LocalFragmentReassembler (src/cluster_client.cpp:39-82) for batches of Aeron fragments: fragment
+// i is data[frag_off[i], frag_off[i+1]) with header flags[i] (BEGIN 0x80, END 0x40).  Returns the
+// delivered messages in order; a message whose END has not arrived yet is kept for the next call,
+// exactly as the reference's accumulator.
+class FragmentReassembler {
+public:
+    EncodedBatch on_fragments(const std::uint8_t* data, const std::uint64_t* frag_off, const std::uint8_t* flags,
+                              std::size_t n);
+    std::size_t pending_bytes() const { return acc_.size(); }
+
+private:
+    std::vector<std::uint8_t> acc_;
+};
 
 // The raw ingress sink (ClusterClient::offer_ingress signature).  Feeds every encoded record of a
 // batch to it in order; returns the number accepted before the first refusal.

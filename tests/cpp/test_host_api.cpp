@@ -244,6 +244,27 @@ int main() {
             CHECK(std::string(ex.what()) == "messageIdLength too long for length type [E109]");
         }
     }
+    // ---- fragment reassembly (src/cluster_client.cpp:39-82), the accumulator across calls ----
+    {
+        FragmentReassembler fr;
+        const std::vector<std::string> frags = {"AB", "cd", "ef", "X", "gh", "ij", "k"};
+        const std::vector<uint8_t> fl = {0xC0, 0x80, 0x00, 0xC0, 0x40, 0x80, 0x00};
+        std::string joined;
+        std::vector<uint64_t> off{0};
+        for (auto& f : frags) {
+            joined += f;
+            off.push_back(joined.size());
+        }
+        auto r1 = fr.on_fragments(reinterpret_cast<const uint8_t*>(joined.data()), off.data(), fl.data(), frags.size());
+        CHECK(r1.offsets.size() == 4);
+        CHECK(std::string(r1.record(0)) == "AB" && std::string(r1.record(1)) == "X" && std::string(r1.record(2)) == "cdefgh");
+        CHECK(fr.pending_bytes() == 3);  // "ijk" waits for its END
+        const std::string rest = "lm";
+        const uint64_t off2[2] = {0, 2};
+        const uint8_t fl2[1] = {0x40};
+        auto r2 = fr.on_fragments(reinterpret_cast<const uint8_t*>(rest.data()), off2, fl2, 1);
+        CHECK(r2.offsets.size() == 2 && std::string(r2.record(0)) == "ijklm" && fr.pending_bytes() == 0);
+    }
     std::printf("host api test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }
