@@ -132,3 +132,19 @@ def test_gpu_reassembled_records_decode(codec):
     exp = T.oracle_decode(enc, eoff, T.DEC_PARSE)
     for k in exp:
         assert np.array_equal(got[k], exp[k]), k
+
+
+@pytest.mark.gpu
+def test_gpu_empty_and_zero_length(codec):
+    import torch
+    # no fragments at all
+    r = codec.reassemble(torch.zeros(16, dtype=torch.uint8, device="cuda"),
+                         torch.zeros(1, dtype=torch.int64, device="cuda"),
+                         torch.zeros(0, dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    assert r.counts.tolist() == [0, 0] and int(r.msg_off[0].item()) == 0
+    # only zero-length fragments
+    flags = np.array([0xC0, 0x80, 0x40, 0x00, 0xC0], np.uint8)
+    off = np.zeros(6, np.uint64)
+    data = np.zeros(1, np.uint8)
+    assert gpu_reassemble(codec, data, off, flags) == T.oracle_reassemble(data, off, flags)
