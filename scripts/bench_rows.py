@@ -49,8 +49,32 @@ def timed(fn, steps, warmup):
     return el / steps, (float(np.mean(pack)) if pack else None), (float(np.mean(deck)) if deck else None)
 
 
+CPU_THREADS = 16
+CPU_SECONDS = 3.0
+
+
+def cpu_rate(fn, n_sample, budget=CPU_SECONDS):
+    """records/s of fn() (the oracle restatement of the row on an n_sample-record slice of the same
+    workload) repeated for about `budget` seconds on the host cores."""
+    fn()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        done += n_sample
+        el = time.perf_counter() - t0
+        if el >= budget:
+            return done / el
+
+
+_cpu = None
+
+
 def line(row, n, step_s, kernels):
+    global _cpu
     out = {"row": row, "records": n, "records_per_s": n / step_s, "ms_per_step": step_s * 1e3, "kernels": {}}
+    if _cpu is not None:
+        out["cpu_baseline"] = _cpu
+        _cpu = None
     for name, (ms, nbytes) in kernels.items():
         if ms is None:
             continue
@@ -59,12 +83,21 @@ def line(row, n, step_s, kernels):
     print(json.dumps(out), flush=True)
 
 
+def set_cpu(value, sample, cores=CPU_THREADS):
+    global _cpu
+    _cpu = {"value": value, "unit": "records/s", "cores": cores, "kind": "port", "sample": sample}
+
+
 def row_mixed(steps, warmup):
     n = 1_000_000
     data, off = T.mixed_records(n)
     d, o = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
     out = sbecodec.alloc_decoded(n, "cuda")
     s, _, dk = timed(lambda: sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out), steps, warmup)
+    k = 200_000
+    dk_, ok_ = data[: int(off[k])], off[: k + 1]
+    set_cpu(cpu_rate(lambda: T.oracle_decode(dk_, ok_, T.DEC_PARSE, nthreads=CPU_THREADS), k),
+            f"{k} records of the same mix, oracle parse_message, OpenMP {CPU_THREADS} threads")
     line("config3_mixed_decode", n, s, {"sbe_decode_kernel<parse_message>": (dk, int(off[-1]) + 8 * n + DESC * n)})
 
 
@@ -85,6 +118,14 @@ def row_var(steps, warmup):
 
     s, pk, dk = timed(step, steps, warmup)
     outb = int(arena.size) + 34 * n
+    k = 200_000
+    ak, Lk, tk = T.var_orders(k)
+
+    def cpu_rt():
+        o, oo_, _ = T.oracle_encode(ak, Lk, tk, nthreads=CPU_THREADS)
+        T.oracle_decode(o, oo_, T.DEC_PARSE, nthreads=CPU_THREADS)
+
+    set_cpu(cpu_rate(cpu_rt, k), f"{k} variable-length records, oracle encode + parse_message, OpenMP {CPU_THREADS} threads")
     line("config4_var_roundtrip", n, s, {"sbe_enc_pack<packed,wire>": (pk, arena.size + 28 * n + outb + 9 * n),
                                          "sbe_decode_kernel<parse_message>": (dk, outb + 8 * n + DESC * n)})
 
@@ -105,6 +146,14 @@ def row_session(steps, warmup):
 
     s, pk, dk = timed(step, steps, warmup)
     rec = 32 + 248
+    k = 200_000
+    ak, Lk, tk = arena[: 222 * k], L[:k], ts[:k]
+
+    def cpu_rt():
+        o, oo_, _ = T.oracle_encode_session(ak, Lk, tk, 7, 8, flags=T.ENC_REF_TRUNCATE8, nthreads=CPU_THREADS)
+        T.oracle_decode(o, oo_, T.DEC_PARSE, nthreads=CPU_THREADS)
+
+    set_cpu(cpu_rate(cpu_rt, k), f"{k} records, oracle session encode + parse_message, OpenMP {CPU_THREADS} threads")
     line("session_fixed256", n, s, {"sbe_enc_pack<session,packed,ref>": (pk, n * (222 + 28 + rec + 9)),
                                     "sbe_decode_kernel<parse_message>": (dk, n * (rec + 8 + DESC))})
 
@@ -128,6 +177,14 @@ def row_lite(t_id, steps, warmup):
 
     s, pk, dk = timed(step, steps, warmup)
     outb = arena.size + (20 + 2 * nf) * n
+    k = 200_000
+    ak, Lk, tk, sk = T.lite_records(k, t_id)
+
+    def cpu_rt():
+        o, oo_, _ = T.oracle_encode_lite(t_id, ak, Lk, tk, sk, nthreads=CPU_THREADS)
+        T.oracle_decode(o, oo_, T.DEC_LITE, nthreads=CPU_THREADS)
+
+    set_cpu(cpu_rate(cpu_rt, k), f"{k} records, oracle Lite encode + decode, OpenMP {CPU_THREADS} threads")
     line(f"lite{t_id}", n, s, {f"sbe_enc_pack<lite{nf},packed>": (pk, arena.size + (4 * nf + 12) * n + outb + 9 * n),
                                "sbe_decode_kernel<lite>": (dk, outb + 8 * n + DESC * n)})
 
@@ -151,6 +208,14 @@ def row_reassemble(steps, warmup):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
     nbytes = 2 * data.size + (8 + 1 + 8) * n  # payload read + written, frag_off + flags read, msg_off written
+    k = 200_000
+    dk_, ok_, fk_ = data[: int(off[k])], np.ascontiguousarray(off[: k + 1]), np.ascontiguousarray(flags[:k])
+    ob_, ab_ = np.zeros(int(off[k]) + 1, np.uint8), np.zeros(int(off[k]) + 1, np.uint8)
+    mo_, cn_ = np.zeros(k + 1, np.uint64), np.zeros(2, np.uint64)
+    P = T._p
+    set_cpu(cpu_rate(lambda: T.oracle().orc_reassemble(P(dk_), P(ok_), P(fk_), k, P(ob_), P(mo_), P(cn_), P(ab_)), k),
+            f"{k} fragments of the same stream, oracle LocalFragmentReassembler restatement, 1 thread (sequential by definition)",
+            cores=1)
     line("reassemble", n, ms * 1e-3, {"sbe_reassemble_fragments (5 launches)": (ms, nbytes)})
 
 
