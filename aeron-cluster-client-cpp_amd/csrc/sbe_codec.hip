@@ -1491,6 +1491,29 @@ __device__ void dec_tm_parse(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
     }
 }
 
+// bit k set iff record byte p + k is printable ([32, 126]), for k < nbytes (<= 64): 17 aligned
+// dword reads (clamped to the record's last dword), four bytes classified per dword (SWAR), the
+// four flags gathered with one multiply
+template <typename R_t>
+__device__ __forceinline__ uint64_t printable_mask64(const R_t& R, uint32_t p, uint32_t nbytes) {
+    const uint32_t sh = R.abs_align(p);
+    const uint32_t q0 = p - sh;  // record offset of the aligned dword holding byte p
+    const uint32_t kmax = (sh + nbytes - 1) >> 2;
+    uint64_t m = 0;
+    uint32_t extra = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 17; ++k) {
+        const uint32_t w = R.adw(q0 + 4 * (k < kmax ? k : kmax));
+        const uint32_t lo7 = w & 0x7f7f7f7fu;
+        const uint32_t pr = (lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u;
+        const uint32_t c = (((pr >> 7) * 0x00204081u) >> 21) & 0xfu;
+        if (k < 16) m |= (uint64_t)c << (4 * k);
+        else extra = c;
+    }
+    if (sh) m = (m >> sh) | ((uint64_t)extra << (64 - sh));
+    return nbytes >= 64 ? m : m & ((1ull << nbytes) - 1);
+}
+
 // decode_acknowledgment_with_sbe (src/sbe_encoder.cpp:833-954)
 template <typename R_t>
 __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
@@ -1500,36 +1523,28 @@ __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& 
     d.status = SBE_ST_ACK;
     d.ts = R.u64(b + 8);
     if (b) d.flags |= SBE_FL_WRAPPED;
+    // maximal runs of printable bytes over [16, len), 64 bytes per block as a bitmask; a run may
+    // continue into the next block
     uint32_t nruns = 0;
     uint64_t run_start = 0, run_len = 0;
-    for (uint64_t i = 16; i < len && nruns < 3; i += 4) {
-        const uint32_t nb = (len - i) < 4 ? (uint32_t)(len - i) : 4u;
-        const uint32_t w = R.bytes(b + i, nb);
-        // printable bytes [32, 126], four at a time: bit 8k+7 set for a printable byte k
-        const uint32_t lo7 = w & 0x7f7f7f7fu;
-        const uint32_t pr = ((lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u) &
-                            (nb == 4 ? 0xffffffffu : (1u << (8 * nb)) - 1u);
-        const uint32_t full = nb == 4 ? 0x80808080u : 0x80808080u & ((1u << (8 * nb)) - 1u);
-        if (pr == full) {  // every byte printable: the run goes on
-            if (run_len == 0) run_start = i;
-            run_len += nb;
-            continue;
-        }
-        if (pr == 0) {  // none printable: the run (if any) ends here
-            if (run_len >= 3 && nruns < 3) {
-                d.set_view(nruns, (uint32_t)(b + run_start), (uint32_t)run_len);
-                ++nruns;
+    for (uint32_t s0 = 16; s0 < len && nruns < 3; s0 += 64) {
+        const uint32_t nb = len - s0 < 64u ? len - s0 : 64u;
+        const uint64_t m = printable_mask64(R, b + s0, nb);
+        uint32_t pos = 0;
+        while (pos < nb && nruns < 3) {
+            if (run_len == 0) {
+                const uint64_t rest = m >> pos;
+                if (rest == 0) break;  // nothing printable left in this block
+                pos += (uint32_t)__builtin_ctzll(rest);
+                run_start = s0 + pos;
             }
-            run_len = 0;
-            continue;
-        }
-        for (uint32_t k = 0; k < nb; ++k) {
-            const uint32_t c = (w >> (8 * k)) & 0xffu;
-            if (c >= 32 && c <= 126) {
-                if (run_len == 0) run_start = i + k;
-                ++run_len;
-            } else {
-                if (run_len >= 3 && nruns < 3) {
+            const uint64_t zeros = ~(m >> pos);  // bits >= nb of m are clear: a run stops at nb
+            const uint32_t o = zeros ? (uint32_t)__builtin_ctzll(zeros) : 64u - pos;
+            const uint32_t take = o < nb - pos ? o : nb - pos;
+            run_len += take;
+            pos += take;
+            if (pos < nb) {  // ended at a non-printable byte inside the block
+                if (run_len >= 3) {
                     d.set_view(nruns, (uint32_t)(b + run_start), (uint32_t)run_len);
                     ++nruns;
                 }
