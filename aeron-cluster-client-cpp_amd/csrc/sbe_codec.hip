@@ -865,7 +865,7 @@ __device__ __forceinline__ void put_clip(lds_u8* wout, int32_t d, uint32_t v, in
 template <class LY>
 __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t* sbase, const TileSt& S,
                                              int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int ra, int rb,
-                                             int lane) {
+                                             int lg, int lane) {
     const int q = lane % kLpr, r = lane / kLpr;
     bk[lane] = ra;
     bool outside = false;
@@ -904,11 +904,11 @@ __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t*
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0] = a;
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = b;
         sbase[r] = s0;
-        // buckets bb with bb*kLaneBytes inside [rw, rend) ∩ [0, wlen)
+        // buckets bb (lane bb's range, 2^lg bytes) starting inside [rw, rend) ∩ [0, wlen)
         const int32_t s1 = rw > 0 ? rw : 0;
         const int32_t e1 = rend < wlen ? rend : wlen;
         if (live && s1 < e1) {
-            for (int32_t bb = (s1 + kLaneBytes - 1) / kLaneBytes; bb * kLaneBytes < e1; ++bb) bk[bb] = r;
+            for (int32_t bb = (s1 + (1 << lg) - 1) >> lg; (bb << lg) < e1; ++bb) bk[bb] = r;
         }
     }
     return __ballot(outside) != 0;
@@ -922,16 +922,20 @@ __device__ __forceinline__ int32_t zone_of(const RecEnt& E, int32_t X) {
 // data, redone by chunk_pass_global).  Three phases so the LDS latency is paid once, not per
 // chunk: source offsets (walking the record table, next entry prefetched), all source reads,
 // then v_alignbyte + one ds_write_b128 per chunk.
+// Lane l owns the kk chunks [l kk, (l+1) kk) of the window: kk = 8 for a full window, fewer for
+// a window that carries less (kk a power of two, so a lane never straddles a padded 256-B row).
 __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk, int32_t wlen,
-                                           int32_t nb, int lane) {
+                                           int32_t nb, int kk, int lg, int lane) {
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
     RecEnt N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
     int32_t u[kCpl];
+    const int32_t lb = lane << lg;  // the lane's first byte
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
-        const int32_t p = kLaneBytes * lane + 16 * k;
+        if (k >= kk) break;
+        const int32_t p = lb + 16 * k;
         if (p >= E.rend && r + 1 < kRpt) {
             do {  // records shorter than a chunk step: rare second iteration
                 ++r;
@@ -944,22 +948,24 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     uint32_t d[kCpl][5];
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
+        if (k >= kk) break;
         int32_t i = u[k] >> 2;
         i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
         lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
 #pragma unroll
         for (int j = 0; j < 5; ++j) d[k][j] = q[j];
     }
-    lds_u8* const wl = wout + kLaneBytes * lane + (kLaneBytes * lane / 256) * kRowPad;  // 16-byte rows never split a lane
+    lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;  // padded rows never split a lane
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
+        if (k >= kk) break;
         const uint32_t sh = (uint32_t)u[k] & 3u;
         u32x4 v;
         v.x = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], sh);
         v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
         v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
         v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
-        if (kLaneBytes * lane + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
+        if (lb + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
 
@@ -968,12 +974,13 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 template <class LY>
 __device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i32* bk, const lds_u64* sbase,
-                                               int32_t wlen, int lane) {
+                                               int32_t wlen, int kk, int lg, int lane) {
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
-    lds_u8* const wl = wout + kLaneBytes * lane + (kLaneBytes * lane / 256) * kRowPad;
-    for (int k = 0; k < kCpl; ++k) {
-        const int32_t p = kLaneBytes * lane + 16 * k;
+    const int32_t lb = lane << lg;
+    lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;
+    for (int k = 0; k < kk; ++k) {
+        const int32_t p = lb + 16 * k;
         if (p >= wlen) break;
         while (p >= E.rend && r + 1 < kRpt) {
             ++r;
@@ -1072,11 +1079,15 @@ template <class LY>
 __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk,
                                             uint64_t* sbase, const TileSt& S, int32_t wrel, int32_t wlen,
                                             uintptr_t swb, int32_t nb, int lane, int ra = 0, int rb = kRpt) {
-    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lane);
+    // chunks per lane for this window: 1, 2, 4 or 8 (the lane's range: 16 kk = 2^lg bytes)
+    const int kk = wlen <= 1024 ? 1 : wlen <= 2048 ? 2 : wlen <= 4096 ? 4 : kCpl;
+    const int lg = kk == 1 ? 4 : kk == 2 ? 5 : kk == 4 ? 6 : 7;
+    static_assert(kCpl == 8, "chunk ownership sizes");
+    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);
     wsync();
 #ifndef SBE_ABL_NO_CHUNK
-    chunk_pass(wout, inb, rt, bk, wlen, nb, lane);
-    if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, lane);
+    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
+    if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, kk, lg, lane);
 #endif
     wsync();
 #ifndef SBE_ABL_NO_FIXUP
@@ -1350,13 +1361,31 @@ __device__ __forceinline__ bool seq_key_at(const R_t& R, uint32_t q, uint32_t w,
     return R.u32(st) == kSeqK0 && R.u32(st + 4) == kSeqK1 && R.u32(st + 8) == kSeqK2 && R.u32(st + 12) == kSeqK3;
 }
 
+// 0x80 in exactly the bytes of w equal to '\\' (no borrow noise: the escape flag is per byte)
+__device__ __forceinline__ uint32_t bs_bytes_exact(uint32_t w) {
+    const uint32_t x = w ^ 0x5c5c5c5cu;
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+// 0x80 in the bytes of the aligned dword at window/record offset A that lie inside [a0, a1)
+__device__ __forceinline__ uint32_t range_bytes(uint32_t A, uint32_t a0, uint32_t a1) {
+    const uint32_t lo = a0 > A ? min(a0 - A, 4u) : 0u, hi = a1 > A ? min(a1 - A, 4u) : 0u;
+    const uint64_t m = ((1ull << (8 * hi)) - 1) & ~((1ull << (8 * lo)) - 1);
+    return (uint32_t)m & 0x80808080u;
+}
+
+// SBE_FL_SEQ_KEY / SBE_FL_SEQ_ESC of the payload [p, p+n) of a record read from HBM: every dword
+// overlapping the payload is read aligned (the first and last may reach outside it, never outside
+// the 4-byte unit of a payload byte)
 template <typename R_t>
-__device__ bool has_seq_key(const R_t& R, uint32_t p, uint32_t n) {
-    if (n < 16) return false;
-    const uint32_t lead = (4u - R.abs_align(p)) & 3u;  // first aligned record offset is p + lead
-    for (uint32_t q = p + lead; q + 4 <= p + n; q += 4)
-        if (seq_key_at(R, q, R.adw(q), p, n)) return true;
-    return false;
+__device__ uint32_t has_seq_key(const R_t& R, uint32_t p, uint32_t n) {
+    if (n < 16) return 0u;
+    uint32_t fl = 0;
+    for (uint32_t q = p - R.abs_align(p); q < p + n; q += 4) {
+        const uint32_t w = R.adw(q);
+        if (bs_bytes_exact(w) & range_bytes(q, p, p + n)) fl |= SBE_FL_SEQ_ESC;
+        if (q >= p && seq_key_at(R, q, w, p, n)) fl |= SBE_FL_SEQ_KEY;
+    }
+    return fl;
 }
 
 // 0 iff some dword of v equals one of the four key slices (the candidates of seq_key_at); the
@@ -1378,26 +1407,32 @@ __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte 
 // in-chunk swizzle permutes dwords, which a membership test does not care about) without a 'q'
 // byte holds no candidate.  Only flagged chunks run the exact per-dword test.  Per lane: the
 // fallback of the window-wide scan below (more hits in one window than its list holds).
-__device__ bool has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
-    if (n < 16) return false;
+__device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
+    if (n < 16) return 0u;
     const uint32_t a0 = R.base + p, a1 = a0 + n;  // window byte range
     const uint32_t c1 = (a1 + 15) >> 4;
+    uint32_t fl = 0;
     for (uint32_t c = a0 >> 4; c < c1; c += 2) {
         const uint4 v0 = lds_read_chunk_raw(R.win, c);
         const uint4 v1 = c + 1 < c1 ? lds_read_chunk_raw(R.win, c + 1) : make_uint4(0, 0, 0, 0);
         const uint32_t t0 = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w)) & 0x80808080u;
         const uint32_t t1 = (q_bytes(v1.x) | q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
-        if ((t0 | t1) && (has_slice(v0) || has_slice(v1))) {
+        const uint32_t b0 = bs_bytes_exact(v0.x) | bs_bytes_exact(v0.y) | bs_bytes_exact(v0.z) | bs_bytes_exact(v0.w);
+        const uint32_t b1 = bs_bytes_exact(v1.x) | bs_bytes_exact(v1.y) | bs_bytes_exact(v1.z) | bs_bytes_exact(v1.w);
+        if (((t0 | t1) && (has_slice(v0) || has_slice(v1))) || (b0 | b1)) {
 #pragma nounroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t A = 16 * c + 4 * k;  // window offset of an aligned dword
+                if (A + 4 <= a0 || A >= a1) continue;
+                const uint32_t w = lds_dw(R.win, A >> 2);
+                if (bs_bytes_exact(w) & range_bytes(A, a0, a1)) fl |= SBE_FL_SEQ_ESC;
                 if (A < a0 || A + 4 > a1) continue;
                 const uint32_t q = A - R.base;
-                if (seq_key_at(R, q, R.adw(q), p, n)) return true;
+                if (seq_key_at(R, q, w, p, n)) fl |= SBE_FL_SEQ_KEY;
             }
         }
     }
-    return false;
+    return fl;
 }
 
 // Staged records are not scanned while parsing: the wave scans the whole window once
@@ -1411,7 +1446,7 @@ constexpr uint32_t kSeqLaneMax = 256;
 constexpr uint32_t kFlSeqPending = 0x80u;
 template <typename R_t>
 __device__ __forceinline__ uint32_t seq_key_state(const R_t& R, uint32_t p, uint32_t n) {
-    return has_seq_key(R, p, n) ? SBE_FL_SEQ_KEY : 0u;
+    return has_seq_key(R, p, n);
 }
 template <>
 __device__ __forceinline__ uint32_t seq_key_state<LdsRec>(const LdsRec&, uint32_t, uint32_t n) {
@@ -1427,21 +1462,28 @@ __device__ __forceinline__ uint32_t win_bytes4(const uint32_t* win, uint32_t s) 
     const uint32_t lo = lds_dw(win, s >> 2), sh = s & 3u;
     return sh ? __builtin_amdgcn_alignbyte(lds_dw(win, (s >> 2) + 1), lo, sh) : lo;
 }
+constexpr uint32_t kHitEsc = 0x80000000u;  // hit kind bit: a '\\' byte (else a key start)
 __device__ __forceinline__ void window_seq_scan(const uint32_t* win, uint32_t nbytes, int lane, uint32_t& hit,
                                                 bool& more) {
     hit = ~0u;
     more = false;
-    const uint32_t nch = nbytes >> 4;
+    const uint32_t nch = (nbytes + 15) >> 4;
 #pragma unroll 4
     for (int k = 0; k < kWin / 16 / kWave; ++k) {
         const uint32_t c = lane + kWave * k;
         const uint4 v = c < nch ? lds_read_chunk_raw(win, c) : make_uint4(0, 0, 0, 0);
         const uint32_t t = (q_bytes(v.x) | q_bytes(v.y) | q_bytes(v.z) | q_bytes(v.w)) & 0x80808080u;
-        if (t && has_slice(v)) {
+        const uint32_t b = bs_bytes_exact(v.x) | bs_bytes_exact(v.y) | bs_bytes_exact(v.z) | bs_bytes_exact(v.w);
+        if ((t && has_slice(v)) || b) {
 #pragma nounroll
             for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t A = 16 * c + 4 * j;
                 const uint32_t w = lds_dw(win, A >> 2);
+                for (uint32_t m = bs_bytes_exact(w) & range_bytes(A, 0, nbytes); m; m &= m - 1) {
+                    const uint32_t x = (A + (__builtin_ctz(m) >> 3)) | kHitEsc;
+                    if (hit == ~0u) hit = x;
+                    else more = true;
+                }
                 if (!(w == kSeqK0 || w == kSeqS1 || w == kSeqS2 || w == kSeqS3)) continue;
                 const uint32_t off = w == kSeqK0 ? 0u : w == kSeqS1 ? 1u : w == kSeqS2 ? 2u : 3u;
                 if (A < off || A - off + 16 > nbytes) continue;
@@ -1805,23 +1847,24 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
         const bool pend = here && (d.flags & kFlSeqPending);
         if (__ballot(pend) && !__ballot(pend && d.len[3] > kSeqLaneMax)) {
             if (pend)
-                d.flags = (d.flags & ~kFlSeqPending) |
-                          (has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]) ? SBE_FL_SEQ_KEY : 0u);
+                d.flags = (d.flags & ~kFlSeqPending) | has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
         } else if (__ballot(pend)) {
             uint32_t hpos;
             bool more;
             window_seq_scan(win, (uint32_t)(we - wb), lane, hpos, more);
             const uint32_t p0 = (uint32_t)(rs - wb) + d.off[3], p1 = p0 + d.len[3];
-            bool hit = false;
+            uint32_t hit = 0;
             if (__ballot(more)) {  // two hits among one lane's chunks: pending lanes scan themselves
                 if (pend) hit = has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
             } else {
                 for (uint64_t m = __ballot(hpos != ~0u); m; m &= m - 1) {  // broadcast each hit
                     const uint32_t x = __builtin_amdgcn_readlane(hpos, __builtin_ctzll(m));
-                    hit |= x >= p0 && x + 16 <= p1;
+                    const uint32_t xa = x & ~kHitEsc;
+                    if (x & kHitEsc) hit |= xa >= p0 && xa < p1 ? SBE_FL_SEQ_ESC : 0u;
+                    else hit |= x >= p0 && x + 16 <= p1 ? SBE_FL_SEQ_KEY : 0u;
                 }
             }
-            if (pend) d.flags = (d.flags & ~kFlSeqPending) | (hit ? SBE_FL_SEQ_KEY : 0u);
+            if (pend) d.flags = (d.flags & ~kFlSeqPending) | hit;
         }
     }
 }
@@ -2281,6 +2324,8 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
     return record_hip(hipGetLastError());
 }
 
+#include "seqnum.hpp"
+
 }  // namespace
 
 // ============================================================================================
@@ -2386,6 +2431,21 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     else
         hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, e0, e1, 0, a);
     prof_commit(1, e0);
+    return record_hip(hipGetLastError());
+}
+
+int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
+                              uint64_t* seq, void* stream) {
+    if (n == 0) return SBE_OK;
+    if (!in || !rec_off || !dec || !dec->status || !dec->flags || !dec->view_off || !dec->view_len || !seq)
+        return SBE_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(rec_off) & 7u) || (reinterpret_cast<uintptr_t>(seq) & 7u) ||
+        (reinterpret_cast<uintptr_t>(dec->view_off) & 3u) || (reinterpret_cast<uintptr_t>(dec->view_len) & 3u))
+        return SBE_EINVAL;
+    SeqArgs a{in, rec_off, n, dec->status, dec->flags, dec->view_off, dec->view_len, seq};
+    const uint64_t blocks = ((n + 15) / 16 + 255) / 256;  // 16 records per thread
+    hipLaunchKernelGGL(sbe_seqnum_kernel, dim3((uint32_t)(blocks < 65536 ? blocks : 65536)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
     return record_hip(hipGetLastError());
 }
 

@@ -92,6 +92,7 @@ struct Desc {
     std::vector<uint16_t> hdr;
     std::vector<uint64_t> ts;
     std::vector<uint32_t> off, len;
+    std::vector<uint64_t> seq;  // parse mode: ParseResult.sequence_number (sbe_eval_sequence_numbers)
 };
 
 Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
@@ -107,10 +108,11 @@ Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t
     for (size_t i = 0; i <= n; ++i) ro[i] = rec_off[i] - base;
     c.d_in.need(total + 16);
     c.d_roff.need((n + 1) * 8);
-    // descriptor SoA: status n, flags n, hdr 8n, ts 8n, off 20n, len 20n (each 16-B aligned)
+    // descriptor SoA: status n, flags n, hdr 8n, ts 8n, off 20n, len 20n, seq 8n (each 16-B aligned)
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
     const size_t o_st = 0, o_fl = al(n), o_hdr = o_fl + al(n), o_ts = o_hdr + al(8 * n), o_off = o_ts + al(8 * n),
-                 o_len = o_off + al(20 * n), dbytes = o_len + al(20 * n);
+                 o_len = o_off + al(20 * n), o_seq = o_len + al(20 * n), dbytes = o_seq + (parse ? al(8 * n) : 0);
     c.d_dec.need(dbytes);
     c.h_dec.need(dbytes);
     hip_check(hipMemcpyAsync(c.d_in.p, c.h_in.p, total, hipMemcpyHostToDevice, c.stream), "H2D");
@@ -120,6 +122,12 @@ Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t
                     reinterpret_cast<uint32_t*>(db + o_off), reinterpret_cast<uint32_t*>(db + o_len)};
     if (sbe_decode_batch(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, mode, &out, c.stream) != SBE_OK)
         fail("sbe_decode_batch");
+    if (parse) {  // sequence_number of the flagged TopicMessages; 0 elsewhere
+        hip_check(hipMemsetAsync(db + o_seq, 0, 8 * n, c.stream), "memset");
+        if (sbe_eval_sequence_numbers(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, &out,
+                                      reinterpret_cast<uint64_t*>(db + o_seq), c.stream) != SBE_OK)
+            fail("sbe_eval_sequence_numbers");
+    }
     hip_check(hipMemcpyAsync(c.h_dec.p, c.d_dec.p, dbytes, hipMemcpyDeviceToHost, c.stream), "D2H");
     hip_check(hipStreamSynchronize(c.stream), "sync");
     const uint8_t* hb = static_cast<const uint8_t*>(c.h_dec.p);
@@ -129,6 +137,8 @@ Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t
     d.ts.assign(reinterpret_cast<const uint64_t*>(hb + o_ts), reinterpret_cast<const uint64_t*>(hb + o_ts) + n);
     d.off.assign(reinterpret_cast<const uint32_t*>(hb + o_off), reinterpret_cast<const uint32_t*>(hb + o_off) + 5 * n);
     d.len.assign(reinterpret_cast<const uint32_t*>(hb + o_len), reinterpret_cast<const uint32_t*>(hb + o_len) + 5 * n);
+    if (parse)
+        d.seq.assign(reinterpret_cast<const uint64_t*>(hb + o_seq), reinterpret_cast<const uint64_t*>(hb + o_seq) + n);
     return d;
 }
 
@@ -155,6 +165,7 @@ ParseResult materialize(const uint8_t* rec, const Desc& d, size_t i) {
             r.headers = view(4);
             r.timestamp = (int64_t)d.ts[i];
             r.sequence_key_present = (fl & SBE_FL_SEQ_KEY) != 0;
+            r.sequence_number = d.seq.empty() ? 0 : d.seq[i];  // src/sbe_encoder.cpp:1031-1125
             take_hdr();
             break;
         case SBE_ST_ACK:  // src/sbe_encoder.cpp:916-941

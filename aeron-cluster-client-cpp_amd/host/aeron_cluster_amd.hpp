@@ -61,8 +61,10 @@ struct ParseResult {
     std::int32_t leader_member_id = 0;
     std::int32_t event_code = 0;
     std::int64_t leadership_term_id = 0;
-    // The payload carries "_sequence_number", which the reference evaluates with jsoncpp
-    // (src/sbe_encoder.cpp:1031-1125); sequence_number is then left 0 here (parity unpinned).
+    // sequence_number: "_sequence_number" of the payload JSON (src/sbe_encoder.cpp:1031-1125),
+    // evaluated on the device with jsoncpp 1.9.5 semantics (sbe_eval_sequence_numbers; jsoncpp is
+    // absent here, so parity with it is unpinned).  sequence_key_present: the payload holds the
+    // literal key bytes (SBE_FL_SEQ_KEY).
     bool sequence_key_present = false;
 
     bool is_session_event() const {

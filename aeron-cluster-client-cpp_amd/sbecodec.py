@@ -28,7 +28,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 2
+ABI_VERSION = 3
 ENC_REF_TRUNCATE8 = 0x1
 ENC_OK, ENC_OVERFLOW = 0, 6
 DEC_PARSE_MESSAGE, DEC_ON_EGRESS, DEC_LITE = 0, 1, 2
@@ -45,7 +45,7 @@ ST_ERR_SESSION_EVENT, ST_ERR_SESSION_SHORT, ST_ERR_EMBEDDED_SHORT = 19, 20, 21
 ST_ERR_EMBEDDED_TEMPLATE, ST_ERR_EMBEDDED_SCHEMA, ST_ERR_DIRECT_TEMPLATE = 22, 23, 24
 ST_ERR_TM_E100, ST_ERR_ACK_SHORT = 25, 26
 ST_EG_ACK_SIMPLE, ST_EG_ACK, ST_EG_TM, ST_EG_NONE, ST_EG_THROW_E100 = 32, 33, 34, 35, 36
-FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED = 1, 2, 4, 8, 16
+FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED, FL_SEQ_ESC = 1, 2, 4, 8, 16, 32
 
 _ERRORS = {0: "ok", -1: "EINVAL", -2: "EHIP", -3: "ENOSPC", -4: "ENODEV"}
 
@@ -113,6 +113,9 @@ def _load():
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.POINTER(_Decoded), ctypes.c_void_p]
+    lib.sbe_eval_sequence_numbers.restype = ctypes.c_int
+    lib.sbe_eval_sequence_numbers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(_Decoded), ctypes.c_void_p, ctypes.c_void_p]
     lib.sbe_profile_enable.restype = ctypes.c_int
     lib.sbe_profile_enable.argtypes = [ctypes.c_int]
     lib.sbe_profile_read.restype = ctypes.c_int
@@ -349,6 +352,22 @@ def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = No
     if n < out.status.numel():
         out = Decoded(*(getattr(out, k)[:n] for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
     return out
+
+
+def eval_sequence_numbers(data, rec_off, dec: Decoded, seq=None, stream=None) -> torch.Tensor:
+    """ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125) of the records a parse-mode
+    decode_batch flagged (FL_SEQ_KEY / FL_SEQ_ESC on a TopicMessage); the JSON evaluation runs on the
+    device.  seq (int64 [n], u64 values) is allocated zeroed when not given; entries of unflagged
+    records are not written (their sequence_number is 0)."""
+    data = _dev(data, torch.uint8, "data")
+    rec_off = _dev(rec_off, torch.int64, "rec_off")
+    n = int(rec_off.numel()) - 1
+    if seq is None:
+        seq = torch.zeros(max(n, 1), dtype=torch.int64, device=data.device)
+    d = _Decoded(*(getattr(dec, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
+    rc = lib().sbe_eval_sequence_numbers(_ptr(data), _ptr(rec_off), n, ctypes.byref(d), _ptr(seq), _stream(stream))
+    _check(rc, "sbe_eval_sequence_numbers")
+    return seq[:n]
 
 
 @dataclass

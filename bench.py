@@ -2,7 +2,10 @@
 
 One step = one round trip of the hot path over one batch resident in HBM:
   sbe_encode_topic_batch (wire-correct TopicMessages, packed SoA input → packed stream + offsets)
-  → sbe_decode_batch(PARSE_MESSAGE) (stream + offsets → per-record descriptors).
+  → sbe_decode_batch(PARSE_MESSAGE) (stream + offsets → per-record descriptors)
+  → sbe_eval_sequence_numbers (ParseResult.sequence_number of the flagged records; this workload's
+    payloads carry no "_sequence_number" and no escapes, as the Order JSON of the reference has
+    none, so the launch reads the flags and writes nothing).
 Workload (BASELINE.json configs[1] extended to the metric's encode+decode): 1,000,000 fixed-256 B
 Order TopicMessages per GPU (seed 0x5EED0002 + rank), synthetic.
 
@@ -112,7 +115,8 @@ def cpu_baseline(n_sample, budget_s, threads):
         done, t0 = 0, time.perf_counter()
         while True:
             out, off, _ = T.oracle_encode(arena, L, ts, nthreads=nthreads)
-            T.oracle_decode(out, off, T.DEC_PARSE, nthreads=nthreads)
+            d = T.oracle_decode(out, off, T.DEC_PARSE, nthreads=nthreads)
+            T.oracle_seq_batch(out, off, d, nthreads=nthreads)
             done += n_sample
             el = time.perf_counter() - t0
             if el >= budget:
@@ -139,6 +143,7 @@ def main():
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     ws = sbecodec.alloc_workspace(n, dev)
     dec = sbecodec.alloc_decoded(n, dev)
+    seq = torch.zeros(n, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
     ev_enc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -155,6 +160,7 @@ def main():
             ev_enc[k][1].record(stream)
             ev_dec[k][0].record(stream)
         sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream)
+        sbecodec.eval_sequence_numbers(out, out_off, dec, seq=seq, stream=stream)
         if k is not None:
             ev_dec[k][1].record(stream)
 
@@ -220,7 +226,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "roundtrip_fixed256_orders", "records_per_gpu": n, "record_bytes": 256,
                        "encode": "wire-correct TopicMessage, packed SoA input",
-                       "decode": "parse_message descriptors (views)", "parallelism": f"shard{world}"},
+                       "decode": "parse_message descriptors (views) + sequence_number evaluation", "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": dom["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
                          "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"],

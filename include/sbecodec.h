@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 2
+#define SBECODEC_ABI_VERSION 3
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -218,9 +218,12 @@ int sbe_encode_lite_batch(const sbe_lite_batch* in, uint64_t n, uint32_t templat
 #define SBE_FL_ID_DEFAULT 0x1u      /* ack: message_id = "ack_" + decimal(ts) */
 #define SBE_FL_PAYLOAD_DEFAULT 0x2u /* ack: payload = "SUCCESS" */
 #define SBE_FL_HEADERS_E100 0x4u    /* TM: headers read hit E100 and was swallowed (headers = "") */
-#define SBE_FL_SEQ_KEY 0x8u         /* TM: payload contains "_sequence_number" (jsoncpp lookup,
-                                       src/sbe_encoder.cpp:1031-1125, not evaluated: parity unpinned) */
+#define SBE_FL_SEQ_KEY 0x8u         /* TM: payload (>= 16 B) contains the bytes "_sequence_number" */
 #define SBE_FL_WRAPPED 0x10u        /* record was a schema-111 session message (embedded decode) */
+#define SBE_FL_SEQ_ESC 0x20u        /* TM: payload (>= 16 B) contains a '\\' byte (a key spelled with
+                                       \u escapes decodes to "_sequence_number" without containing it) */
+/* A TM record without SEQ_KEY and SEQ_ESC has ParseResult.sequence_number == 0 under any JSON
+ * parser; sbe_eval_sequence_numbers evaluates the others. */
 
 /* Decoded records, struct of arrays, all device arrays of n (or n*4 / n*5) elements.
  *   hdr      [n][4] block_length, template_id, schema_id, version as ParseResult reports them.
@@ -241,6 +244,19 @@ typedef struct sbe_decoded {
  * the SBE header carries no total length.  Alignment: in 16 B, rec_off/hdr/ts 8 B, views 4 B. */
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream);
+
+/* ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125): for every record that
+ * sbe_decode_batch(SBE_DEC_PARSE_MESSAGE) left with status SBE_ST_TM and flag SBE_FL_SEQ_KEY or
+ * SBE_FL_SEQ_ESC, parse its payload with the semantics of jsoncpp 1.9.5's CharReaderBuilder
+ * defaults (comments and trailing commas allowed, extra content after the root ignored, stack
+ * limit 1000, UTF-8 BOM skipped) and write seq[i] = the first non-zero "_sequence_number" of
+ * root, root.message, root.message.message, root.message.message.message (extractSequence:
+ * integers as u64, other numbers through a correctly rounded double and the x86-64 cast, strings
+ * through std::stoull), or 0 when the payload does not parse.  seq[i] of any other record is not
+ * written: its sequence_number is 0.  in / rec_off / status / flags / view_* are the arguments and
+ * outputs of that decode call; seq is a device u64[n] (8-B aligned).  Same stream order rules. */
+int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
+                              uint64_t* seq, void* stream);
 
 /* ============================ Aeron fragment reassembly ============================ */
 /* Replaces LocalFragmentReassembler::onFragment (src/cluster_client.cpp:39-82) for a batch of

@@ -8,6 +8,7 @@
  */
 #include "sbe_oracle.h"
 
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -265,8 +266,8 @@ static void set_hdr(desc_t* d, const uint8_t* p) {
     d->hdr[3] = rd16(p + 6);
 }
 
-/* Does [p, p+n) contain "_sequence_number"?  Marks the jsoncpp-dependent case
- * (src/sbe_encoder.cpp:1031-1125), whose sequence_number is not evaluated (parity unpinned). */
+/* Does [p, p+n) contain "_sequence_number"?  With SBE_FL_SEQ_ESC, marks the payloads whose
+ * sequence_number needs the JSON evaluation below (src/sbe_encoder.cpp:1031-1125). */
 static int has_seq_key(const uint8_t* p, uint64_t n) {
     static const char key[] = "_sequence_number";
     const uint64_t k = sizeof(key) - 1;
@@ -304,6 +305,7 @@ static void dec_tm_parse(const uint8_t* rec, uint64_t len, uint64_t base, desc_t
     r.ts = rd64(rec + 8); /* in bounds: success implies len >= 16 + blk */
     if (base) r.flags |= SBE_FL_WRAPPED;
     if (has_seq_key(rec + (r.off[3] - base), r.len[3])) r.flags |= SBE_FL_SEQ_KEY;
+    if (r.len[3] >= 16 && memchr(rec + (r.off[3] - base), '\\', r.len[3])) r.flags |= SBE_FL_SEQ_ESC;
     /* headers in their own try: E100 → headers = "" and success stays (:1127-1135) */
     if (pos + 2 > len || pos + 2 + (uint64_t)rd16(rec + pos) > len) {
         r.flags |= SBE_FL_HEADERS_E100;
@@ -582,5 +584,403 @@ int orc_reassemble(const uint8_t* in, const uint64_t* frag_off, const uint8_t* f
     memcpy(out + at, acc_buf, acc);
     counts[0] = m;
     counts[1] = acc;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125): parse the payload with jsoncpp's
+ * CharReaderBuilder defaults (jsoncpp 1.9: comments allowed, trailing commas allowed, extra
+ * content after the root ignored, no single quotes / numeric keys / special floats, stack limit
+ * 1000; OurReader's tokenizer: a NUL byte outside a string ends the stream), then look up
+ * "_sequence_number" in the root object, root.message, root.message.message and
+ * root.message.message.message, first value > 0 wins (extractSequence: UInt64, Int64, other
+ * numbers through double, strings through std::stoull, else 0).  Any parse failure or exception
+ * gives 0.  jsoncpp is absent from this image: PARITY UNPINNED (restated from its published
+ * algorithm; decimal → double is exact only on the Clinger fast path, ≤ 19 significant digits).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    const uint8_t* p;
+    uint64_t n, i;
+} jcur;
+
+enum { JT_OBEG, JT_OEND, JT_ABEG, JT_AEND, JT_STR, JT_NUM, JT_TRUE, JT_FALSE, JT_NULL, JT_COMMA, JT_COLON,
+       JT_COMMENT, JT_EOS, JT_ERR };
+
+static int jc_get(jcur* c) { return c->i < c->n ? c->p[c->i++] : 0; }
+
+static void jc_skip_spaces(jcur* c) {
+    while (c->i < c->n) {
+        const uint8_t ch = c->p[c->i];
+        if (ch == ' ' || ch == '\t' || ch == '\r' || ch == '\n') ++c->i;
+        else break;
+    }
+}
+
+/* OurReader::readToken; *s, *e: the token's bytes */
+static int jc_token(jcur* c, uint64_t* s, uint64_t* e) {
+    jc_skip_spaces(c);
+    *s = c->i;
+    const int ch = jc_get(c);
+    int t = JT_ERR;
+    switch (ch) {
+        case '{': t = JT_OBEG; break;
+        case '}': t = JT_OEND; break;
+        case '[': t = JT_ABEG; break;
+        case ']': t = JT_AEND; break;
+        case ',': t = JT_COMMA; break;
+        case ':': t = JT_COLON; break;
+        case 0: t = JT_EOS; break;
+        case '"': { /* readString: to the next unescaped quote */
+            int q = 0;
+            while (c->i < c->n) {
+                const int x = jc_get(c);
+                if (x == '\\') jc_get(c);
+                else if (x == '"') { q = 1; break; }
+            }
+            t = q ? JT_STR : JT_ERR;
+            break;
+        }
+        case '/': { /* readComment */
+            const int x = jc_get(c);
+            if (x == '*') { /* readCStyleComment: stops one byte early, then needs '/' */
+                int ok = 0;
+                while (c->i + 1 < c->n) {
+                    const int y = jc_get(c);
+                    if (y == '*' && c->p[c->i] == '/') break;
+                }
+                ok = jc_get(c) == '/';
+                t = ok ? JT_COMMENT : JT_ERR;
+            } else if (x == '/') {
+                while (c->i < c->n) {
+                    const int y = jc_get(c);
+                    if (y == '\n') break;
+                    if (y == '\r') { if (c->i < c->n && c->p[c->i] == '\n') ++c->i; break; }
+                }
+                t = JT_COMMENT;
+            } else {
+                t = JT_ERR;
+            }
+            break;
+        }
+        case 't': t = (c->n - c->i >= 3 && memcmp(c->p + c->i, "rue", 3) == 0) ? (c->i += 3, JT_TRUE) : JT_ERR; break;
+        case 'f': t = (c->n - c->i >= 4 && memcmp(c->p + c->i, "alse", 4) == 0) ? (c->i += 4, JT_FALSE) : JT_ERR; break;
+        case 'n': t = (c->n - c->i >= 3 && memcmp(c->p + c->i, "ull", 3) == 0) ? (c->i += 3, JT_NULL) : JT_ERR; break;
+        default:
+            if (ch == '-' && c->i < c->n && c->p[c->i] == 'I') { /* readNumber(checkInf): -Infinity, not allowed */
+                ++c->i;
+                t = JT_ERR;
+            } else if ((ch >= '0' && ch <= '9') || ch == '-') { /* readNumber */
+                uint64_t k = c->i;
+                int x = '0';
+#define NX() (x = (c->i = k) < c->n ? c->p[k++] : 0)
+                while (x >= '0' && x <= '9') NX();
+                if (x == '.') { NX(); while (x >= '0' && x <= '9') NX(); }
+                if (x == 'e' || x == 'E') { NX(); if (x == '+' || x == '-') NX(); while (x >= '0' && x <= '9') NX(); }
+#undef NX
+                t = JT_NUM;
+            }
+            break;
+    }
+    *e = c->i;
+    return t;
+}
+
+/* Reader::decodeString into out (up to cap bytes kept; *len = full decoded length); 0 on error */
+static void jc_utf8(uint32_t cp, uint8_t* out, uint64_t cap, uint64_t* len) {
+    uint8_t b[4];
+    int k = 0;
+    if (cp <= 0x7f) b[k++] = (uint8_t)cp;
+    else if (cp <= 0x7ff) { b[k++] = (uint8_t)(0xc0 | (cp >> 6)); b[k++] = (uint8_t)(0x80 | (cp & 0x3f)); }
+    else if (cp <= 0xffff) { b[k++] = (uint8_t)(0xe0 | (cp >> 12)); b[k++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3f)); b[k++] = (uint8_t)(0x80 | (cp & 0x3f)); }
+    else if (cp <= 0x10ffff) { b[k++] = (uint8_t)(0xf0 | (cp >> 18)); b[k++] = (uint8_t)(0x80 | ((cp >> 12) & 0x3f)); b[k++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3f)); b[k++] = (uint8_t)(0x80 | (cp & 0x3f)); }
+    for (int j = 0; j < k; ++j) { if (*len < cap) out[*len] = b[j]; ++*len; }
+}
+static int jc_hex4(const uint8_t* p, uint64_t avail, uint32_t* v) {
+    if (avail < 4) return 0;
+    uint32_t r = 0;
+    for (int j = 0; j < 4; ++j) {
+        const uint8_t h = p[j];
+        r <<= 4;
+        if (h >= '0' && h <= '9') r |= h - '0';
+        else if (h >= 'a' && h <= 'f') r |= h - 'a' + 10;
+        else if (h >= 'A' && h <= 'F') r |= h - 'A' + 10;
+        else return 0;
+    }
+    *v = r;
+    return 1;
+}
+static int jc_decode_string(const uint8_t* p, uint64_t s, uint64_t e, uint8_t* out, uint64_t cap, uint64_t* len) {
+    *len = 0;
+    uint64_t i = s + 1, end = e - 1; /* inside the quotes */
+    while (i < end) {
+        const uint8_t ch = p[i++];
+        if (ch == '"') break;
+        if (ch == '\\') {
+            if (i == end) return 0; /* "Empty escape sequence in string" */
+            const uint8_t x = p[i++];
+            uint8_t o = 0;
+            switch (x) {
+                case '"': o = '"'; break;
+                case '/': o = '/'; break;
+                case '\\': o = '\\'; break;
+                case 'b': o = '\b'; break;
+                case 'f': o = '\f'; break;
+                case 'n': o = '\n'; break;
+                case 'r': o = '\r'; break;
+                case 't': o = '\t'; break;
+                case 'u': {
+                    uint32_t cp;
+                    if (!jc_hex4(p + i, end - i, &cp)) return 0;
+                    i += 4;
+                    if (cp >= 0xD800 && cp <= 0xDBFF) { /* surrogate pair: another \uXXXX must follow */
+                        if (end - i < 6) return 0;
+                        if (p[i] != '\\' || p[i + 1] != 'u') return 0;
+                        uint32_t lo;
+                        if (!jc_hex4(p + i + 2, end - i - 2, &lo)) return 0;
+                        i += 6;
+                        cp = 0x10000 + ((cp & 0x3FF) << 10) + (lo & 0x3FF);
+                    }
+                    jc_utf8(cp, out, cap, len);
+                    continue;
+                }
+                default: return 0; /* "Bad escape sequence in string" */
+            }
+            if (*len < cap) out[*len] = o;
+            ++*len;
+        } else {
+            if (*len < cap) out[*len] = ch;
+            ++*len;
+        }
+    }
+    return 1;
+}
+
+/* decoded value of one number token: kind 1 int64, 2 uint64, 3 double; 0 on error */
+static int jc_decode_number(const uint8_t* p, uint64_t s, uint64_t e, int64_t* iv, uint64_t* uv, double* dv) {
+    uint64_t i = s;
+    const int neg = p[i] == '-';
+    if (neg) ++i;
+    const uint64_t maxv = neg ? (uint64_t)1 << 63 : ~0ull;
+    const uint64_t thr = maxv / 10, lastd = maxv % 10;
+    uint64_t v = 0;
+    int dbl = 0;
+    for (; i < e; ++i) {
+        const uint8_t ch = p[i];
+        if (ch < '0' || ch > '9') { dbl = 1; break; }
+        const uint64_t dg = ch - '0';
+        if (v >= thr && (v > thr || i + 1 != e || dg > lastd)) { dbl = 1; break; }
+        v = v * 10 + dg;
+    }
+    if (!dbl) {
+        if (neg) { *iv = (int64_t)(0 - v); return 1; }
+        if (v <= (uint64_t)INT64_MAX) { *iv = (int64_t)v; return 1; }
+        *uv = v;
+        return 2;
+    }
+    /* decodeDouble: istringstream >> double over the token.  libstdc++'s num_get hands the
+     * accumulated characters to strtod and fails unless all of them convert; an overflow
+     * (±HUGE_VAL) becomes ±max with failbit, which jsoncpp turns back into ±infinity.  The token
+     * grammar (readNumber) admits only digits, '-', '.', 'e', 'E', '+', so strtod over the whole
+     * token is the same conversion (glibc strtod is correctly rounded). */
+    char sbuf[128];
+    const uint64_t tl = e - s;
+    char* tb = tl < sizeof sbuf ? sbuf : (char*)malloc(tl + 1);
+    if (!tb) return 0;
+    memcpy(tb, p + s, tl);
+    tb[tl] = 0;
+    char* endp = NULL;
+    const double d = strtod(tb, &endp);
+    const int full = endp == tb + tl && tl > 0;
+    if (tb != sbuf) free(tb);
+    if (!full) return 0; /* "'...' is not a number." */
+    *dv = d;
+    return 3;
+}
+
+/* extractSequence on a realValue d (jsoncpp 1.9.5 json_value.cpp): isUInt64 (integral, 0 <= d < 2^64)
+ * → asUInt64; isInt64 (integral, -2^63 <= d < 2^63) → asInt64; else static_cast<uint64_t>(asDouble())
+ * as x86-64 gcc compiles it: d < 2^63 → cvttsd2si(d), else cvttsd2si(d - 2^63) ^ 2^63, where
+ * cvttsd2si gives 0x8000000000000000 out of range (so d >= 2^64, +inf included, gives 0). */
+static uint64_t jc_real_seq(double d) {
+    if (d != d) return 0x8000000000000000ull;
+    if (d >= 18446744073709551616.0) return 0;
+    if (d >= 9223372036854775808.0) return (uint64_t)d; /* integral: exact */
+    if (d < -9223372036854775808.0) return 0x8000000000000000ull;
+    return (uint64_t)(int64_t)d; /* truncation toward zero */
+}
+
+/* std::stoull(s) (base 10) with 0 for the exceptions the reference catches */
+static uint64_t jc_stoull(const uint8_t* s, uint64_t n) {
+    uint64_t i = 0;
+    while (i < n && (s[i] == ' ' || (s[i] >= 9 && s[i] <= 13))) ++i;
+    if (i < n && s[i] == 0) return 0;
+    int neg = 0;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; ++i; }
+    uint64_t v = 0;
+    int any = 0, ovf = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) {
+        any = 1;
+        const uint64_t dg = s[i] - '0';
+        if (v > (~0ull - dg) / 10) ovf = 1;
+        else v = v * 10 + dg;
+    }
+    if (!any || ovf) return 0; /* invalid_argument / out_of_range */
+    return neg ? 0 - v : v;
+}
+
+#define J_MAX_DEPTH 1000
+#define J_KEYCAP 32
+uint64_t orc_seq_eval(const uint8_t* p, uint64_t n) {
+    jcur c = {p, n, 0};
+    if (n >= 3 && p[0] == 0xEF && p[1] == 0xBB && p[2] == 0xBF) c.i = 3; /* skipBom (jsoncpp 1.9.5) */
+    uint8_t stk[J_MAX_DEPTH + 2]; /* 1 object, 2 array */
+    int depth = 0;                /* containers open */
+    int chain = 0;                /* containers [0, chain) are the root / message chain objects */
+    uint64_t res[4] = {0, 0, 0, 0};
+    int hobj[4] = {0, 0, 0, 0};
+    int root_obj = 0;
+    /* the member whose value comes next: 0 other, 1 "_sequence_number", 2 "message" (of a chain object) */
+    int pend_kind = 0, pend_level = 0;
+    uint64_t s, e;
+    int t;
+    enum { S_VALUE, S_KEY, S_COLON, S_OAFTER, S_AFIRST, S_AAFTER } st = S_VALUE;
+    for (;;) {
+        if (st == S_VALUE || st == S_AFIRST) {
+            if (st == S_AFIRST) { /* readArray: ']' right after '[' or a ',' (spaces only) */
+                jc_skip_spaces(&c);
+                if (c.i < c.n && c.p[c.i] == ']') {
+                    ++c.i;
+                    --depth;
+                    goto value_done;
+                }
+            }
+            if (depth >= J_MAX_DEPTH) return 0; /* "Exceeded stackLimit in readValue()" */
+            do t = jc_token(&c, &s, &e); while (t == JT_COMMENT);
+            const int kind = pend_kind, level = pend_level;
+            pend_kind = 0;
+            switch (t) {
+                case JT_OBEG:
+                    stk[depth++] = 1;
+                    if (depth == 1) { root_obj = 1; chain = 1; }
+                    else if (kind == 2 && depth - 1 == level + 1 && chain == level + 1) { chain = depth; hobj[level + 1] = 1; }
+                    if (kind == 1) res[level] = 0;
+                    st = S_KEY;
+                    continue;
+                case JT_ABEG:
+                    stk[depth++] = 2;
+                    if (kind == 1) res[level] = 0;
+                    st = S_AFIRST;
+                    continue;
+                case JT_NUM: {
+                    int64_t iv = 0;
+                    uint64_t uv = 0;
+                    double dv = 0;
+                    const int k = jc_decode_number(c.p, s, e, &iv, &uv, &dv);
+                    if (!k) return 0;
+                    if (kind == 1) {
+                        if (k == 1) res[level] = (uint64_t)iv; /* isUInt64 / isInt64 */
+                        else if (k == 2) res[level] = uv;
+                        else res[level] = jc_real_seq(dv);
+                    }
+                    break;
+                }
+                case JT_STR: {
+                    uint8_t buf[64];
+                    uint64_t len;
+                    if (!jc_decode_string(c.p, s, e, buf, sizeof buf, &len)) return 0;
+                    if (kind == 1) {
+                        /* c_str(): stops at an embedded NUL */
+                        uint64_t m = len < sizeof buf ? len : sizeof buf;
+                        for (uint64_t j = 0; j < m; ++j) if (buf[j] == 0) { m = j; break; }
+                        res[level] = len <= sizeof buf ? jc_stoull(buf, m) : 0;
+                        if (len > sizeof buf) { /* long strings: decode fully (rare) */
+                            uint8_t* big = (uint8_t*)__builtin_alloca(len);
+                            jc_decode_string(c.p, s, e, big, len, &len);
+                            uint64_t mm = len;
+                            for (uint64_t j = 0; j < len; ++j) if (big[j] == 0) { mm = j; break; }
+                            res[level] = jc_stoull(big, mm);
+                        }
+                    }
+                    break;
+                }
+                case JT_TRUE: case JT_FALSE: case JT_NULL:
+                    if (kind == 1) res[level] = 0;
+                    break;
+                default:
+                    return 0; /* "Syntax error: value, object or array expected." */
+            }
+        value_done:
+            if (depth == 0) break; /* root done: extra content is ignored */
+            st = stk[depth - 1] == 1 ? S_OAFTER : S_AAFTER;
+            continue;
+        }
+        if (st == S_KEY) { /* key or '}' (empty object or trailing comma) */
+            do t = jc_token(&c, &s, &e); while (t == JT_COMMENT);
+            if (t == JT_OEND) {
+                if (depth == chain) chain = depth - 1;
+                --depth;
+                goto value_done;
+            }
+            if (t != JT_STR) return 0;
+            uint8_t key[J_KEYCAP];
+            uint64_t klen;
+            if (!jc_decode_string(c.p, s, e, key, J_KEYCAP, &klen)) return 0;
+            if (depth == chain && depth <= 4) {
+                const int level = depth - 1;
+                if (klen == 16 && memcmp(key, "_sequence_number", 16) == 0) { pend_kind = 1; pend_level = level; }
+                else if (klen == 7 && memcmp(key, "message", 7) == 0 && level < 3) {
+                    pend_kind = 2;
+                    pend_level = level;
+                    for (int k = level + 1; k < 4; ++k) { res[k] = 0; hobj[k] = 0; }
+                }
+            }
+            do t = jc_token(&c, &s, &e); while (0);
+            if (t != JT_COLON) return 0; /* "Missing ':' after object member name" */
+            st = S_VALUE;
+            continue;
+        }
+        if (st == S_OAFTER) {
+            t = jc_token(&c, &s, &e);
+            if (t != JT_OEND && t != JT_COMMA && t != JT_COMMENT) return 0;
+            if (t == JT_COMMENT) { /* after comments, the next token is taken as the separator */
+                while (t == JT_COMMENT) t = jc_token(&c, &s, &e);
+                if (t == JT_ERR && s == e) return 0;
+            }
+            if (t == JT_OEND) {
+                if (depth == chain) chain = depth - 1;
+                --depth;
+                goto value_done;
+            }
+            st = S_KEY;
+            continue;
+        }
+        if (st == S_AAFTER) {
+            do t = jc_token(&c, &s, &e); while (t == JT_COMMENT);
+            if (t == JT_AEND) { --depth; goto value_done; }
+            if (t != JT_COMMA) return 0; /* "Missing ',' or ']' in array declaration" */
+            st = S_AFIRST;
+            continue;
+        }
+    }
+    if (!root_obj) return 0; /* isMember on a non-object root throws (or is false for null) */
+    if (res[0]) return res[0];
+    for (int k = 1; k < 4; ++k) {
+        if (!hobj[k]) break;
+        if (res[k]) return res[k];
+    }
+    return 0;
+}
+
+int orc_seq_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const uint8_t* status,
+                  const uint8_t* flags, const uint32_t* view_off, const uint32_t* view_len, uint64_t* seq,
+                  int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        if (status[i] != SBE_ST_TM || !(flags[i] & (SBE_FL_SEQ_KEY | SBE_FL_SEQ_ESC))) continue;
+        seq[i] = orc_seq_eval(in + rec_off[i] + view_off[5 * i + 3], view_len[5 * i + 3]);
+    }
     return 0;
 }

@@ -65,6 +65,15 @@ int orc_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
 int orc_reassemble(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
                    uint8_t* out, uint64_t* msg_off, uint64_t counts[2], uint8_t* acc_buf);
 
+/* ParseResult.sequence_number of a payload (src/sbe_encoder.cpp:1031-1125 over jsoncpp 1.9.5's
+ * CharReaderBuilder defaults; jsoncpp is absent here: PARITY UNPINNED, restated). */
+uint64_t orc_seq_eval(const uint8_t* payload, uint64_t n);
+
+/* sbe_eval_sequence_numbers over host arrays (the outputs of orc_decode_batch in parse mode). */
+int orc_seq_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const uint8_t* status,
+                  const uint8_t* flags, const uint32_t* view_off, const uint32_t* view_len, uint64_t* seq,
+                  int nthreads);
+
 /* protocol.hpp:37-42 */
 uint64_t orc_to_nanos_auto(uint64_t ts);
 

@@ -17,6 +17,7 @@ PROF = os.path.join(ROOT, "profiles")
 # rocprof kernel names (TopicMessage layout Lay<0, 16, 5, true>, packed input, wire length)
 KERNELS = {"sbe_enc_pack<(anonymous namespace)::Lay<0, 16, 5, true>, true, false>": "sbe_enc_pack<packed,wire>",
            "sbe_decode_kernel<0u>": "sbe_decode_kernel<parse_message>",
+           "sbe_seqnum_kernel": "sbe_seqnum_kernel",
            "sbe_enc_sums<(anonymous namespace)::Lay<0, 16, 5, true>, true, false>": "sbe_enc_sums<packed,wire>"}
 
 

@@ -77,6 +77,23 @@ int main() {
     std::vector<uint8_t> cut(wire.begin(), wire.begin() + 50);
     pr = MessageParser::parse_message(cut.data(), cut.size());
     CHECK(!pr.success && pr.template_id == 0 && pr.error_message == "SBE TopicMessage decoding failed: buffer too short [E100]");
+    // sequence_number: the payload's "_sequence_number", evaluated on the device (jsoncpp 1.9.5
+    // semantics; src/sbe_encoder.cpp:1031-1125), against the oracle restatement
+    {
+        const std::vector<std::string> pays = {
+            "{\"_sequence_number\":17}", "{\"message\":{\"_sequence_number\":\"4\"}}",
+            "{\"\\u005fsequence_number\": 9}", "/* c */ {\"_sequence_number\": 2.5,}", "{\"_sequence_number\": -1}",
+            "{\"_sequence_number\": 5", "[{\"_sequence_number\": 5}]", "{\"a\": \"\\\"q\\\"\"}"};
+        const uint64_t want[] = {17, 4, 9, 2, ~0ULL, 0, 0, 0};
+        for (size_t k = 0; k < pays.size(); ++k) {
+            auto f = f5;
+            f[3] = pays[k];
+            auto w = wire_tm(f, 7);
+            auto p = MessageParser::parse_message(w.data(), w.size());
+            const uint64_t o = orc_seq_eval(reinterpret_cast<const uint8_t*>(pays[k].data()), pays[k].size());
+            CHECK(p.success && p.payload == pays[k] && p.sequence_number == want[k] && o == want[k]);
+        }
+    }
     auto t9 = wire;
     t9[2] = 9;
     pr = MessageParser::parse_message(t9.data(), t9.size());

@@ -35,7 +35,7 @@ ST_ERR_SESSION_EVENT, ST_ERR_SESSION_SHORT, ST_ERR_EMBEDDED_SHORT = 19, 20, 21
 ST_ERR_EMBEDDED_TEMPLATE, ST_ERR_EMBEDDED_SCHEMA, ST_ERR_DIRECT_TEMPLATE = 22, 23, 24
 ST_ERR_TM_E100, ST_ERR_ACK_SHORT = 25, 26
 ST_EG_ACK_SIMPLE, ST_EG_ACK, ST_EG_TM, ST_EG_NONE, ST_EG_THROW_E100 = 32, 33, 34, 35, 36
-FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED = 1, 2, 4, 8, 16
+FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED, FL_SEQ_ESC = 1, 2, 4, 8, 16, 32
 
 U64 = np.uint64
 
@@ -63,6 +63,9 @@ def oracle():
         L.orc_encode_lite_batch.argtypes = [vp, vp, vp, vp, vp, u64, u32, vp, vp, vp, i]
         L.orc_reassemble.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
         L.orc_decode_batch.argtypes = [vp, vp, u64, u32, vp, vp, vp, vp, vp, vp, i]
+        L.orc_seq_eval.restype = u64
+        L.orc_seq_eval.argtypes = [vp, u64]
+        L.orc_seq_batch.argtypes = [vp, vp, u64, vp, vp, vp, vp, vp, i]
         L.orc_to_nanos_auto.restype = u64
         L.orc_to_nanos_auto.argtypes = [u64]
         _oracle = L
@@ -192,6 +195,25 @@ def oracle_decode(data, rec_off, mode=DEC_PARSE, nthreads=1):
     oracle().orc_decode_batch(_p(buf), _p(rec_off), n, mode, _p(d["status"]), _p(d["flags"]), _p(d["hdr"]),
                               _p(d["ts"]), _p(d["view_off"]), _p(d["view_len"]), nthreads)
     return {k: v[:n] for k, v in d.items()}
+
+
+def oracle_seq_eval(payload: bytes) -> int:
+    """ParseResult.sequence_number of one payload (oracle restatement of jsoncpp 1.9.5; unpinned)."""
+    buf = np.frombuffer(payload, np.uint8) if payload else np.zeros(1, np.uint8)
+    return int(oracle().orc_seq_eval(_p(np.ascontiguousarray(buf)), len(payload)))
+
+
+def oracle_seq_batch(data, rec_off, dec, nthreads=1):
+    """sbe_eval_sequence_numbers over the oracle's parse-mode descriptors; unwritten slots stay 0."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = rec_off.size - 1
+    seq = np.zeros(max(n, 1), np.uint64)
+    buf = data if data.size else np.zeros(1, np.uint8)
+    oracle().orc_seq_batch(_p(buf), _p(rec_off), n, _p(np.ascontiguousarray(dec["status"])),
+                           _p(np.ascontiguousarray(dec["flags"])), _p(np.ascontiguousarray(dec["view_off"])),
+                           _p(np.ascontiguousarray(dec["view_len"])), _p(seq), nthreads)
+    return seq[:n]
 
 
 # ------------------------------------------------------------------------------------------
@@ -499,6 +521,7 @@ def var_orders(n: int, seed: int = 0x5EED0004):
     fill = splitmix64(seed ^ 0xABCDEF, (arena.size + 7) // 8).view(np.uint8)[: arena.size]
     arena[:] = (fill % 94) + 32
     arena[arena == ord('_')] = ord('-')  # keep "_sequence_number" out of synthetic payloads
+    arena[arena == ord('\\')] = ord('/')  # and escapes (JSON order payloads carry none)
     base = starts[:-1]
     for k, t in enumerate(_TOPICS):
         idx = base[ti == k]
