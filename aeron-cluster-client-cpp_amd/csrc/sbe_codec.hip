@@ -1244,6 +1244,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
     }
 }
 
+#include "seqnum.hpp"
+
 // ------------------------------------------------------------------------------------------
 // Decode
 // ------------------------------------------------------------------------------------------
@@ -1257,6 +1259,7 @@ struct DecArgs {
     uint64_t* ts;
     uint32_t* view_off;
     uint32_t* view_len;
+    uint64_t* seq;  // parse mode, optional: sequence_number of the flagged TopicMessages
 };
 
 // Reads of one record: LDS window [wb, we) where staged, global memory elsewhere.
@@ -1958,6 +1961,12 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
             dst_store(vl + i, win[5 * kWave + i]);
         }
     }
+    // ParseResult.sequence_number of flagged TopicMessages (rare: payloads with the key or a
+    // backslash), evaluated from HBM by the lanes that hold one
+    if (kMode == SBE_DEC_PARSE_MESSAGE && a.seq) {
+        const bool cand = valid && d.status == SBE_ST_TM && (d.flags & kSeqCand);
+        if (__ballot(cand) && cand) a.seq[r] = json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
+    }
 }
 
 thread_local char g_last_error[256] = "";
@@ -2324,8 +2333,6 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
     return record_hip(hipGetLastError());
 }
 
-#include "seqnum.hpp"
-
 }  // namespace
 
 // ============================================================================================
@@ -2419,7 +2426,11 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
         return SBE_EINVAL;
     const uint64_t tiles = (n + kTile - 1) / kTile;
     if (tiles > kMaxTiles) return SBE_EINVAL;
-    DecArgs a{in, rec_off, n, out->status, out->flags, out->hdr, out->ts, out->view_off, out->view_len};
+    if (mode == SBE_DEC_PARSE_MESSAGE && out->seq && (reinterpret_cast<uintptr_t>(out->seq) & 7u)) return SBE_EINVAL;
+    DecArgs a{in,           rec_off,       n,
+              out->status,  out->flags,    out->hdr,
+              out->ts,      out->view_off, out->view_len,
+              mode == SBE_DEC_PARSE_MESSAGE ? out->seq : nullptr};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((uint32_t)tiles), block(kWave);
     hipEvent_t e0, e1;

@@ -510,6 +510,10 @@ __device__ uint64_t json_seq_eval(const uint8_t* p, uint32_t n) {
 }
 
 #ifndef SEQNUM_HOST_CHECK  // tests/cpp/seqnum_host_check.cpp compiles the parser above for the host
+// the decode kernel's call (parse mode with sbe_decoded.seq): kept out of line so the rare
+// evaluation does not widen the decode kernel's register allocation
+__device__ __noinline__ uint64_t json_seq_eval_call(const uint8_t* p, uint32_t n) { return json_seq_eval(p, n); }
+
 struct SeqArgs {
     const uint8_t* in;
     const uint64_t* rec_off;
@@ -521,6 +525,7 @@ struct SeqArgs {
     uint64_t* seq;
 };
 
+// Standalone launch (sbe_eval_sequence_numbers), for descriptors decoded without sbe_decoded.seq.
 // One lane per flagged record.  A thread first tests the flags of 16 records with one 16-B load
 // (the common batch has no candidate at all, so the launch is a 1-B/record flag read).
 constexpr uint32_t kSeqCand = SBE_FL_SEQ_KEY | SBE_FL_SEQ_ESC;

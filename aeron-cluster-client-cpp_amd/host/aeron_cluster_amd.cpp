@@ -119,15 +119,13 @@ Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t
     hip_check(hipMemcpyAsync(c.d_roff.p, c.h_roff.p, (n + 1) * 8, hipMemcpyHostToDevice, c.stream), "H2D");
     uint8_t* db = static_cast<uint8_t*>(c.d_dec.p);
     sbe_decoded out{db + o_st, db + o_fl, reinterpret_cast<uint16_t*>(db + o_hdr), reinterpret_cast<uint64_t*>(db + o_ts),
-                    reinterpret_cast<uint32_t*>(db + o_off), reinterpret_cast<uint32_t*>(db + o_len)};
+                    reinterpret_cast<uint32_t*>(db + o_off), reinterpret_cast<uint32_t*>(db + o_len), nullptr};
+    if (parse) {  // sequence_number of the flagged TopicMessages, in the decode launch; 0 elsewhere
+        out.seq = reinterpret_cast<uint64_t*>(db + o_seq);
+        hip_check(hipMemsetAsync(out.seq, 0, 8 * n, c.stream), "memset");
+    }
     if (sbe_decode_batch(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, mode, &out, c.stream) != SBE_OK)
         fail("sbe_decode_batch");
-    if (parse) {  // sequence_number of the flagged TopicMessages; 0 elsewhere
-        hip_check(hipMemsetAsync(db + o_seq, 0, 8 * n, c.stream), "memset");
-        if (sbe_eval_sequence_numbers(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, &out,
-                                      reinterpret_cast<uint64_t*>(db + o_seq), c.stream) != SBE_OK)
-            fail("sbe_eval_sequence_numbers");
-    }
     hip_check(hipMemcpyAsync(c.h_dec.p, c.d_dec.p, dbytes, hipMemcpyDeviceToHost, c.stream), "D2H");
     hip_check(hipStreamSynchronize(c.stream), "sync");
     const uint8_t* hb = static_cast<const uint8_t*>(c.h_dec.p);

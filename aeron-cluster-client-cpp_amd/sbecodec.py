@@ -66,7 +66,8 @@ class _LiteBatch(ctypes.Structure):
 
 class _Decoded(ctypes.Structure):
     _fields_ = [("status", ctypes.c_void_p), ("flags", ctypes.c_void_p), ("hdr", ctypes.c_void_p),
-                ("ts", ctypes.c_void_p), ("view_off", ctypes.c_void_p), ("view_len", ctypes.c_void_p)]
+                ("ts", ctypes.c_void_p), ("view_off", ctypes.c_void_p), ("view_len", ctypes.c_void_p),
+                ("seq", ctypes.c_void_p)]
 
 
 def _load():
@@ -321,6 +322,7 @@ class Decoded:
     ts: torch.Tensor        # int64 [n]    (u64)
     view_off: torch.Tensor  # int32 [n,5]  (u32, relative to the record start)
     view_len: torch.Tensor  # int32 [n,5]  (u32)
+    seq: torch.Tensor | None = None  # int64 [n] (u64): sequence_number of flagged records (parse mode)
 
     def numpy(self):
         import numpy as np
@@ -339,18 +341,30 @@ def alloc_decoded(n: int, device) -> Decoded:
                    torch.empty((m, 5), dtype=torch.int32, device=device))
 
 
-def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = None, stream=None) -> Decoded:
-    """Batch decode of the records data[rec_off[i]:rec_off[i+1]] (rec_off int64 [n+1])."""
+def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = None, stream=None,
+                 seq=None) -> Decoded:
+    """Batch decode of the records data[rec_off[i]:rec_off[i+1]] (rec_off int64 [n+1]).
+    Parse mode with seq (int64 [n]): the same launch writes ParseResult.sequence_number of the
+    records flagged FL_SEQ_KEY / FL_SEQ_ESC (others are not written; seq=True allocates it zeroed)."""
     data = _dev(data, torch.uint8, "data")
     rec_off = _dev(rec_off, torch.int64, "rec_off")
     n = int(rec_off.numel()) - 1
     if out is None:
         out = alloc_decoded(n, data.device)
-    d = _Decoded(*(getattr(out, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
+    if seq is True:
+        seq = torch.zeros(max(n, 1), dtype=torch.int64, device=data.device)
+    if seq is not None:
+        seq = _dev(seq, torch.int64, "seq")
+    d = _Decoded(*(getattr(out, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")),
+                 None if seq is None else seq.data_ptr())
     rc = lib().sbe_decode_batch(_ptr(data), _ptr(rec_off), n, mode, ctypes.byref(d), _stream(stream))
     _check(rc, "sbe_decode_batch")
+    keys = ("status", "flags", "hdr", "ts", "view_off", "view_len")
     if n < out.status.numel():
-        out = Decoded(*(getattr(out, k)[:n] for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
+        out = Decoded(*(getattr(out, k)[:n] for k in keys))
+    else:
+        out = Decoded(*(getattr(out, k) for k in keys))
+    out.seq = None if seq is None else seq[:n]
     return out
 
 

@@ -3,9 +3,9 @@
 One step = one round trip of the hot path over one batch resident in HBM:
   sbe_encode_topic_batch (wire-correct TopicMessages, packed SoA input → packed stream + offsets)
   → sbe_decode_batch(PARSE_MESSAGE) (stream + offsets → per-record descriptors)
-  → sbe_eval_sequence_numbers (ParseResult.sequence_number of the flagged records; this workload's
-    payloads carry no "_sequence_number" and no escapes, as the Order JSON of the reference has
-    none, so the launch reads the flags and writes nothing).
+    with ParseResult.sequence_number evaluated in the same launch for flagged records (this
+    workload's payloads carry no "_sequence_number" and no escapes, as the Order JSON of the
+    reference has none, so nothing is evaluated; --separate-seq uses the standalone launch).
 Workload (BASELINE.json configs[1] extended to the metric's encode+decode): 1,000,000 fixed-256 B
 Order TopicMessages per GPU (seed 0x5EED0002 + rank), synthetic.
 
@@ -50,6 +50,8 @@ def parse_args():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--separate-seq", action="store_true",
+                   help="sequence_number evaluation as its own launch (sbe_eval_sequence_numbers)")
     p.add_argument("--gather", action="store_true", help="also time the RCCL gather of encoded shards")
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
     p.add_argument("--event-every", type=int, default=4,
@@ -159,8 +161,11 @@ def main():
         if k is not None:
             ev_enc[k][1].record(stream)
             ev_dec[k][0].record(stream)
-        sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream)
-        sbecodec.eval_sequence_numbers(out, out_off, dec, seq=seq, stream=stream)
+        if args.separate_seq:
+            sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream)
+            sbecodec.eval_sequence_numbers(out, out_off, dec, seq=seq, stream=stream)
+        else:
+            sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream, seq=seq)
         if k is not None:
             ev_dec[k][1].record(stream)
 

@@ -237,6 +237,9 @@ typedef struct sbe_decoded {
     uint64_t* ts;
     uint32_t* view_off;
     uint32_t* view_len;
+    uint64_t* seq; /* optional (NULL: skip), parse mode only: seq[i] = ParseResult.sequence_number of
+                      every TopicMessage flagged SBE_FL_SEQ_KEY / SBE_FL_SEQ_ESC, evaluated in the same
+                      launch (see sbe_eval_sequence_numbers); other entries are not written (8-B aligned) */
 } sbe_decoded;
 
 /* Decode n records; record i is in[rec_off[i] .. rec_off[i+1]) (rec_off: [n+1] device u64).
@@ -245,7 +248,8 @@ typedef struct sbe_decoded {
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream);
 
-/* ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125): for every record that
+/* ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125) as a separate launch, for
+ * descriptors decoded with seq == NULL: for every record that
  * sbe_decode_batch(SBE_DEC_PARSE_MESSAGE) left with status SBE_ST_TM and flag SBE_FL_SEQ_KEY or
  * SBE_FL_SEQ_ESC, parse its payload with the semantics of jsoncpp 1.9.5's CharReaderBuilder
  * defaults (comments and trailing commas allowed, extra content after the root ignored, stack

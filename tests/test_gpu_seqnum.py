@@ -72,15 +72,16 @@ def run(codec, recs, lead):
     exp_seq = T.oracle_seq_batch(data, off, exp)
     d = to_dev(data, torch.uint8)
     ro = to_dev(np.asarray(off, np.uint64), torch.int64)
-    dec = codec.decode_batch(d, ro, mode=codec.DEC_PARSE_MESSAGE)
-    seq = codec.eval_sequence_numbers(d, ro, dec)
+    dec = codec.decode_batch(d, ro, mode=codec.DEC_PARSE_MESSAGE, seq=True)  # evaluated in the decode launch
+    seq = codec.eval_sequence_numbers(d, ro, dec)                           # the standalone launch
     torch.cuda.synchronize()
     got = dec.numpy()
     assert_same_decode(got, exp)
-    got_seq = seq.cpu().numpy().view(np.uint64)
-    bad = np.nonzero(got_seq != exp_seq)[0]
-    assert bad.size == 0, [(int(i), data[int(off[i]):int(off[i + 1])].tobytes()[:200], int(got_seq[i]), int(exp_seq[i]))
-                           for i in bad[:5]]
+    for s in (dec.seq, seq):
+        got_seq = s.cpu().numpy().view(np.uint64)
+        bad = np.nonzero(got_seq != exp_seq)[0]
+        assert bad.size == 0, [(int(i), data[int(off[i]):int(off[i + 1])].tobytes()[:200], int(got_seq[i]),
+                                int(exp_seq[i])) for i in bad[:5]]
     return exp, exp_seq
 
 
@@ -128,8 +129,9 @@ def test_seq_bench_workload_has_no_candidates(codec):
     assert not (exp["flags"] & (T.FL_SEQ_KEY | T.FL_SEQ_ESC)).any()
     d = to_dev(eo, torch.uint8)
     ro = to_dev(np.asarray(eoff, np.uint64), torch.int64)
-    dec = codec.decode_batch(d, ro, mode=codec.DEC_PARSE_MESSAGE)
+    seq1 = torch.full((20000,), 77, dtype=torch.int64, device="cuda")
+    dec = codec.decode_batch(d, ro, mode=codec.DEC_PARSE_MESSAGE, seq=seq1)
     seq = torch.full((20000,), 77, dtype=torch.int64, device="cuda")
     codec.eval_sequence_numbers(d, ro, dec, seq=seq)
     torch.cuda.synchronize()
-    assert bool((seq == 77).all())
+    assert bool((seq == 77).all()) and bool((seq1 == 77).all())
