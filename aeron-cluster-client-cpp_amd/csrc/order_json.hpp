@@ -1,0 +1,549 @@
+// order_json.hpp — Order JSON text on the GPU (included by sbe_codec.hip).
+//
+// Replaces Order::to_json (src/order_types.cpp:122-181) and the headers JSON publish_order builds
+// (src/cluster_client.cpp:308-323): jsoncpp StreamWriterBuilder with indentation "" (compact,
+// colon ":", object members in std::map order), so the text is a fixed skeleton with eight
+// variable slots — escaped strings, two decimal integers and the quantity printed twice, once by
+// jsoncpp valueToString ("%.17g", ".0" appended when there is no '.' or 'e') and once by
+// std::to_string ("%f").  Both number formats follow glibc printf on the EXACT binary value
+// (round half to even on the exact decimal expansion), so the formatter below expands the double
+// exactly: the integer part as base-1e9 limbs, the fraction F / 2^k as a multiword numerator that
+// yields nine digits per multiply.  Values with short binary fractions (prices, quantities) touch
+// one or two words; the full range (subnormals, 1e308) takes more words, never a different path.
+//
+// One lane per Order; a sizing launch (text length + packed-arena string total), two device scans,
+// then the writing launch.  The text is written through an 8-byte store buffer per lane.
+#pragma once
+
+namespace oj {
+
+constexpr uint32_t kFields = SBE_ORDER_FIELDS;
+constexpr uint32_t kBlock = 256;
+
+struct JsonArgs {
+    const uint8_t* arena;
+    const uint32_t* str_off;
+    const uint32_t* str_len;
+    const int64_t* customer_id;
+    const int64_t* timestamp;
+    const double* quantity;
+    uint64_t n;
+    uint32_t what;
+    uint8_t* out;
+    uint64_t cap;
+    uint64_t* out_off;  // n + 1 text offsets (scan of sz)
+    uint8_t* status;
+    uint64_t* sz;       // n + 1 text lengths (sz[n] = 0)
+    uint64_t* str_tot;  // n + 1 packed-arena string totals (str_tot[n] = 0)
+    uint64_t* str_base; // n + 1 their scan
+};
+
+// ---- byte sinks: counting (sizing launch) and writing (8-byte buffered, byte-exact edges) ----
+struct CountSink {
+    uint64_t n = 0;
+    __device__ void put(uint8_t) { ++n; }
+    __device__ void flush() {}
+};
+
+struct WriteSink {
+    uint8_t* p;     // record start
+    uint64_t n = 0; // bytes produced
+    uint64_t buf = 0;
+    uint32_t fill = 0;  // bytes in buf
+    __device__ explicit WriteSink(uint8_t* q) : p(q) {}
+    __device__ void put(uint8_t b) {
+        buf |= (uint64_t)b << (8 * fill);
+        ++fill;
+        ++n;
+        if (fill == 8 || (((uintptr_t)(p + n)) & 7) == 0) drain();
+    }
+    __device__ void drain() {
+        uint8_t* d = p + n - fill;
+        if (fill == 8 && (((uintptr_t)d) & 7) == 0) {
+            *reinterpret_cast<uint64_t*>(d) = buf;
+        } else {
+            for (uint32_t i = 0; i < fill; ++i) d[i] = (uint8_t)(buf >> (8 * i));
+        }
+        buf = 0;
+        fill = 0;
+    }
+    __device__ void flush() {
+        if (fill) drain();
+    }
+};
+
+template <class S>
+__device__ inline void lit(S& s, const char* t) {
+    while (*t) s.put((uint8_t)*t++);
+}
+
+// jsoncpp json_writer.cpp utf8ToCodepoint (lead byte decides the length; continuation bytes are
+// not checked; truncated / overlong / surrogate → U+FFFD; a truncated sequence consumes 1 byte).
+__device__ inline uint32_t utf8_cp(const uint8_t* s, uint64_t left, uint32_t& used) {
+    const uint32_t b = s[0];
+    used = 1;
+    if (b < 0x80) return b;
+    if (b < 0xE0) {
+        if (left < 2) return 0xFFFD;
+        const uint32_t c = ((b & 0x1F) << 6) | (s[1] & 0x3F);
+        used = 2;
+        return c < 0x80 ? 0xFFFD : c;
+    }
+    if (b < 0xF0) {
+        if (left < 3) return 0xFFFD;
+        const uint32_t c = ((b & 0x0F) << 12) | ((uint32_t)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+        used = 3;
+        if (c >= 0xD800 && c <= 0xDFFF) return 0xFFFD;
+        return c < 0x800 ? 0xFFFD : c;
+    }
+    if (b < 0xF8) {
+        if (left < 4) return 0xFFFD;
+        const uint32_t c = ((b & 0x07) << 18) | ((uint32_t)(s[1] & 0x3F) << 12) | ((uint32_t)(s[2] & 0x3F) << 6) |
+                           (s[3] & 0x3F);
+        used = 4;
+        return c < 0x10000 ? 0xFFFD : c;
+    }
+    return 0xFFFD;
+}
+
+template <class S>
+__device__ inline void hex4(S& s, uint32_t v) {
+    const char* hx = "0123456789abcdef";
+    s.put('\\');
+    s.put('u');
+    s.put((uint8_t)hx[(v >> 12) & 15]);
+    s.put((uint8_t)hx[(v >> 8) & 15]);
+    s.put((uint8_t)hx[(v >> 4) & 15]);
+    s.put((uint8_t)hx[v & 15]);
+}
+
+// jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
+template <class S>
+__device__ void quoted(S& s, const uint8_t* p, uint64_t len) {
+    s.put('"');
+    uint64_t i = 0;
+    while (i < len) {
+        const uint8_t c = p[i];
+        if (c >= 0x20 && c < 0x80 && c != '"' && c != '\\') {  // the common case
+            s.put(c);
+            ++i;
+            continue;
+        }
+        switch (c) {
+            case '"': s.put('\\'); s.put('"'); ++i; continue;
+            case '\\': s.put('\\'); s.put('\\'); ++i; continue;
+            case '\b': s.put('\\'); s.put('b'); ++i; continue;
+            case '\f': s.put('\\'); s.put('f'); ++i; continue;
+            case '\n': s.put('\\'); s.put('n'); ++i; continue;
+            case '\r': s.put('\\'); s.put('r'); ++i; continue;
+            case '\t': s.put('\\'); s.put('t'); ++i; continue;
+            default: break;
+        }
+        uint32_t used;
+        uint32_t cp = utf8_cp(p + i, len - i, used);
+        i += used;
+        if (cp < 0x10000) {
+            hex4(s, cp);
+        } else {
+            cp -= 0x10000;
+            hex4(s, 0xD800 + ((cp >> 10) & 0x3FF));
+            hex4(s, 0xDC00 + (cp & 0x3FF));
+        }
+    }
+    s.put('"');
+}
+
+template <class S>
+__device__ inline void key(S& s, const char* k) {
+    s.put('"');
+    lit(s, k);
+    s.put('"');
+    s.put(':');
+}
+
+template <class S>
+__device__ void dec_u64(S& s, uint64_t v) {
+    char b[20];
+    int n = 0;
+    do {
+        b[n++] = (char)('0' + v % 10);
+        v /= 10;
+    } while (v);
+    while (n) s.put((uint8_t)b[--n]);
+}
+
+template <class S>
+__device__ void dec_i64(S& s, int64_t v) {  // "%ld"
+    if (v < 0) {
+        s.put('-');
+        dec_u64(s, 0ull - (uint64_t)v);
+    } else {
+        dec_u64(s, (uint64_t)v);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Exact decimal expansion of a finite, non-zero |v| = I + F / 2^k.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kE9 = 1000000000u;
+
+struct Exact {
+    uint32_t lim[36];  // integer part, base-1e9 limbs, most significant first
+    int nl;            // 0 when I == 0
+    uint32_t fw[35];   // fraction numerator, little-endian words (k bits)
+    int nfw, k;
+
+    __device__ void init(double v) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(v) & ~(1ull << 63);
+        const uint32_t ex = (uint32_t)(bits >> 52);
+        uint64_t m = bits & ((1ull << 52) - 1);
+        int e;
+        if (ex == 0) e = -1074;
+        else m |= 1ull << 52, e = (int)ex - 1075;
+        const int t = __builtin_ctzll(m);
+        m >>= t;
+        e += t;
+        nl = 0;
+        nfw = 0;
+        k = 0;
+        if (e < 0) {
+            k = -e;
+            const uint64_t ip = k >= 64 ? 0 : (m >> k);
+            const uint64_t fp = k >= 64 ? m : (m & ((1ull << k) - 1));
+            int_from_u64(ip);
+            nfw = (k + 31) / 32;
+            for (int j = 0; j < nfw; ++j) fw[j] = 0;
+            fw[0] = (uint32_t)fp;
+            if (nfw > 1) fw[1] = (uint32_t)(fp >> 32);
+        } else if (e <= 10) {
+            int_from_u64(m << e);  // m < 2^53
+        } else {
+            // I = m << e as a little-endian word array, then repeated division by 1e9
+            uint32_t w[34];
+            const int nw = (53 + e + 31) / 32;
+            for (int j = 0; j < nw; ++j) w[j] = 0;
+            const int ws = e / 32, bs = e % 32;
+            const unsigned __int128 sh = (unsigned __int128)m << bs;
+            w[ws] = (uint32_t)sh;
+            if (ws + 1 < nw) w[ws + 1] = (uint32_t)(sh >> 32);
+            if (ws + 2 < nw) w[ws + 2] = (uint32_t)(sh >> 64);
+            int top = nw;
+            uint32_t rev[36];
+            int nr = 0;
+            while (top > 0) {
+                uint64_t r = 0;
+                for (int j = top - 1; j >= 0; --j) {
+                    const uint64_t cur = (r << 32) | w[j];
+                    w[j] = (uint32_t)(cur / kE9);
+                    r = cur % kE9;
+                }
+                rev[nr++] = (uint32_t)r;
+                while (top > 0 && w[top - 1] == 0) --top;
+            }
+            nl = nr;
+            for (int j = 0; j < nr; ++j) lim[j] = rev[nr - 1 - j];
+        }
+    }
+
+    __device__ void int_from_u64(uint64_t ip) {
+        nl = 0;
+        if (ip == 0) return;
+        uint32_t r[3];
+        int c = 0;
+        while (ip) {
+            r[c++] = (uint32_t)(ip % kE9);
+            ip /= kE9;
+        }
+        nl = c;
+        for (int j = 0; j < c; ++j) lim[j] = r[c - 1 - j];
+    }
+
+    __device__ bool frac_nonzero() const {
+        uint32_t o = 0;
+        for (int j = 0; j < nfw; ++j) o |= fw[j];
+        return o != 0;
+    }
+
+    // The next nine fraction digits, as an integer < 1e9 (F ← F·1e9 mod 2^k).
+    __device__ uint32_t frac_next9() {
+        if (nfw == 0) return 0;
+        uint64_t carry = 0;
+        for (int j = 0; j < nfw; ++j) {
+            const uint64_t t = (uint64_t)fw[j] * kE9 + carry;
+            fw[j] = (uint32_t)t;
+            carry = t >> 32;
+        }
+        const int kb = k & 31;
+        if (kb == 0) return (uint32_t)carry;
+        const uint32_t top = fw[nfw - 1];
+        fw[nfw - 1] = top & ((1u << kb) - 1);
+        return (uint32_t)((carry << (32 - kb)) | (top >> kb));
+    }
+};
+
+__device__ inline int ndig9(uint32_t v) {  // decimal digits of 0 < v < 1e9
+    int d = 1;
+    while (v >= 10) v /= 10, ++d;
+    return d;
+}
+
+__device__ inline uint32_t pow10u(int p) {
+    uint32_t r = 1;
+    while (p-- > 0) r *= 10;
+    return r;
+}
+
+// "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
+// round half to even on the exact value; inf / nan as glibc prints them.
+template <class S>
+__device__ void fmt_fixed6(S& s, double v) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const bool neg = (bits >> 63) != 0;
+    if (__builtin_isnan(v)) {
+        if (neg) s.put('-');
+        lit(s, "nan");
+        return;
+    }
+    if (neg) s.put('-');
+    if (__builtin_isinf(v)) {
+        lit(s, "inf");
+        return;
+    }
+    if ((bits << 1) == 0) {
+        lit(s, "0.000000");
+        return;
+    }
+    Exact x;
+    x.init(v);
+    const uint32_t c1 = x.frac_next9();
+    uint32_t kept = c1 / 1000;
+    const uint32_t rest = c1 % 1000;
+    const bool up = rest > 500 || (rest == 500 && (x.frac_nonzero() || (kept & 1)));
+    bool carry = false;
+    if (up && ++kept == 1000000) kept = 0, carry = true;
+    if (carry) {  // add one to the integer limbs
+        int j = x.nl - 1;
+        for (; j >= 0; --j) {
+            if (++x.lim[j] < kE9) break;
+            x.lim[j] = 0;
+        }
+        if (j < 0) {  // all limbs overflowed (or there were none): a new leading limb 1
+            for (int q = x.nl; q > 0; --q) x.lim[q] = x.lim[q - 1];
+            x.lim[0] = 1;
+            ++x.nl;
+        }
+    }
+    if (x.nl == 0) {
+        s.put('0');
+    } else {
+        dec_u64(s, x.lim[0]);
+        for (int j = 1; j < x.nl; ++j)
+            for (uint32_t p = 100000000u; p; p /= 10) s.put((uint8_t)('0' + (x.lim[j] / p) % 10));
+    }
+    s.put('.');
+    for (uint32_t p = 100000u; p; p /= 10) s.put((uint8_t)('0' + (kept / p) % 10));
+}
+
+// jsoncpp valueToString(double, false, 17, significantDigits): "%.17g" then ".0" when the text
+// has neither '.' nor 'e'; NaN → null, ±inf → ±1e+9999.
+template <class S>
+__device__ void fmt_g17(S& s, double v) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    if (__builtin_isnan(v)) {
+        lit(s, "null");
+        return;
+    }
+    const bool neg = (bits >> 63) != 0;
+    if (__builtin_isinf(v)) {
+        lit(s, neg ? "-1e+9999" : "1e+9999");
+        return;
+    }
+    if (neg) s.put('-');
+    if ((bits << 1) == 0) {
+        lit(s, "0.0");
+        return;
+    }
+    Exact x;
+    x.init(v);
+    // first 18 significant digits of the expansion, the decimal exponent X of the first, sticky
+    uint8_t d[18];
+    int cnt = 0, X = 0;
+    bool sticky = false;
+    auto take = [&](uint32_t chunk, int width) {  // `width` digits of chunk, most significant first
+        for (int q = width - 1; q >= 0; --q) {
+            const uint32_t dg = (chunk / pow10u(q)) % 10;
+            if (cnt < 18) d[cnt++] = (uint8_t)dg;
+            else if (dg) sticky = true;
+        }
+    };
+    if (x.nl) {
+        const int w0 = ndig9(x.lim[0]);
+        X = w0 - 1 + 9 * (x.nl - 1);
+        take(x.lim[0], w0);
+        for (int j = 1; j < x.nl; ++j) take(x.lim[j], 9);
+    } else {
+        X = -1;
+        uint32_t c;
+        while ((c = x.frac_next9()) == 0) X -= 9;
+        const int w0 = ndig9(c);
+        X -= 9 - w0;
+        take(c, w0);
+    }
+    while (cnt < 18 && x.frac_nonzero()) take(x.frac_next9(), 9);
+    while (cnt < 18) d[cnt++] = 0;
+    if (x.frac_nonzero()) sticky = true;
+    // round to 17 digits, half to even
+    const bool up = d[17] > 5 || (d[17] == 5 && (sticky || (d[16] & 1)));
+    if (up) {
+        int j = 16;
+        for (; j >= 0; --j) {
+            if (++d[j] < 10) break;
+            d[j] = 0;
+        }
+        if (j < 0) d[0] = 1, ++X;  // 99..9 → 10..0
+    }
+    int last = 16;  // trailing zeros are dropped (%g without '#')
+    while (last > 0 && d[last] == 0) --last;
+    if (X < -4 || X >= 17) {
+        s.put((uint8_t)('0' + d[0]));
+        if (last > 0) {
+            s.put('.');
+            for (int j = 1; j <= last; ++j) s.put((uint8_t)('0' + d[j]));
+        }
+        s.put('e');
+        int ax = X;
+        if (ax < 0) s.put('-'), ax = -ax;
+        else s.put('+');
+        if (ax < 10) s.put('0');
+        dec_u64(s, (uint64_t)ax);
+        return;  // has an 'e': no ".0"
+    }
+    if (X >= 0) {
+        for (int j = 0; j <= X; ++j) s.put((uint8_t)('0' + d[j]));
+        if (last > X) {
+            s.put('.');
+            for (int j = X + 1; j <= last; ++j) s.put((uint8_t)('0' + d[j]));
+        } else {
+            lit(s, ".0");
+        }
+    } else {
+        s.put('0');
+        s.put('.');
+        for (int j = 0; j < -X - 1; ++j) s.put('0');
+        for (int j = 0; j <= last; ++j) s.put((uint8_t)('0' + d[j]));
+    }
+}
+
+__device__ inline bool eq_lit(const uint8_t* p, uint64_t n, const char* t) {
+    uint64_t i = 0;
+    for (; t[i]; ++i)
+        if (i >= n || p[i] != (uint8_t)t[i]) return false;
+    return i == n;
+}
+
+// One Order's text (src/order_types.cpp:122-181, src/cluster_client.cpp:308-323).
+template <class S>
+__device__ void order_text(S& s, const JsonArgs& a, uint64_t i, const uint8_t* const f[kFields],
+                           const uint32_t l[kFields]) {
+    if (a.what == SBE_JSON_PUBLISH_HEADERS) {
+        const bool upd = eq_lit(f[7], l[7], "UPDATED") || eq_lit(f[7], l[7], "CANCELLED");
+        lit(s, "{\"messageId\":");
+        quoted(s, f[6], l[6]);
+        lit(s, upd ? ",\"messageType\":\"UPDATE_ORDER\",\"orderId\":" : ",\"messageType\":\"CREATE_ORDER\",\"orderId\":");
+        quoted(s, f[5], l[5]);
+        s.put('}');
+        return;
+    }
+    const double q = a.quantity[i];
+    uint32_t id_len = l[1];  // headers["origin_id"] = identifier.c_str()
+    for (uint32_t j = 0; j < id_len; ++j)
+        if (f[1][j] == 0) {
+            id_len = j;
+            break;
+        }
+    lit(s, "{\"message\":{\"headers\":{\"auth_token\":\"Bearer xxx\",\"connection_uuid\":\"130032\",\"create_ts\":\"");
+    dec_i64(s, a.timestamp[i] / 1000000);
+    lit(s, "\",\"customer_id\":\"");
+    dec_i64(s, a.customer_id[i]);
+    lit(s, "\",\"ip_address\":\"10.37.62.251\",\"origin\":\"fix\",\"origin_id\":");
+    quoted(s, f[1], id_len);
+    lit(s, ",\"origin_name\":\"FIX_GATEWAY\"},\"message\":{\"action\":\"CREATE\",\"order_details\":{\"client_order_id\":");
+    quoted(s, f[0], l[0]);
+    lit(s, ",\"order_type\":\"market\",\"quantity\":{\"token\":");
+    quoted(s, f[2], l[2]);
+    lit(s, ",\"value\":");
+    fmt_g17(s, q);
+    lit(s, "},\"quantity_value_str\":\"");
+    fmt_fixed6(s, q);
+    lit(s, "\",\"side\":");
+    quoted(s, f[4], l[4]);
+    lit(s, ",\"token_pair\":{\"base_token\":");
+    quoted(s, f[2], l[2]);
+    lit(s, ",\"quote_token\":");
+    quoted(s, f[3], l[3]);
+    lit(s, "}}}},\"msg_type\":\"D\",\"uuid\":");
+    quoted(s, f[0], l[0]);
+    s.put('}');
+}
+
+__device__ inline void fields_of(const JsonArgs& a, uint64_t i, uint64_t base, const uint8_t* f[kFields],
+                                 uint32_t l[kFields]) {
+    for (uint32_t j = 0; j < kFields; ++j) {
+        l[j] = a.str_len[kFields * i + j];
+        if (a.str_off) {
+            f[j] = a.arena + a.str_off[kFields * i + j];
+        } else {
+            f[j] = a.arena + base;
+            base += l[j];
+        }
+    }
+}
+
+// Packed arena: each record's string total (scan → its base).
+__global__ __launch_bounds__(kBlock) void order_json_totals(JsonArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i > a.n) return;
+    uint64_t t = 0;
+    if (i < a.n)
+        for (uint32_t j = 0; j < kFields; ++j) t += a.str_len[kFields * i + j];
+    a.str_tot[i] = t;
+}
+
+// Sizing launch: the text length of record i into sz[i] (sz[n] = 0).
+__global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i > a.n) return;
+    if (i == a.n) {
+        a.sz[i] = 0;
+        return;
+    }
+    const uint8_t* f[kFields];
+    uint32_t l[kFields];
+    fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
+    CountSink c;
+    order_text(c, a, i, f, l);
+    a.sz[i] = c.n;
+}
+
+__global__ __launch_bounds__(kBlock) void order_json_write(JsonArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t o = a.out_off[i], e = a.out_off[i + 1];
+    const bool fits = e <= a.cap;
+    if (a.status) a.status[i] = fits ? SBE_JSON_OK : SBE_JSON_OVERFLOW;
+    if (!fits) return;
+    const uint8_t* f[kFields];
+    uint32_t l[kFields];
+    fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
+    WriteSink w(a.out + o);
+    order_text(w, a, i, f, l);
+    w.flush();
+}
+
+inline size_t scan_temp(uint64_t n) {
+    size_t t = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (uint64_t*)nullptr, (uint64_t*)nullptr, n + 1, nullptr);
+    return t + 256;
+}
+
+}  // namespace oj

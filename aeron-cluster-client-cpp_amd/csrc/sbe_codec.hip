@@ -1245,6 +1245,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
 }
 
 #include "seqnum.hpp"
+#include "order_json.hpp"
 
 // ------------------------------------------------------------------------------------------
 // Decode
@@ -2504,6 +2505,49 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     if (e != hipSuccess) return record_hip(e);
     const uint64_t cb = (n + 1 + 4 * kFragGroup - 1) / (4 * kFragGroup);  // four waves per block
     hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < 4096 ? cb : 4096)), dim3(256), 0, s, a);
+    return record_hip(hipGetLastError());
+}
+
+size_t sbe_order_json_workspace_size(uint64_t n) {
+    return (size_t)(3 * 8 * (n + 1) + 4 * 16) + oj::scan_temp(n);
+}
+
+int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what, uint8_t* out,
+                            uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!in || !out_off || what > SBE_JSON_PUBLISH_HEADERS) return SBE_EINVAL;
+    if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, 8, s));
+    if (!in->arena || !in->str_len || !in->customer_id || !in->timestamp || !in->quantity || !workspace)
+        return SBE_EINVAL;
+    if (n >= (1ull << 40)) return SBE_EINVAL;
+    if (workspace_bytes < sbe_order_json_workspace_size(n)) return SBE_ENOSPC;
+    if (!out && out_capacity) return SBE_EINVAL;
+    auto al = [](uintptr_t x) { return (x + 15) & ~(uintptr_t)15; };
+    uintptr_t w = al(reinterpret_cast<uintptr_t>(workspace));
+    uint64_t* sz = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    uint64_t* tot = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    uint64_t* base = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * (n + 1));
+    void* tmp = reinterpret_cast<void*>(w);
+    size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
+    oj::JsonArgs a{in->arena, in->str_off, in->str_len, in->customer_id, in->timestamp, in->quantity, n, what,
+                   out,       out_capacity, out_off,    status,          sz,             tot,           base};
+    const uint32_t blocks = (uint32_t)((n + 1 + oj::kBlock - 1) / oj::kBlock);
+    hipError_t e = hipSuccess;
+    if (!in->str_off) {
+        hipLaunchKernelGGL(oj::order_json_totals, dim3(blocks), dim3(oj::kBlock), 0, s, a);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tot, base, n + 1, s);
+        if (e != hipSuccess) return record_hip(e);
+    }
+    hipLaunchKernelGGL(oj::order_json_measure, dim3(blocks), dim3(oj::kBlock), 0, s, a);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sz, out_off, n + 1, s);
+    if (e != hipSuccess) return record_hip(e);
+    hipLaunchKernelGGL(oj::order_json_write, dim3(blocks), dim3(oj::kBlock), 0, s, a);
     return record_hip(hipGetLastError());
 }
 

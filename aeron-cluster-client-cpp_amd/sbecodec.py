@@ -15,6 +15,8 @@ Reference surface mirrored (paths relative to the reference tree):
   decode_batch(PARSE) ~ MessageParser::parse_message        src/sbe_encoder.cpp:513-551
   decode_batch(EGRESS)~ decode_ack + MessageHandler::on_egress
                         src/ack_decoder.cpp:29-105, include/aeron_cluster/message_handler.hpp:35-68
+  order_to_json_batch ~ Order::to_json src/order_types.cpp:122-181 and publish_order's headers JSON
+                        src/cluster_client.cpp:308-323
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 3
+ABI_VERSION = 4
 ENC_REF_TRUNCATE8 = 0x1
 ENC_OK, ENC_OVERFLOW = 0, 6
 DEC_PARSE_MESSAGE, DEC_ON_EGRESS, DEC_LITE = 0, 1, 2
@@ -38,6 +40,9 @@ COMMIT_OFFSET_LITE, ORDER_REQUEST_LITE, ORDER_NOTIFICATION_LITE = 301, 201, 202
 LITE_FIELDS = {COMMIT_OFFSET_LITE: 2, ORDER_REQUEST_LITE: 3, ORDER_NOTIFICATION_LITE: 3}
 ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
 FRAG_BEGIN, FRAG_END = 0x80, 0x40
+ORDER_FIELDS = 8  # client_order_uuid, identifier, base_token, quote_token, side, id, message_id, status
+JSON_ORDER_PAYLOAD, JSON_PUBLISH_HEADERS = 0, 1
+JSON_OK, JSON_OVERFLOW = 0, 6
 
 ST_TM, ST_ACK, ST_SESSION_EVENT = 0, 1, 2
 ST_ERR_NULL_EMPTY, ST_ERR_HEADER, ST_ERR_UNKNOWN_TYPE = 16, 17, 18
@@ -62,6 +67,11 @@ class _TmBatch(ctypes.Structure):
 class _LiteBatch(ctypes.Structure):
     _fields_ = [("arena", ctypes.c_void_p), ("str_off", ctypes.c_void_p), ("str_len", ctypes.c_void_p),
                 ("topic_id", ctypes.c_void_p), ("sequence", ctypes.c_void_p)]
+
+
+class _OrderBatch(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("str_off", ctypes.c_void_p), ("str_len", ctypes.c_void_p),
+                ("customer_id", ctypes.c_void_p), ("timestamp", ctypes.c_void_p), ("quantity", ctypes.c_void_p)]
 
 
 class _Decoded(ctypes.Structure):
@@ -118,6 +128,12 @@ def _load():
     lib.sbe_eval_sequence_numbers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(_Decoded), ctypes.c_void_p, ctypes.c_void_p]
     lib.sbe_profile_enable.restype = ctypes.c_int
+    lib.sbe_order_json_workspace_size.argtypes = [ctypes.c_uint64]
+    lib.sbe_order_json_workspace_size.restype = ctypes.c_size_t
+    lib.sbe_order_to_json_batch.argtypes = [ctypes.POINTER(_OrderBatch), ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.sbe_order_to_json_batch.restype = ctypes.c_int
     lib.sbe_profile_enable.argtypes = [ctypes.c_int]
     lib.sbe_profile_read.restype = ctypes.c_int
     lib.sbe_profile_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
@@ -412,3 +428,51 @@ def reassemble(data, frag_off, flags, out=None, msg_off=None, workspace=None, st
                                         _ptr(counts), _ptr(workspace), workspace.numel(), _stream(stream))
     _check(rc, "sbe_reassemble_fragments")
     return Reassembled(out, msg_off, counts)
+
+
+@dataclass
+class OrderJson:
+    out: torch.Tensor      # u8 text, record i = out[out_off[i]:out_off[i+1]]
+    out_off: torch.Tensor  # i64 [n+1]
+    status: torch.Tensor   # u8 [n]
+
+
+def order_json_workspace_size(n: int) -> int:
+    return int(lib().sbe_order_json_workspace_size(n))
+
+
+def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=JSON_ORDER_PAYLOAD,
+                        str_off=None, out=None, out_capacity=None, out_off=None, status=None, workspace=None,
+                        stream=None) -> OrderJson:
+    """Order::to_json (what=JSON_ORDER_PAYLOAD) or publish_order's headers JSON
+    (what=JSON_PUBLISH_HEADERS) of n Orders, str_len [n][8] (ORDER_FIELDS order)."""
+    arena = _dev(arena, torch.uint8, "arena")
+    str_len = _dev(str_len, torch.int32, "str_len")
+    customer_id = _dev(customer_id, torch.int64, "customer_id")
+    timestamp = _dev(timestamp, torch.int64, "timestamp")
+    quantity = _dev(quantity, torch.float64, "quantity")
+    n = int(customer_id.numel())
+    if str_len.numel() != ORDER_FIELDS * n or timestamp.numel() != n or quantity.numel() != n:
+        raise SbeError("order batch arrays disagree on n")
+    if str_off is not None:
+        str_off = _dev(str_off, torch.int32, "str_off")
+        if str_off.numel() != ORDER_FIELDS * n:
+            raise SbeError("str_off must be [n][8]")
+    dev = arena.device
+    if out is None:
+        cap = out_capacity if out_capacity is not None else 600 * n + 6 * 3 * int(arena.numel()) + 64
+        out = torch.empty(max(int(cap), 16), dtype=torch.uint8, device=dev)
+    cap = int(out.numel()) if out_capacity is None else int(out_capacity)
+    if out_off is None:
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    need = order_json_workspace_size(n)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
+    b = _OrderBatch(_ptr(arena), _ptr(str_off) if str_off is not None else None, _ptr(str_len),
+                    _ptr(customer_id), _ptr(timestamp), _ptr(quantity))
+    rc = lib().sbe_order_to_json_batch(ctypes.byref(b), n, what, _ptr(out), cap, _ptr(out_off), _ptr(status),
+                                       _ptr(workspace), workspace.numel(), _stream(stream))
+    _check(rc, "sbe_order_to_json_batch")
+    return OrderJson(out, out_off, status)

@@ -40,6 +40,9 @@
  * sbe_decode_batch(ON_EGRESS)     decode_ack  src/ack_decoder.cpp:29-105 (AckInfo
  *                                  include/aeron_cluster/ack_decoder.hpp:9-15) and
  *                                  MessageHandler::on_egress include/aeron_cluster/message_handler.hpp:35-68
+ * sbe_order_to_json_batch()       Order::to_json src/order_types.cpp:122-181 and publish_order's
+ *                                  headers JSON src/cluster_client.cpp:308-323 (the strings that
+ *                                  become the TopicMessage payload / headers)
  */
 #ifndef SBECODEC_H
 #define SBECODEC_H
@@ -51,7 +54,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 3
+#define SBECODEC_ABI_VERSION 4
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -281,6 +284,47 @@ size_t sbe_reassemble_workspace_size(uint64_t n);
 int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
                              uint8_t* out, uint64_t* msg_off, uint64_t* counts, void* workspace,
                              size_t workspace_bytes, void* stream);
+
+/* ========================== Order JSON (publish_order payload) ========================== */
+/* Replaces Order::to_json (src/order_types.cpp:122-181, jsoncpp StreamWriterBuilder with
+ * indentation "" → compact, keys sorted) and the headers JSON publish_order builds beside it
+ * (src/cluster_client.cpp:308-323), for a batch of Orders, so the strings feed
+ * sbe_encode_topic_batch as payload / headers without a host round trip.
+ * A batch of Orders (struct of arrays; order_types.hpp:16-66):
+ *   arena, str_off ([n][8] or NULL = packed), str_len [n][8]: the string members
+ *     0 client_order_uuid, 1 identifier, 2 base_token, 3 quote_token, 4 side, 5 id,
+ *     6 message_id (OrderUtils::generate_message_id's value, made by the caller),
+ *     7 status (selects messageType: "UPDATED" / "CANCELLED" → UPDATE_ORDER, else CREATE_ORDER);
+ *   customer_id [n], timestamp [n] (ns; create_ts = timestamp / 1000000), quantity [n] (f64).
+ * Number text follows glibc printf on the exact binary value: "%.17g" (jsoncpp valueToString,
+ * ".0" appended when there is no '.' or 'e'; NaN → null, ±inf → ±1e+9999) and "%f"
+ * (std::to_string); strings are escaped as jsoncpp 1.9.5 valueToQuotedStringN with emitUTF8
+ * false (\" \\ \b \f \n \r \t, other controls and every non-ASCII code point as lower-case \uXXXX,
+ * invalid UTF-8 as �); identifier is cut at its first NUL (.c_str(), order_types.cpp:138). */
+#define SBE_ORDER_FIELDS 8u
+#define SBE_JSON_ORDER_PAYLOAD 0u   /* Order::to_json() */
+#define SBE_JSON_PUBLISH_HEADERS 1u /* {"messageId":…,"messageType":…,"orderId":…} */
+#define SBE_JSON_OK 0u
+#define SBE_JSON_OVERFLOW 6u        /* record ends past out_capacity (nothing written) */
+typedef struct sbe_order_batch {
+    const uint8_t* arena;
+    const uint32_t* str_off;
+    const uint32_t* str_len;
+    const int64_t* customer_id;
+    const int64_t* timestamp;
+    const double* quantity;
+} sbe_order_batch;
+
+/* Bytes of device workspace sbe_order_to_json_batch needs for n records. */
+size_t sbe_order_json_workspace_size(uint64_t n);
+
+/* Write the JSON text of n Orders back to back: record i = out[out_off[i] .. out_off[i+1]).
+ * out_off (n + 1 device u64) always holds the full sizes; a record past out_capacity is not
+ * written and gets status SBE_JSON_OVERFLOW (status: n device u8 or NULL).  Two launches and a
+ * device scan on `stream`. */
+int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what, uint8_t* out,
+                            uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ================================== profiling ================================== */
 /* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every

@@ -984,3 +984,234 @@ int orc_seq_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const 
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Order JSON: Order::to_json (src/order_types.cpp:122-181) and publish_order's headers JSON
+ * (src/cluster_client.cpp:308-323).  Both go through jsoncpp's StreamWriterBuilder with
+ * indentation "" (compact: no newlines, colon ":"), whose object members come out in std::map
+ * order (Value::CZString::operator<: memcmp of the common prefix, then the shorter first).
+ * jsoncpp 1.9.5 is absent here: the writer logic below is restated from its published source
+ * (PARITY UNPINNED against jsoncpp itself); the number text is glibc snprintf, the same
+ * function jsoncpp (valueToString) and libstdc++ (std::to_string) call.
+ * ------------------------------------------------------------------------------------------ */
+#include <math.h>
+#include <stdio.h>
+
+typedef struct {
+    uint8_t* out; /* NULL: count only */
+    uint64_t n;
+} jw;
+
+static void jw_put(jw* w, const char* s, uint64_t n) {
+    if (w->out) memcpy(w->out + w->n, s, n);
+    w->n += n;
+}
+static void jw_lit(jw* w, const char* s) { jw_put(w, s, strlen(s)); }
+
+/* jsoncpp json_writer.cpp utf8ToCodepoint: lead byte decides the length, continuation bytes
+ * are not checked, overlong / surrogate / truncated → U+FFFD (a truncated one consumes 1 byte). */
+static uint32_t orc_utf8_cp(const uint8_t** s, const uint8_t* e) {
+    const uint8_t* p = *s;
+    uint32_t b = p[0], c;
+    if (b < 0x80) return b;
+    if (b < 0xE0) {
+        if (e - p < 2) return 0xFFFD;
+        c = ((b & 0x1F) << 6) | (p[1] & 0x3F);
+        *s = p + 1;
+        return c < 0x80 ? 0xFFFD : c;
+    }
+    if (b < 0xF0) {
+        if (e - p < 3) return 0xFFFD;
+        c = ((b & 0x0F) << 12) | ((uint32_t)(p[1] & 0x3F) << 6) | (p[2] & 0x3F);
+        *s = p + 2;
+        if (c >= 0xD800 && c <= 0xDFFF) return 0xFFFD;
+        return c < 0x800 ? 0xFFFD : c;
+    }
+    if (b < 0xF8) {
+        if (e - p < 4) return 0xFFFD;
+        c = ((b & 0x07) << 18) | ((uint32_t)(p[1] & 0x3F) << 12) | ((uint32_t)(p[2] & 0x3F) << 6) | (p[3] & 0x3F);
+        *s = p + 3;
+        return c < 0x10000 ? 0xFFFD : c;
+    }
+    return 0xFFFD;
+}
+
+static void jw_hex(jw* w, uint32_t v) { /* appendHex: "\\u" + 4 lower-case hex digits */
+    static const char hx[] = "0123456789abcdef";
+    char b[6] = {'\\', 'u', hx[(v >> 12) & 15], hx[(v >> 8) & 15], hx[(v >> 4) & 15], hx[v & 15]};
+    jw_put(w, b, 6);
+}
+
+/* jsoncpp valueToQuotedStringN(str, len, emitUTF8=false) */
+static void jw_quoted(jw* w, const uint8_t* s, uint64_t n) {
+    const uint8_t* e = s + n;
+    jw_put(w, "\"", 1);
+    for (const uint8_t* c = s; c < e; ++c) {
+        switch (*c) {
+            case '"': jw_put(w, "\\\"", 2); break;
+            case '\\': jw_put(w, "\\\\", 2); break;
+            case '\b': jw_put(w, "\\b", 2); break;
+            case '\f': jw_put(w, "\\f", 2); break;
+            case '\n': jw_put(w, "\\n", 2); break;
+            case '\r': jw_put(w, "\\r", 2); break;
+            case '\t': jw_put(w, "\\t", 2); break;
+            default: {
+                uint32_t cp = orc_utf8_cp(&c, e);
+                if (cp < 0x20) jw_hex(w, cp);
+                else if (cp < 0x80) { char ch = (char)cp; jw_put(w, &ch, 1); }
+                else if (cp < 0x10000) jw_hex(w, cp);
+                else {
+                    cp -= 0x10000;
+                    jw_hex(w, 0xD800 + ((cp >> 10) & 0x3FF));
+                    jw_hex(w, 0xDC00 + (cp & 0x3FF));
+                }
+            }
+        }
+    }
+    jw_put(w, "\"", 1);
+}
+
+static void jw_key(jw* w, const char* k) { /* "key": (keys here need no escaping) */
+    jw_put(w, "\"", 1);
+    jw_lit(w, k);
+    jw_put(w, "\":", 2);
+}
+
+/* jsoncpp valueToString(double, useSpecialFloats=false, precision=17, significantDigits) */
+static void jw_double(jw* w, double v) {
+    char b[64];
+    if (!isfinite(v)) {
+        jw_lit(w, isnan(v) ? "null" : (v < 0 ? "-1e+9999" : "1e+9999"));
+        return;
+    }
+    int n = snprintf(b, sizeof b, "%.*g", 17, v);
+    jw_put(w, b, (uint64_t)n);
+    if (!strchr(b, '.') && !strchr(b, 'e')) jw_lit(w, ".0");
+}
+
+/* std::to_string(double) = "%f"; std::to_string(long) = "%ld" */
+static void jw_fixed6(jw* w, double v) {
+    char b[400];
+    int n = snprintf(b, sizeof b, "%f", v);
+    jw_put(w, b, (uint64_t)n);
+}
+static void jw_i64(jw* w, int64_t v) {
+    char b[24];
+    int n = snprintf(b, sizeof b, "%lld", (long long)v);
+    jw_put(w, b, (uint64_t)n);
+}
+
+static void jw_qstr_i64(jw* w, int64_t v) {
+    jw_put(w, "\"", 1);
+    jw_i64(w, v);
+    jw_put(w, "\"", 1);
+}
+
+static uint64_t orc_cstr_len(const uint8_t* s, uint64_t n) { /* std::string(x.c_str()) */
+    const uint8_t* z = memchr(s, 0, n);
+    return z ? (uint64_t)(z - s) : n;
+}
+
+static int orc_eq(const uint8_t* s, uint64_t n, const char* lit) {
+    return n == strlen(lit) && memcmp(s, lit, n) == 0;
+}
+
+/* One Order's JSON text (what = SBE_JSON_*); returns its length, writes it when out != NULL. */
+uint64_t orc_order_json_one(const uint8_t* const s[8], const uint32_t len[8], int64_t customer_id,
+                            int64_t timestamp, double quantity, uint32_t what, uint8_t* out) {
+    jw w = {out, 0};
+    if (what == SBE_JSON_PUBLISH_HEADERS) {
+        /* cluster_client.cpp:308-323: message_type from order.status; keys sorted */
+        const int upd = orc_eq(s[7], len[7], "UPDATED") || orc_eq(s[7], len[7], "CANCELLED");
+        jw_lit(&w, "{");
+        jw_key(&w, "messageId");
+        jw_quoted(&w, s[6], len[6]);
+        jw_lit(&w, ",");
+        jw_key(&w, "messageType");
+        jw_lit(&w, upd ? "\"UPDATE_ORDER\"" : "\"CREATE_ORDER\"");
+        jw_lit(&w, ",");
+        jw_key(&w, "orderId");
+        jw_quoted(&w, s[5], len[5]);
+        jw_lit(&w, "}");
+        return w.n;
+    }
+    /* order_types.cpp:122-181, members in sorted order at every level */
+    jw_lit(&w, "{\"message\":{\"headers\":{\"auth_token\":\"Bearer xxx\",\"connection_uuid\":\"130032\",");
+    jw_key(&w, "create_ts");
+    jw_qstr_i64(&w, timestamp / 1000000);
+    jw_lit(&w, ",");
+    jw_key(&w, "customer_id");
+    jw_qstr_i64(&w, customer_id);
+    jw_lit(&w, ",\"ip_address\":\"10.37.62.251\",\"origin\":\"fix\",");
+    jw_key(&w, "origin_id");
+    jw_quoted(&w, s[1], orc_cstr_len(s[1], len[1]));
+    jw_lit(&w, ",\"origin_name\":\"FIX_GATEWAY\"},\"message\":{\"action\":\"CREATE\",\"order_details\":{");
+    jw_key(&w, "client_order_id");
+    jw_quoted(&w, s[0], len[0]);
+    jw_lit(&w, ",\"order_type\":\"market\",\"quantity\":{");
+    jw_key(&w, "token");
+    jw_quoted(&w, s[2], len[2]);
+    jw_lit(&w, ",");
+    jw_key(&w, "value");
+    jw_double(&w, quantity);
+    jw_lit(&w, "},");
+    jw_key(&w, "quantity_value_str");
+    jw_put(&w, "\"", 1);
+    jw_fixed6(&w, quantity);
+    jw_put(&w, "\"", 1);
+    jw_lit(&w, ",");
+    jw_key(&w, "side");
+    jw_quoted(&w, s[4], len[4]);
+    jw_lit(&w, ",\"token_pair\":{");
+    jw_key(&w, "base_token");
+    jw_quoted(&w, s[2], len[2]);
+    jw_lit(&w, ",");
+    jw_key(&w, "quote_token");
+    jw_quoted(&w, s[3], len[3]);
+    jw_lit(&w, "}}}},\"msg_type\":\"D\",");
+    jw_key(&w, "uuid");
+    jw_quoted(&w, s[0], len[0]);
+    jw_lit(&w, "}");
+    return w.n;
+}
+
+/* sbe_order_to_json_batch over host arrays (no capacity limit: out holds the full text). */
+int orc_order_json_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                         const int64_t* customer_id, const int64_t* timestamp, const double* quantity,
+                         uint64_t n, uint32_t what, uint8_t* out, uint64_t* out_off, int nthreads) {
+    if (what > SBE_JSON_PUBLISH_HEADERS) return SBE_EINVAL;
+    if (nthreads < 1) nthreads = 1;
+    uint64_t* base = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    if (!base) return SBE_EINVAL;
+    /* string bases for packed input */
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        base[i] = acc;
+        if (!str_off)
+            for (int f = 0; f < 8; ++f) acc += str_len[8 * i + f];
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const uint8_t* s[8];
+            uint32_t l[8];
+            uint64_t at = base[i];
+            for (int f = 0; f < 8; ++f) {
+                l[f] = str_len[8 * i + f];
+                if (str_off) s[f] = arena + str_off[8 * i + f];
+                else { s[f] = arena + at; at += l[f]; }
+            }
+            uint64_t m = orc_order_json_one(s, l, customer_id[i], timestamp[i], quantity[i], what,
+                                            pass ? out + out_off[i] : NULL);
+            if (!pass) out_off[i + 1] = m;
+        }
+        if (!pass) {
+            out_off[0] = 0;
+            for (uint64_t i = 0; i < n; ++i) out_off[i + 1] += out_off[i];
+        }
+    }
+    free(base);
+    return 0;
+}

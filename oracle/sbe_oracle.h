@@ -74,6 +74,17 @@ int orc_seq_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const 
                   const uint8_t* flags, const uint32_t* view_off, const uint32_t* view_len, uint64_t* seq,
                   int nthreads);
 
+/* Order::to_json (src/order_types.cpp:122-181) / publish_order headers JSON
+ * (src/cluster_client.cpp:308-323) of one Order: fields s[0..7] as in sbe_order_batch.  Returns
+ * the text length and writes it when out != NULL.  jsoncpp absent: PARITY UNPINNED, restated. */
+uint64_t orc_order_json_one(const uint8_t* const s[8], const uint32_t len[8], int64_t customer_id,
+                            int64_t timestamp, double quantity, uint32_t what, uint8_t* out);
+
+/* sbe_order_to_json_batch over host arrays (out holds the whole text). */
+int orc_order_json_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
+                         const int64_t* customer_id, const int64_t* timestamp, const double* quantity,
+                         uint64_t n, uint32_t what, uint8_t* out, uint64_t* out_off, int nthreads);
+
 /* protocol.hpp:37-42 */
 uint64_t orc_to_nanos_auto(uint64_t ts);
 

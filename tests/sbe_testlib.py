@@ -66,6 +66,9 @@ def oracle():
         L.orc_seq_eval.restype = u64
         L.orc_seq_eval.argtypes = [vp, u64]
         L.orc_seq_batch.argtypes = [vp, vp, u64, vp, vp, vp, vp, vp, i]
+        L.orc_order_json_one.restype = u64
+        L.orc_order_json_one.argtypes = [vp, vp, i64, i64, ctypes.c_double, u32, vp]
+        L.orc_order_json_batch.argtypes = [vp, vp, vp, vp, vp, vp, u64, u32, vp, vp, i]
         L.orc_to_nanos_auto.restype = u64
         L.orc_to_nanos_auto.argtypes = [u64]
         _oracle = L
@@ -691,3 +694,97 @@ def edge_records():
             body = bytes((b % 6) if i % 9 == 0 else (32 + b % 95) for i, b in enumerate(body))
         out.append((f"random{k}", hdr_bytes(*h) + body))
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Order JSON (Order::to_json, publish_order headers)
+# ------------------------------------------------------------------------------------------
+ORDER_FIELDS = 8  # client_order_uuid, identifier, base_token, quote_token, side, id, message_id, status
+
+
+def oracle_order_json_one(fields, customer_id, timestamp, quantity, what=0) -> bytes:
+    bufs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in fields]
+    ptrs = (ctypes.c_void_p * 8)(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+    lens = (ctypes.c_uint32 * 8)(*[len(f) for f in fields])
+    L = oracle()
+    n = L.orc_order_json_one(ptrs, lens, int(customer_id), int(timestamp), float(quantity), what, None)
+    out = ctypes.create_string_buffer(max(n, 1))
+    L.orc_order_json_one(ptrs, lens, int(customer_id), int(timestamp), float(quantity), what, out)
+    return out.raw[:n]
+
+
+def oracle_order_json(arena, str_len, customer_id, timestamp, quantity, what=0, str_off=None, nthreads=1):
+    """Batch Order JSON over host arrays → (text bytes, out_off uint64[n+1])."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    str_len = np.ascontiguousarray(str_len, dtype=np.uint32).reshape(-1, 8)
+    customer_id = np.ascontiguousarray(customer_id, dtype=np.int64)
+    timestamp = np.ascontiguousarray(timestamp, dtype=np.int64)
+    quantity = np.ascontiguousarray(quantity, dtype=np.float64)
+    n = customer_id.size
+    if str_off is not None:
+        str_off = np.ascontiguousarray(str_off, dtype=np.uint32).reshape(-1, 8)
+    cap = 700 * n + 12 * int(str_len.sum(dtype=np.uint64)) + 16
+    out = np.zeros(cap, dtype=np.uint8)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    oracle().orc_order_json_batch(_p(arena if arena.size else np.zeros(1, np.uint8)), _p(str_off), _p(str_len),
+                                  _p(customer_id), _p(timestamp), _p(quantity), n, what, _p(out), _p(out_off),
+                                  nthreads)
+    return out[: int(out_off[n])].tobytes(), out_off
+
+
+EDGE_DOUBLES = [0.0, -0.0, 1.0, -1.0, 0.1, 0.5, 1.5, 100.0, 1e16, 1e17, 123456789012345680.0, 2.0 ** 60,
+                1 + 2.0 ** -17, 0.0078125, 9.9999995, 0.0000005, 1e-5, 1e-4, 9.99999999999999e-5, 1e21, 1e22,
+                5e-324, 2.2250738585072014e-308, 1.7976931348623157e308, 0.30000000000000004, 999999.9999995,
+                123.456, 2.5, 0.125, 1e-300, 3.0e100, float("inf"), float("-inf"), float("nan"), -float("nan"),
+                9007199254740993.0, 4503599627370495.5, 0.000001, 0.0000015, 99999999999999999.0, 1e15 + 0.3]
+
+
+def order_batch(n: int, seed: int, hard: bool = True):
+    """Seeded Orders: (fields [n][8] list of bytes, customer_id, timestamp, quantity).  With hard,
+    strings carry quotes, backslashes, controls, NULs, UTF-8 (valid and not) and doubles span the
+    whole binary range."""
+    rng = np.random.default_rng(seed)
+    alpha = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+    specials = [b'"', b"\\", b"\n", b"\t", b"\x00", b"\x01", b"\x1f", b"\x7f", b"\xc3\xa9", b"\xe2\x82\xac",
+                b"\xf0\x9f\x98\x80", b"\xff", b"\xc3", b"\xe2\x82", b"\xed\xa0\x80", b"\xc0\xaf", b"\xf8", b"/",
+                b"\xf4\x90\x80\x80", b"\x80"]
+
+    def rstr(lo, hi):
+        k = int(rng.integers(lo, hi + 1))
+        b = bytearray(rng.choice(np.frombuffer(alpha, np.uint8), k).tobytes())
+        if hard and k and rng.random() < 0.3:
+            for _ in range(int(rng.integers(1, 4))):
+                at = int(rng.integers(0, len(b) + 1))
+                b[at:at] = specials[int(rng.integers(0, len(specials)))]
+        return bytes(b)
+
+    statuses = [b"CREATED", b"UPDATED", b"CANCELLED", b"UPDATE", b"", b"CANCELLED\x00"]
+    fields = []
+    for _ in range(n):
+        fields.append([rstr(0, 40), rstr(0, 12), rstr(0, 6), rstr(0, 6), rstr(0, 5), rstr(0, 20), rstr(0, 30),
+                       statuses[int(rng.integers(0, len(statuses)))]])
+    customer_id = rng.integers(-(2 ** 63), 2 ** 63 - 1, n, dtype=np.int64, endpoint=True)
+    timestamp = rng.integers(-(2 ** 63), 2 ** 63 - 1, n, dtype=np.int64, endpoint=True)
+    small = rng.random(n) < 0.5
+    customer_id[small] = rng.integers(0, 10 ** 6, int(small.sum()))
+    timestamp[small] = 1_760_000_000_000_000_000 + rng.integers(0, 10 ** 12, int(small.sum()))
+    kind = rng.integers(0, 4, n)
+    q = np.empty(n, dtype=np.float64)
+    # prices / quantities with few decimals, random bit patterns, edge values, round-ish values
+    k0 = int((kind == 0).sum())
+    scale = 10.0 ** rng.integers(0, 9, k0)
+    q[kind == 0] = np.round(rng.random(k0) * 10.0 ** rng.integers(0, 7, k0) * scale) / scale
+    q[kind == 1] = rng.integers(0, 2 ** 64, int((kind == 1).sum()), dtype=np.uint64).view(np.float64)
+    q[kind == 2] = np.array(EDGE_DOUBLES)[rng.integers(0, len(EDGE_DOUBLES), int((kind == 2).sum()))]
+    q[kind == 3] = rng.integers(1, 10 ** 9, int((kind == 3).sum())) / 2.0 ** rng.integers(0, 30, int((kind == 3).sum()))
+    if not hard:
+        q = np.abs(np.nan_to_num(q, nan=1.0, posinf=1.0, neginf=1.0))
+    return fields, customer_id, timestamp, q
+
+
+def pack_order_fields(fields):
+    """[n][8] bytes → (packed arena uint8, str_len uint32[n,8])."""
+    flat = [f for rec in fields for f in rec]
+    arena = np.frombuffer(b"".join(flat), dtype=np.uint8) if flat else np.zeros(0, np.uint8)
+    str_len = np.array([len(f) for f in flat], dtype=np.uint32).reshape(-1, 8)
+    return arena, str_len

@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_side_entry_points(lib):
     lib.sbe_abi_version.restype = ctypes.c_int
-    assert lib.sbe_abi_version() == 3
+    assert lib.sbe_abi_version() == 4
     lib.sbe_encode_workspace_size.restype = ctypes.c_size_t
     lib.sbe_encode_workspace_size.argtypes = [ctypes.c_uint64]
     assert lib.sbe_encode_workspace_size(1_000_000) >= 16 * (1_000_000 // 256)
@@ -52,12 +52,19 @@ def test_host_side_entry_points(lib):
     lib.sbe_lite_output_bound.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
     assert lib.sbe_lite_output_bound(10, 500, 301) == 500 + 24 * 10
     assert lib.sbe_lite_output_bound(10, 500, 201) == 500 + 26 * 10
+    lib.sbe_order_json_workspace_size.restype = ctypes.c_size_t
+    lib.sbe_order_json_workspace_size.argtypes = [ctypes.c_uint64]
+    assert lib.sbe_order_json_workspace_size(1000) >= 3 * 8 * 1001
     lib.sbe_last_error.restype = ctypes.c_char_p
     assert lib.sbe_last_error() == b""
 
 
 def test_invalid_arguments_are_rejected_before_any_launch(lib):
     vp = ctypes.c_void_p
+    lib.sbe_order_to_json_batch.restype = ctypes.c_int
+    lib.sbe_order_to_json_batch.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp, vp, vp,
+                                            ctypes.c_size_t, vp]
+    assert lib.sbe_order_to_json_batch(None, 1, 0, None, 0, None, None, None, 0, None) == -1
     lib.sbe_encode_topic_batch.restype = ctypes.c_int
     lib.sbe_encode_topic_batch.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp,
                                            ctypes.c_uint64, vp, vp, vp, ctypes.c_size_t, vp]
