@@ -12,7 +12,7 @@
 // one or two words; the full range (subnormals, 1e308) takes more words, never a different path.
 //
 // One lane per Order; a sizing launch (text length + packed-arena string total), two device scans,
-// then the writing launch.  The text is written through an 8-byte store buffer per lane.
+// then the writing launch, which stages each wave's texts in LDS and stores them coalesced.
 #pragma once
 
 namespace oj {
@@ -42,34 +42,16 @@ struct JsonArgs {
 struct CountSink {
     uint64_t n = 0;
     __device__ void put(uint8_t) { ++n; }
-    __device__ void flush() {}
 };
 
-struct WriteSink {
-    uint8_t* p;     // record start
-    uint64_t n = 0; // bytes produced
-    uint64_t buf = 0;
-    uint32_t fill = 0;  // bytes in buf
-    __device__ explicit WriteSink(uint8_t* q) : p(q) {}
-    __device__ void put(uint8_t b) {
-        buf |= (uint64_t)b << (8 * fill);
-        ++fill;
-        ++n;
-        if (fill == 8 || (((uintptr_t)(p + n)) & 7) == 0) drain();
-    }
-    __device__ void drain() {
-        uint8_t* d = p + n - fill;
-        if (fill == 8 && (((uintptr_t)d) & 7) == 0) {
-            *reinterpret_cast<uint64_t*>(d) = buf;
-        } else {
-            for (uint32_t i = 0; i < fill; ++i) d[i] = (uint8_t)(buf >> (8 * i));
-        }
-        buf = 0;
-        fill = 0;
-    }
-    __device__ void flush() {
-        if (fill) drain();
-    }
+// One byte store per put through a generic pointer: the LDS window or, for a record that does
+// not fit the window, HBM.  One sink type keeps one copy of the text code in the kernel (the
+// kernel must stay well inside the instruction cache).
+struct ByteSink {
+    uint8_t* p;
+    uint64_t n = 0;
+    __device__ explicit ByteSink(uint8_t* q) : p(q) {}
+    __device__ void put(uint8_t b) { p[n++] = b; }
 };
 
 template <class S>
@@ -119,7 +101,7 @@ __device__ inline void hex4(S& s, uint32_t v) {
 
 // jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
 template <class S>
-__device__ void quoted(S& s, const uint8_t* p, uint64_t len) {
+__device__ __noinline__ void quoted(S& s, const uint8_t* p, uint64_t len) {
     s.put('"');
     uint64_t i = 0;
     while (i < len) {
@@ -296,7 +278,7 @@ __device__ inline uint32_t pow10u(int p) {
 // "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
 // round half to even on the exact value; inf / nan as glibc prints them.
 template <class S>
-__device__ void fmt_fixed6(S& s, double v) {
+__device__ __noinline__ void fmt_fixed6(S& s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     const bool neg = (bits >> 63) != 0;
     if (__builtin_isnan(v)) {
@@ -347,7 +329,7 @@ __device__ void fmt_fixed6(S& s, double v) {
 // jsoncpp valueToString(double, false, 17, significantDigits): "%.17g" then ".0" when the text
 // has neither '.' nor 'e'; NaN → null, ±inf → ±1e+9999.
 template <class S>
-__device__ void fmt_g17(S& s, double v) {
+__device__ __noinline__ void fmt_g17(S& s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     if (__builtin_isnan(v)) {
         lit(s, "null");
@@ -442,10 +424,10 @@ __device__ inline bool eq_lit(const uint8_t* p, uint64_t n, const char* t) {
 }
 
 // One Order's text (src/order_types.cpp:122-181, src/cluster_client.cpp:308-323).
-template <class S>
+template <uint32_t kWhat, class S>
 __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, const uint8_t* const f[kFields],
                            const uint32_t l[kFields]) {
-    if (a.what == SBE_JSON_PUBLISH_HEADERS) {
+    if (kWhat == SBE_JSON_PUBLISH_HEADERS) {
         const bool upd = eq_lit(f[7], l[7], "UPDATED") || eq_lit(f[7], l[7], "CANCELLED");
         lit(s, "{\"messageId\":");
         quoted(s, f[6], l[6]);
@@ -510,6 +492,7 @@ __global__ __launch_bounds__(kBlock) void order_json_totals(JsonArgs a) {
 }
 
 // Sizing launch: the text length of record i into sz[i] (sz[n] = 0).
+template <uint32_t kWhat>
 __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i > a.n) return;
@@ -521,23 +504,67 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
     uint32_t l[kFields];
     fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
     CountSink c;
-    order_text(c, a, i, f, l);
+    order_text<kWhat>(c, a, i, f, l);
     a.sz[i] = c.n;
 }
 
-__global__ __launch_bounds__(kBlock) void order_json_write(JsonArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= a.n) return;
-    const uint64_t o = a.out_off[i], e = a.out_off[i + 1];
-    const bool fits = e <= a.cap;
-    if (a.status) a.status[i] = fits ? SBE_JSON_OK : SBE_JSON_OVERFLOW;
-    if (!fits) return;
-    const uint8_t* f[kFields];
-    uint32_t l[kFields];
-    fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-    WriteSink w(a.out + o);
-    order_text(w, a, i, f, l);
-    w.flush();
+// Writing launch: one wave per 64 Orders.  Their texts are contiguous in `out`, so each lane
+// writes its record into an LDS window (byte writes) and the wave then stores the window
+// with 16-byte coalesced stores; only the bytes of a record that does not fit the window go to
+// HBM straight from its lane.  Records past out_capacity are written by nobody.
+constexpr uint32_t kWWave = 64;
+#ifndef SBE_OJ_WIN
+#define SBE_OJ_WIN 24576
+#endif
+constexpr uint32_t kWin = SBE_OJ_WIN;  // bytes of LDS window per wave
+
+template <uint32_t kWhat>
+__global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWin ? kWin : 16];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * kWWave;
+    const uint64_t i = r0 + lane;
+    const uint64_t rend = r0 + kWWave < a.n ? r0 + kWWave : a.n;
+    const uint64_t o0 = a.out_off[r0];
+    // window origin: the 16-byte aligned address at or below out + o0 (LDS offset ≡ address mod 16)
+    const uint64_t skew = (uint64_t)((uintptr_t)(a.out + o0) & 15);
+    const uint64_t wbase = o0 - skew;  // output coordinate of win[0]
+    uint64_t my_end = o0;              // end of the bytes this lane may let the window store
+    if (i < rend) {
+        const uint64_t o = a.out_off[i], e = a.out_off[i + 1];
+        const bool fits = e <= a.cap;
+        if (a.status) a.status[i] = fits ? SBE_JSON_OK : SBE_JSON_OVERFLOW;
+        if (fits) {
+            const uint8_t* f[kFields];
+            uint32_t l[kFields];
+            fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
+            const bool staged = e - wbase <= kWin;
+            ByteSink w(staged ? win + (o - wbase) : a.out + o);
+            order_text<kWhat>(w, a, i, f, l);
+            if (staged) my_end = e;
+        }
+    }
+    // the window holds [o0, cend): the largest staged end over the wave
+    uint64_t cend = my_end;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t t = __shfl_xor(cend, d, kWWave);
+        cend = t > cend ? t : cend;
+    }
+    __syncthreads();
+    if (cend <= o0) return;
+    const uint64_t nch = (cend - wbase + 15) / 16;
+    for (uint64_t c = lane; c < nch; c += kWWave) {
+        const uint64_t x0 = wbase + 16 * c;  // output coordinate of this 16-byte chunk
+        if (x0 >= o0 && x0 + 16 <= cend) {
+            const uint4 v = *reinterpret_cast<const uint4*>(win + 16 * c);
+            __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(a.out + x0));
+            __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(a.out + x0) + 1);
+            __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(a.out + x0) + 2);
+            __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(a.out + x0) + 3);
+        } else {
+            for (uint64_t x = x0 < o0 ? o0 : x0; x < x0 + 16 && x < cend; ++x) a.out[x] = win[x - wbase];
+        }
+    }
 }
 
 inline size_t scan_temp(uint64_t n) {

@@ -401,6 +401,91 @@ std::vector<std::uint8_t> CommitManager::build_commit_offset_message(const std::
     return b.bytes;
 }
 
+OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vector<std::string>& message_ids) {
+    const size_t n = orders.size();
+    if (message_ids.size() != n) throw std::invalid_argument("orders_to_json: one message id per order");
+    OrderJsonBatch r;
+    for (EncodedBatch* b : {&r.payload, &r.headers}) {
+        b->offsets.assign(n + 1, 0);
+        b->status.assign(n, 0);
+    }
+    if (n == 0) return r;
+    auto field = [&](size_t i, int k) -> std::string_view {
+        const Order& o = orders[i];
+        switch (k) {
+            case 0: return o.client_order_uuid;
+            case 1: return o.identifier;
+            case 2: return o.base_token;
+            case 3: return o.quote_token;
+            case 4: return o.side;
+            case 5: return o.id;
+            case 6: return message_ids[i];
+            default: return o.status;
+        }
+    };
+    Ctx& c = ctx();
+    size_t arena = 0;
+    for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) arena += field(i, k).size();
+    const size_t nlen = n * 4 * SBE_ORDER_FIELDS, nnum = n * 24;
+    c.h_arena.need(arena + 16);
+    c.h_len.need(nlen + nnum);
+    uint8_t* ap = static_cast<uint8_t*>(c.h_arena.p);
+    uint32_t* lp = static_cast<uint32_t*>(c.h_len.p);
+    int64_t* cid = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(c.h_len.p) + ((nlen + 7) & ~(size_t)7));
+    int64_t* ts = cid + n;
+    double* q = reinterpret_cast<double*>(ts + n);
+    size_t at = 0;
+    for (size_t i = 0; i < n; ++i) {
+        for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) {
+            const std::string_view f = field(i, k);
+            std::memcpy(ap + at, f.data(), f.size());
+            at += f.size();
+            lp[SBE_ORDER_FIELDS * i + k] = (uint32_t)f.size();
+        }
+        cid[i] = orders[i].customer_id;
+        ts[i] = orders[i].timestamp;
+        q[i] = orders[i].quantity;
+    }
+    const size_t small = ((nlen + 7) & ~(size_t)7) + nnum;
+    const uint64_t cap = 12 * (uint64_t)arena + 700 * (uint64_t)n + 16;  // escapes ≤ 6x, strings used ≤ twice
+    c.d_arena.need(arena + 16);
+    c.d_len.need(small);
+    c.d_out.need(2 * cap);
+    c.d_off.need(2 * (n + 1) * 8);
+    c.d_st.need(2 * n);
+    c.d_ws.need(sbe_order_json_workspace_size(n));
+    hip_check(hipMemcpyAsync(c.d_arena.p, ap, arena, hipMemcpyHostToDevice, c.stream), "H2D");
+    hip_check(hipMemcpyAsync(c.d_len.p, c.h_len.p, small, hipMemcpyHostToDevice, c.stream), "H2D");
+    const uint8_t* dl = static_cast<const uint8_t*>(c.d_len.p);
+    const int64_t* d_cid = reinterpret_cast<const int64_t*>(dl + ((nlen + 7) & ~(size_t)7));
+    sbe_order_batch in{static_cast<const uint8_t*>(c.d_arena.p), nullptr, reinterpret_cast<const uint32_t*>(dl),
+                       d_cid, d_cid + n, reinterpret_cast<const double*>(d_cid + 2 * n)};
+    for (int w = 0; w < 2; ++w) {
+        EncodedBatch& b = w ? r.headers : r.payload;
+        uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
+        uint64_t* off = static_cast<uint64_t*>(c.d_off.p) + w * (n + 1);
+        uint8_t* st = static_cast<uint8_t*>(c.d_st.p) + w * n;
+        if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, out, cap, off, st,
+                                    c.d_ws.p, c.d_ws.cap, c.stream) != SBE_OK)
+            fail("sbe_order_to_json_batch");
+        hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
+        hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, c.stream), "D2H");
+        hip_check(hipStreamSynchronize(c.stream), "sync");
+        b.bytes.resize(b.offsets[n]);
+        if (b.offsets[n]) {
+            hip_check(hipMemcpyAsync(b.bytes.data(), out, b.offsets[n], hipMemcpyDeviceToHost, c.stream), "D2H");
+            hip_check(hipStreamSynchronize(c.stream), "sync");
+        }
+    }
+    return r;
+}
+
+std::string Order::to_json() const {
+    OrderJsonBatch b = orders_to_json({*this}, {std::string()});
+    return std::string(b.payload.bytes.begin(), b.payload.bytes.end());
+}
+
 std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
                                                            const std::string& uuid, const std::string& payload,
                                                            const std::string& headers, std::int64_t timestamp) {

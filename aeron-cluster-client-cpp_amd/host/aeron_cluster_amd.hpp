@@ -219,6 +219,32 @@ private:
     std::vector<std::uint8_t> acc_;
 };
 
+// include/aeron_cluster/order_types.hpp:16-66: the members Order::to_json and publish_order read
+// (the reference class carries more; they play no part in the text).
+struct Order {
+    std::string id;
+    std::string client_order_uuid;
+    std::string base_token;
+    std::string quote_token;
+    std::string side;
+    double quantity = 0.0;
+    std::int64_t customer_id = 0;
+    std::string status = "CREATED";
+    std::int64_t timestamp = 0;
+    std::string identifier;
+    // src/order_types.cpp:122-181 (one-record batch on the GPU)
+    std::string to_json() const;
+};
+
+// A batch of Orders → Order::to_json texts (payload) and the headers JSON publish_order builds
+// beside them (src/cluster_client.cpp:308-323, messageId = message_ids[i]); record i of each is
+// bytes[offsets[i], offsets[i+1]), ready to be TopicMessage payload / headers.
+struct OrderJsonBatch {
+    EncodedBatch payload;
+    EncodedBatch headers;
+};
+OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vector<std::string>& message_ids);
+
 // The raw ingress sink (ClusterClient::offer_ingress signature).  Feeds every encoded record of a
 // batch to it in order; returns the number accepted before the first refusal.
 using OfferFn = std::function<bool(const std::uint8_t* data, std::size_t len)>;

@@ -6,6 +6,7 @@ algorithmic bytes per launch (computed from the actual record sizes) and its fra
   config4_var_roundtrip  16 M variable-length TopicMessages, encode + parse decode (config 4)
   session_fixed256       1 M session-framed Order TopicMessages (32-B SessionMessageHeader + 248 B)
   lite301 / lite201      1 M CommitOffsetLite / OrderRequestLite records, encode + Lite decode
+  order_json             1 M Orders → Order::to_json payload + publish_order headers JSON (two calls)
   reassemble             1 M Aeron fragments (90 % whole messages, the rest BEGIN..END groups),
                          BEGIN/END reassembly (all five launches, torch events around the call)
 Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...]  (GPU only)
@@ -219,11 +220,46 @@ def row_reassemble(steps, warmup):
     line("reassemble", n, ms * 1e-3, {"sbe_reassemble_fragments (5 launches)": (ms, nbytes)})
 
 
+def row_order_json(steps, warmup):
+    n = 1_000_000
+    fields, cid, ts, q = T.realistic_orders(n)
+    arena, str_len = T.pack_order_fields(fields)
+    args = (dev(arena, torch.uint8), dev(str_len.astype(np.int32), torch.int32), dev(cid, torch.int64),
+            dev(ts, torch.int64), torch.from_numpy(q).cuda())
+    outs = {}
+    for what in (sbecodec.JSON_ORDER_PAYLOAD, sbecodec.JSON_PUBLISH_HEADERS):
+        r = sbecodec.order_to_json_batch(*args, what=what)
+        outs[what] = r
+    fn = lambda: [sbecodec.order_to_json_batch(*args, what=w, out=outs[w].out, out_off=outs[w].out_off,  # noqa: E731
+                                               status=outs[w].status) for w in outs]
+    for _ in range(warmup):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    text = sum(int(outs[w].out_off[-1]) for w in outs)
+    # strings read (payload reads uuid / base twice), lengths + numbers read, text + offsets written
+    sl = str_len.astype(np.int64)
+    nbytes = int(2 * sl[:, 0].sum() + sl[:, 1:5].sum() + sl[:, 2].sum() + sl[:, 5:8].sum()) + n * (32 + 24) + \
+        text + 2 * 8 * n
+    k = 100_000
+    ak, lk = T.pack_order_fields(fields[:k])
+    set_cpu(cpu_rate(lambda: [T.oracle_order_json(ak, lk, cid[:k], ts[:k], q[:k], w, nthreads=CPU_THREADS)
+                              for w in (0, 1)], k),
+            f"{k} Orders of the same batch, oracle payload + headers JSON (glibc snprintf), OpenMP {CPU_THREADS} threads")
+    line("order_json", n, ms * 1e-3, {"sbe_order_to_json_batch x2 (payload + headers)": (ms, nbytes)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble")
+    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json")
     args = ap.parse_args()
     sbecodec.require_device()
     for r in args.rows.split(","):
@@ -235,6 +271,8 @@ def main():
             row_session(args.steps, args.warmup)
         elif r == "reassemble":
             row_reassemble(args.steps, args.warmup)
+        elif r == "order_json":
+            row_order_json(args.steps, args.warmup)
         elif r.startswith("lite"):
             row_lite(int(r[4:]), args.steps, args.warmup)
         torch.cuda.empty_cache()

@@ -282,6 +282,69 @@ int main() {
         auto r2 = fr.on_fragments(reinterpret_cast<const uint8_t*>(rest.data()), off2, fl2, 1);
         CHECK(r2.offsets.size() == 2 && std::string(r2.record(0)) == "ijklm" && fr.pending_bytes() == 0);
     }
+    {  // Order::to_json / orders_to_json (src/order_types.cpp:122-181, src/cluster_client.cpp:308-323)
+        Order o;
+        o.client_order_uuid = "cli-uuid-1";
+        o.identifier = "FIXID";
+        o.base_token = "BTC";
+        o.quote_token = "USDC";
+        o.side = "BUY";
+        o.id = "ord-7";
+        o.customer_id = 42;
+        o.timestamp = 1760000000123456789LL;
+        o.quantity = 0.1;
+        const std::string known =
+            "{\"message\":{\"headers\":{\"auth_token\":\"Bearer xxx\",\"connection_uuid\":\"130032\",\"create_ts\":"
+            "\"1760000000123\",\"customer_id\":\"42\",\"ip_address\":\"10.37.62.251\",\"origin\":\"fix\",\"origin_id\":"
+            "\"FIXID\",\"origin_name\":\"FIX_GATEWAY\"},\"message\":{\"action\":\"CREATE\",\"order_details\":{"
+            "\"client_order_id\":\"cli-uuid-1\",\"order_type\":\"market\",\"quantity\":{\"token\":\"BTC\",\"value\":"
+            "0.10000000000000001},\"quantity_value_str\":\"0.100000\",\"side\":\"BUY\",\"token_pair\":{\"base_token\":"
+            "\"BTC\",\"quote_token\":\"USDC\"}}}},\"msg_type\":\"D\",\"uuid\":\"cli-uuid-1\"}";
+        CHECK(o.to_json() == known);
+        std::mt19937_64 rng(5);
+        std::vector<Order> orders(3000);
+        std::vector<std::string> mids(orders.size());
+        for (size_t i = 0; i < orders.size(); ++i) {
+            Order& x = orders[i];
+            x.client_order_uuid = "u" + std::to_string(rng() % 100000) + (i % 7 == 0 ? "\"\\\n\xc3\xa9" : "");
+            x.identifier = i % 11 == 0 ? std::string("id\0tail", 7) : "ID" + std::to_string(i);
+            x.base_token = "BTC";
+            x.quote_token = i % 2 ? "USDC" : "USDT";
+            x.side = i % 3 ? "BUY" : "SELL";
+            x.id = "o" + std::to_string(i);
+            x.status = i % 5 == 0 ? "UPDATED" : (i % 5 == 1 ? "CANCELLED" : "CREATED");
+            x.customer_id = (int64_t)(rng() >> 20);
+            x.timestamp = (int64_t)rng();
+            uint64_t bits = rng();
+            double d;
+            std::memcpy(&d, &bits, 8);
+            x.quantity = i % 2 ? d : (double)(rng() % 1000000) / 10000.0;
+            mids[i] = "msg_" + std::to_string(i);
+        }
+        OrderJsonBatch b = orders_to_json(orders, mids);
+        for (size_t i = 0; i < orders.size(); ++i) {
+            const Order& x = orders[i];
+            const std::string* fs[8] = {&x.client_order_uuid, &x.identifier, &x.base_token, &x.quote_token,
+                                        &x.side, &x.id, &mids[i], &x.status};
+            const uint8_t* sp[8];
+            uint32_t sl[8];
+            for (int k = 0; k < 8; ++k) {
+                sp[k] = reinterpret_cast<const uint8_t*>(fs[k]->data());
+                sl[k] = (uint32_t)fs[k]->size();
+            }
+            for (int w = 0; w < 2; ++w) {
+                const EncodedBatch& e = w ? b.headers : b.payload;
+                std::vector<uint8_t> exp(orc_order_json_one(sp, sl, x.customer_id, x.timestamp, x.quantity, w, nullptr));
+                orc_order_json_one(sp, sl, x.customer_id, x.timestamp, x.quantity, w, exp.data());
+                const std::vector<uint8_t> got(e.bytes.begin() + e.offsets[i], e.bytes.begin() + e.offsets[i + 1]);
+                if (got != exp) {
+                    CHECK(got == exp);
+                    break;
+                }
+            }
+        }
+        CHECK(b.payload.status.size() == orders.size() && b.headers.offsets.size() == orders.size() + 1);
+    }
     std::printf("host api test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }

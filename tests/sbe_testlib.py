@@ -788,3 +788,25 @@ def pack_order_fields(fields):
     arena = np.frombuffer(b"".join(flat), dtype=np.uint8) if flat else np.zeros(0, np.uint8)
     str_len = np.array([len(f) for f in flat], dtype=np.uint32).reshape(-1, 8)
     return arena, str_len
+
+
+def realistic_orders(n: int, seed: int = 0x5EED00F3):
+    """Order-shaped batch for the bench row: uuid 36 B, identifier 8 B, BTC/USDC-like tokens,
+    BUY/SELL, id 20 B, message id 29 B, status; quantities with <= 4 decimals below 1e4."""
+    rng = np.random.default_rng(seed)
+    hexd = np.frombuffer(b"0123456789abcdef", np.uint8)
+    uu = rng.choice(hexd, (n, 36))
+    uu[:, [8, 13, 18, 23]] = ord("-")
+    ident = rng.choice(np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZ", np.uint8), (n, 8))
+    oid = rng.choice(hexd, (n, 20))
+    mid = np.concatenate([np.tile(np.frombuffer(b"msg_", np.uint8), (n, 1)),
+                          (48 + rng.integers(0, 10, (n, 19))).astype(np.uint8),
+                          np.full((n, 1), ord("_"), np.uint8), (48 + rng.integers(0, 10, (n, 5))).astype(np.uint8)], 1)
+    bases, quotes, sides = [b"BTC", b"ETH", b"SOL"], [b"USDC", b"USDT"], [b"BUY", b"SELL"]
+    bi, qi, si = rng.integers(0, 3, n), rng.integers(0, 2, n), rng.integers(0, 2, n)
+    fields = [[uu[i].tobytes(), ident[i].tobytes(), bases[bi[i]], quotes[qi[i]], sides[si[i]], oid[i].tobytes(),
+               mid[i].tobytes(), b"CREATED"] for i in range(n)]
+    cid = rng.integers(1, 10 ** 7, n).astype(np.int64)
+    ts = (1_760_000_000_000_000_000 + rng.integers(0, 10 ** 12, n)).astype(np.int64)
+    q = np.round(rng.random(n) * 10 ** 4, 4)
+    return fields, cid, ts, q
