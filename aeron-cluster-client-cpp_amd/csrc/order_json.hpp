@@ -18,6 +18,13 @@
 namespace oj {
 
 constexpr uint32_t kFields = SBE_ORDER_FIELDS;
+
+// Address-space-typed pointers: the helpers are out of line, and a plain pointer argument would
+// make every byte access a flat instruction (which waits on both the LDS and the vector-memory
+// counters).  Strings are read from HBM (global), texts are written to LDS or HBM.
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint8_t gw8;
+typedef __attribute__((address_space(3))) uint8_t lw8;
 constexpr uint32_t kBlock = 256;
 
 struct JsonArgs {
@@ -44,13 +51,18 @@ struct CountSink {
     __device__ void put(uint8_t) { ++n; }
 };
 
-// One byte store per put through a generic pointer: the LDS window or, for a record that does
-// not fit the window, HBM.  One sink type keeps one copy of the text code in the kernel (the
-// kernel must stay well inside the instruction cache).
-struct ByteSink {
-    uint8_t* p;
+// One byte store per put: into the wave's LDS window (ds_write_b8) or, for a record larger than
+// the window, straight to HBM.
+struct LdsSink {
+    lw8* p;
+    uint32_t n = 0;
+    __device__ explicit LdsSink(lw8* q) : p(q) {}
+    __device__ void put(uint8_t b) { p[n++] = b; }
+};
+struct HbmSink {
+    gw8* p;
     uint64_t n = 0;
-    __device__ explicit ByteSink(uint8_t* q) : p(q) {}
+    __device__ explicit HbmSink(gw8* q) : p(q) {}
     __device__ void put(uint8_t b) { p[n++] = b; }
 };
 
@@ -61,32 +73,55 @@ __device__ inline void lit(S& s, const char* t) {
 
 // jsoncpp json_writer.cpp utf8ToCodepoint (lead byte decides the length; continuation bytes are
 // not checked; truncated / overlong / surrogate → U+FFFD; a truncated sequence consumes 1 byte).
-__device__ inline uint32_t utf8_cp(const uint8_t* s, uint64_t left, uint32_t& used) {
-    const uint32_t b = s[0];
+// b1..b3 are the bytes after the lead (0 past the end of the string).
+__device__ inline uint32_t utf8_cp(uint32_t b, uint32_t b1, uint32_t b2, uint32_t b3, uint64_t left,
+                                   uint32_t& used) {
     used = 1;
     if (b < 0x80) return b;
     if (b < 0xE0) {
         if (left < 2) return 0xFFFD;
-        const uint32_t c = ((b & 0x1F) << 6) | (s[1] & 0x3F);
+        const uint32_t c = ((b & 0x1F) << 6) | (b1 & 0x3F);
         used = 2;
         return c < 0x80 ? 0xFFFD : c;
     }
     if (b < 0xF0) {
         if (left < 3) return 0xFFFD;
-        const uint32_t c = ((b & 0x0F) << 12) | ((uint32_t)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+        const uint32_t c = ((b & 0x0F) << 12) | ((b1 & 0x3F) << 6) | (b2 & 0x3F);
         used = 3;
         if (c >= 0xD800 && c <= 0xDFFF) return 0xFFFD;
         return c < 0x800 ? 0xFFFD : c;
     }
     if (b < 0xF8) {
         if (left < 4) return 0xFFFD;
-        const uint32_t c = ((b & 0x07) << 18) | ((uint32_t)(s[1] & 0x3F) << 12) | ((uint32_t)(s[2] & 0x3F) << 6) |
-                           (s[3] & 0x3F);
+        const uint32_t c = ((b & 0x07) << 18) | ((b1 & 0x3F) << 12) | ((b2 & 0x3F) << 6) | (b3 & 0x3F);
         used = 4;
         return c < 0x10000 ? 0xFFFD : c;
     }
     return 0xFFFD;
 }
+
+// Reads a string through aligned 16-byte loads, so a lane's walk over its string issues one
+// load per 16 bytes instead of one dependent load per byte.  A block holding a byte of the
+// string lies inside the allocation's page, so the over-read is harmless.
+struct BlockReader {
+    uintptr_t blk = ~(uintptr_t)0;
+    uint4 v;
+    __device__ uint32_t at(gu8* p) {
+        const uintptr_t a = (uintptr_t)p, b = a & ~(uintptr_t)15;
+        if (b != blk) {
+            blk = b;
+            typedef const __attribute__((address_space(1))) uint32_t gu32;
+            gu32* q = reinterpret_cast<gu32*>(b);
+            v.x = q[0];
+            v.y = q[1];
+            v.z = q[2];
+            v.w = q[3];
+        }
+        const uint32_t o = (uint32_t)(a & 15);
+        const uint32_t w = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);
+        return (w >> (8 * (o & 3))) & 0xFF;
+    }
+};
 
 template <class S>
 __device__ inline void hex4(S& s, uint32_t v) {
@@ -100,12 +135,15 @@ __device__ inline void hex4(S& s, uint32_t v) {
 }
 
 // jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
+// Out-of-line helpers take the sink by value and return it: a sink passed by reference lives in
+// scratch and every put would load and store its count.
 template <class S>
-__device__ __noinline__ void quoted(S& s, const uint8_t* p, uint64_t len) {
+__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
     s.put('"');
+    BlockReader rd;
     uint64_t i = 0;
     while (i < len) {
-        const uint8_t c = p[i];
+        const uint8_t c = (uint8_t)rd.at(p + i);
         if (c >= 0x20 && c < 0x80 && c != '"' && c != '\\') {  // the common case
             s.put(c);
             ++i;
@@ -122,7 +160,10 @@ __device__ __noinline__ void quoted(S& s, const uint8_t* p, uint64_t len) {
             default: break;
         }
         uint32_t used;
-        uint32_t cp = utf8_cp(p + i, len - i, used);
+        const uint64_t left = len - i;
+        const uint32_t b1 = left > 1 ? rd.at(p + i + 1) : 0, b2 = left > 2 ? rd.at(p + i + 2) : 0,
+                       b3 = left > 3 ? rd.at(p + i + 3) : 0;
+        uint32_t cp = utf8_cp(c, b1, b2, b3, left, used);
         i += used;
         if (cp < 0x10000) {
             hex4(s, cp);
@@ -133,6 +174,7 @@ __device__ __noinline__ void quoted(S& s, const uint8_t* p, uint64_t len) {
         }
     }
     s.put('"');
+    return s;
 }
 
 template <class S>
@@ -278,22 +320,22 @@ __device__ inline uint32_t pow10u(int p) {
 // "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
 // round half to even on the exact value; inf / nan as glibc prints them.
 template <class S>
-__device__ __noinline__ void fmt_fixed6(S& s, double v) {
+__device__ __noinline__ S fmt_fixed6(S s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     const bool neg = (bits >> 63) != 0;
     if (__builtin_isnan(v)) {
         if (neg) s.put('-');
         lit(s, "nan");
-        return;
+        return s;
     }
     if (neg) s.put('-');
     if (__builtin_isinf(v)) {
         lit(s, "inf");
-        return;
+        return s;
     }
     if ((bits << 1) == 0) {
         lit(s, "0.000000");
-        return;
+        return s;
     }
     Exact x;
     x.init(v);
@@ -324,26 +366,27 @@ __device__ __noinline__ void fmt_fixed6(S& s, double v) {
     }
     s.put('.');
     for (uint32_t p = 100000u; p; p /= 10) s.put((uint8_t)('0' + (kept / p) % 10));
+    return s;
 }
 
 // jsoncpp valueToString(double, false, 17, significantDigits): "%.17g" then ".0" when the text
 // has neither '.' nor 'e'; NaN → null, ±inf → ±1e+9999.
 template <class S>
-__device__ __noinline__ void fmt_g17(S& s, double v) {
+__device__ __noinline__ S fmt_g17(S s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     if (__builtin_isnan(v)) {
         lit(s, "null");
-        return;
+        return s;
     }
     const bool neg = (bits >> 63) != 0;
     if (__builtin_isinf(v)) {
         lit(s, neg ? "-1e+9999" : "1e+9999");
-        return;
+        return s;
     }
     if (neg) s.put('-');
     if ((bits << 1) == 0) {
         lit(s, "0.0");
-        return;
+        return s;
     }
     Exact x;
     x.init(v);
@@ -398,7 +441,7 @@ __device__ __noinline__ void fmt_g17(S& s, double v) {
         else s.put('+');
         if (ax < 10) s.put('0');
         dec_u64(s, (uint64_t)ax);
-        return;  // has an 'e': no ".0"
+        return s;  // has an 'e': no ".0"
     }
     if (X >= 0) {
         for (int j = 0; j <= X; ++j) s.put((uint8_t)('0' + d[j]));
@@ -414,32 +457,35 @@ __device__ __noinline__ void fmt_g17(S& s, double v) {
         for (int j = 0; j < -X - 1; ++j) s.put('0');
         for (int j = 0; j <= last; ++j) s.put((uint8_t)('0' + d[j]));
     }
+    return s;
 }
 
-__device__ inline bool eq_lit(const uint8_t* p, uint64_t n, const char* t) {
+__device__ inline bool eq_lit(gu8* p, uint64_t n, const char* t) {
+    BlockReader rd;
     uint64_t i = 0;
     for (; t[i]; ++i)
-        if (i >= n || p[i] != (uint8_t)t[i]) return false;
+        if (i >= n || rd.at(p + i) != (uint8_t)t[i]) return false;
     return i == n;
 }
 
 // One Order's text (src/order_types.cpp:122-181, src/cluster_client.cpp:308-323).
 template <uint32_t kWhat, class S>
-__device__ void order_text(S& s, const JsonArgs& a, uint64_t i, const uint8_t* const f[kFields],
+__device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFields],
                            const uint32_t l[kFields]) {
     if (kWhat == SBE_JSON_PUBLISH_HEADERS) {
         const bool upd = eq_lit(f[7], l[7], "UPDATED") || eq_lit(f[7], l[7], "CANCELLED");
         lit(s, "{\"messageId\":");
-        quoted(s, f[6], l[6]);
+        s = quoted(s, f[6], l[6]);
         lit(s, upd ? ",\"messageType\":\"UPDATE_ORDER\",\"orderId\":" : ",\"messageType\":\"CREATE_ORDER\",\"orderId\":");
-        quoted(s, f[5], l[5]);
+        s = quoted(s, f[5], l[5]);
         s.put('}');
         return;
     }
     const double q = a.quantity[i];
     uint32_t id_len = l[1];  // headers["origin_id"] = identifier.c_str()
+    BlockReader rd;
     for (uint32_t j = 0; j < id_len; ++j)
-        if (f[1][j] == 0) {
+        if (rd.at(f[1] + j) == 0) {
             id_len = j;
             break;
         }
@@ -448,34 +494,34 @@ __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, const uint8_t* c
     lit(s, "\",\"customer_id\":\"");
     dec_i64(s, a.customer_id[i]);
     lit(s, "\",\"ip_address\":\"10.37.62.251\",\"origin\":\"fix\",\"origin_id\":");
-    quoted(s, f[1], id_len);
+    s = quoted(s, f[1], id_len);
     lit(s, ",\"origin_name\":\"FIX_GATEWAY\"},\"message\":{\"action\":\"CREATE\",\"order_details\":{\"client_order_id\":");
-    quoted(s, f[0], l[0]);
+    s = quoted(s, f[0], l[0]);
     lit(s, ",\"order_type\":\"market\",\"quantity\":{\"token\":");
-    quoted(s, f[2], l[2]);
+    s = quoted(s, f[2], l[2]);
     lit(s, ",\"value\":");
-    fmt_g17(s, q);
+    s = fmt_g17(s, q);
     lit(s, "},\"quantity_value_str\":\"");
-    fmt_fixed6(s, q);
+    s = fmt_fixed6(s, q);
     lit(s, "\",\"side\":");
-    quoted(s, f[4], l[4]);
+    s = quoted(s, f[4], l[4]);
     lit(s, ",\"token_pair\":{\"base_token\":");
-    quoted(s, f[2], l[2]);
+    s = quoted(s, f[2], l[2]);
     lit(s, ",\"quote_token\":");
-    quoted(s, f[3], l[3]);
+    s = quoted(s, f[3], l[3]);
     lit(s, "}}}},\"msg_type\":\"D\",\"uuid\":");
-    quoted(s, f[0], l[0]);
+    s = quoted(s, f[0], l[0]);
     s.put('}');
 }
 
-__device__ inline void fields_of(const JsonArgs& a, uint64_t i, uint64_t base, const uint8_t* f[kFields],
+__device__ inline void fields_of(const JsonArgs& a, uint64_t i, uint64_t base, gu8* f[kFields],
                                  uint32_t l[kFields]) {
     for (uint32_t j = 0; j < kFields; ++j) {
         l[j] = a.str_len[kFields * i + j];
         if (a.str_off) {
-            f[j] = a.arena + a.str_off[kFields * i + j];
+            f[j] = (gu8*)(a.arena + a.str_off[kFields * i + j]);
         } else {
-            f[j] = a.arena + base;
+            f[j] = (gu8*)(a.arena + base);
             base += l[j];
         }
     }
@@ -500,7 +546,7 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
         a.sz[i] = 0;
         return;
     }
-    const uint8_t* f[kFields];
+    gu8* f[kFields];
     uint32_t l[kFields];
     fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
     CountSink c;
@@ -508,62 +554,91 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
     a.sz[i] = c.n;
 }
 
-// Writing launch: one wave per 64 Orders.  Their texts are contiguous in `out`, so each lane
-// writes its record into an LDS window (byte writes) and the wave then stores the window
-// with 16-byte coalesced stores; only the bytes of a record that does not fit the window go to
-// HBM straight from its lane.  Records past out_capacity are written by nobody.
+// Writing launch: one wave per 64 Orders.  Their texts are contiguous in `out`: the wave stages
+// them in an LDS window (one byte write per character), stores the window with 16-byte coalesced
+// stores and moves the window on to the first record not yet written, until every record is out.
+// Only a record larger than the window is written from its lane straight to HBM.  Records past
+// out_capacity are written by nobody.
 constexpr uint32_t kWWave = 64;
 #ifndef SBE_OJ_WIN
 #define SBE_OJ_WIN 24576
 #endif
 constexpr uint32_t kWin = SBE_OJ_WIN;  // bytes of LDS window per wave
 
+__device__ inline uint64_t wave_max(uint64_t v) {
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t t = __shfl_xor(v, d, kWWave);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWin ? kWin : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWin];
     const uint32_t lane = threadIdx.x;
-    const uint64_t r0 = (uint64_t)blockIdx.x * kWWave;
-    const uint64_t i = r0 + lane;
-    const uint64_t rend = r0 + kWWave < a.n ? r0 + kWWave : a.n;
-    const uint64_t o0 = a.out_off[r0];
-    // window origin: the 16-byte aligned address at or below out + o0 (LDS offset ≡ address mod 16)
-    const uint64_t skew = (uint64_t)((uintptr_t)(a.out + o0) & 15);
-    const uint64_t wbase = o0 - skew;  // output coordinate of win[0]
-    uint64_t my_end = o0;              // end of the bytes this lane may let the window store
-    if (i < rend) {
-        const uint64_t o = a.out_off[i], e = a.out_off[i + 1];
+    const uint64_t i = (uint64_t)blockIdx.x * kWWave + lane;
+    const bool live = i < a.n;
+    uint64_t o = 0, e = 0;
+    bool done = true;
+    gu8* f[kFields];
+    uint32_t l[kFields];
+    if (live) {
+        o = a.out_off[i];
+        e = a.out_off[i + 1];
         const bool fits = e <= a.cap;
         if (a.status) a.status[i] = fits ? SBE_JSON_OK : SBE_JSON_OVERFLOW;
+        done = !fits;
         if (fits) {
-            const uint8_t* f[kFields];
-            uint32_t l[kFields];
             fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-            const bool staged = e - wbase <= kWin;
-            ByteSink w(staged ? win + (o - wbase) : a.out + o);
-            order_text<kWhat>(w, a, i, f, l);
-            if (staged) my_end = e;
+            if (e - o > kWin - 16) {  // larger than any window: straight to HBM
+                HbmSink w((gw8*)(a.out + o));
+                order_text<kWhat>(w, a, i, f, l);
+                done = true;
+            }
         }
     }
-    // the window holds [o0, cend): the largest staged end over the wave
-    uint64_t cend = my_end;
+    uint64_t start = ~0ull;  // output coordinate of the first record still to stage
     for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t t = __shfl_xor(cend, d, kWWave);
-        cend = t > cend ? t : cend;
+        const uint64_t t = __shfl_xor(done ? ~0ull : o, d, kWWave);
+        start = t < start ? t : start;
     }
-    __syncthreads();
-    if (cend <= o0) return;
-    const uint64_t nch = (cend - wbase + 15) / 16;
-    for (uint64_t c = lane; c < nch; c += kWWave) {
-        const uint64_t x0 = wbase + 16 * c;  // output coordinate of this 16-byte chunk
-        if (x0 >= o0 && x0 + 16 <= cend) {
-            const uint4 v = *reinterpret_cast<const uint4*>(win + 16 * c);
-            __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(a.out + x0));
-            __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(a.out + x0) + 1);
-            __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(a.out + x0) + 2);
-            __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(a.out + x0) + 3);
-        } else {
-            for (uint64_t x = x0 < o0 ? o0 : x0; x < x0 + 16 && x < cend; ++x) a.out[x] = win[x - wbase];
+    start = done ? start : (o < start ? o : start);
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t t = __shfl_xor(start, d, kWWave);
+        start = t < start ? t : start;
+    }
+    while (start != ~0ull) {  // uniform: every lane holds the same start
+        const uint64_t wbase = start - (uint64_t)((uintptr_t)(a.out + start) & 15);  // win[0] ≡ out + wbase (mod 16)
+        uint64_t my_end = 0;
+        if (!done && e - wbase <= kWin) {
+            LdsSink w((lw8*)(win + (o - wbase)));
+            order_text<kWhat>(w, a, i, f, l);
+            done = true;
+            my_end = e;
         }
+        const uint64_t cend = wave_max(my_end);
+        __syncthreads();
+        const uint64_t nch = (cend - wbase + 15) / 16;
+        for (uint64_t c = lane; c < nch; c += kWWave) {
+            const uint64_t x0 = wbase + 16 * c;  // output coordinate of this 16-byte chunk
+            if (x0 >= start && x0 + 16 <= cend) {
+                const uint4 v = *reinterpret_cast<const uint4*>(win + 16 * c);
+                __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(a.out + x0));
+                __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(a.out + x0) + 1);
+                __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(a.out + x0) + 2);
+                __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(a.out + x0) + 3);
+            } else {
+                for (uint64_t x = x0 < start ? start : x0; x < x0 + 16 && x < cend; ++x) a.out[x] = win[x - wbase];
+            }
+        }
+        __syncthreads();
+        uint64_t nx = done ? ~0ull : o;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t t = __shfl_xor(nx, d, kWWave);
+            nx = t < nx ? t : nx;
+        }
+        start = nx;
     }
 }
 
