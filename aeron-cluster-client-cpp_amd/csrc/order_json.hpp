@@ -563,7 +563,12 @@ constexpr uint32_t kWWave = 64;
 #ifndef SBE_OJ_WIN
 #define SBE_OJ_WIN 24576
 #endif
+#ifndef SBE_OJ_DIRECT
+#define SBE_OJ_DIRECT 0
+#endif
 constexpr uint32_t kWin = SBE_OJ_WIN;  // bytes of LDS window per wave
+static_assert(kWin >= 4096, "the window must hold a typical record");
+constexpr bool kDirect = SBE_OJ_DIRECT != 0;  // A/B switch: every record straight to HBM
 
 __device__ inline uint64_t wave_max(uint64_t v) {
     for (int d = 32; d >= 1; d >>= 1) {
@@ -575,7 +580,7 @@ __device__ inline uint64_t wave_max(uint64_t v) {
 
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWin];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kDirect ? 16 : kWin];
     const uint32_t lane = threadIdx.x;
     const uint64_t i = (uint64_t)blockIdx.x * kWWave + lane;
     const bool live = i < a.n;
@@ -591,7 +596,7 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         done = !fits;
         if (fits) {
             fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-            if (e - o > kWin - 16) {  // larger than any window: straight to HBM
+            if (kDirect || e - o > kWin - 16) {  // larger than any window: straight to HBM
                 HbmSink w((gw8*)(a.out + o));
                 order_text<kWhat>(w, a, i, f, l);
                 done = true;
