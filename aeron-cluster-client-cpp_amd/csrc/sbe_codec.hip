@@ -2006,6 +2006,12 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
                 break;
             }
     }
+    // A/B override of the persistent grid (SBE_PACK_GRID=<workgroups>), read once
+    static const uint64_t g_env = [] {
+        const char* v = getenv("SBE_PACK_GRID");
+        return v ? (uint64_t)strtoull(v, nullptr, 10) : 0ull;
+    }();
+    if (g_env) g = g_env;
     // the pack kernel's tile_load adds at most one superblock total per lane per tile step:
     // G/128 + 1 <= 64
     if (g > (uint64_t)(kWave - 1) * kTilesPerSb) g = (uint64_t)(kWave - 1) * kTilesPerSb;
