@@ -311,10 +311,24 @@ __device__ inline int ndig9(uint32_t v) {  // decimal digits of 0 < v < 1e9
     return d;
 }
 
-__device__ inline uint32_t pow10u(int p) {
-    uint32_t r = 1;
-    while (p-- > 0) r *= 10;
-    return r;
+// The nine decimal digits of v < 1e9, most significant first (constant divisors: multiply-shift,
+// no runtime division).
+__device__ inline void split9(uint32_t v, uint8_t dg[9]) {
+#pragma unroll
+    for (int q = 8; q >= 0; --q) {
+        dg[q] = (uint8_t)(v % 10u);
+        v /= 10u;
+    }
+}
+
+// The last w (<= 9) digits of v, zero padded.
+template <class S>
+__device__ inline void put_digits(S& s, uint32_t v, int w) {
+    uint8_t dg[9];
+    split9(v, dg);
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+        if (q >= 9 - w) s.put((uint8_t)('0' + dg[q]));
 }
 
 // "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
@@ -362,10 +376,10 @@ __device__ __noinline__ S fmt_fixed6(S s, double v) {
     } else {
         dec_u64(s, x.lim[0]);
         for (int j = 1; j < x.nl; ++j)
-            for (uint32_t p = 100000000u; p; p /= 10) s.put((uint8_t)('0' + (x.lim[j] / p) % 10));
+            put_digits(s, x.lim[j], 9);
     }
     s.put('.');
-    for (uint32_t p = 100000u; p; p /= 10) s.put((uint8_t)('0' + (kept / p) % 10));
+    put_digits(s, kept, 6);
     return s;
 }
 
@@ -395,10 +409,13 @@ __device__ __noinline__ S fmt_g17(S s, double v) {
     int cnt = 0, X = 0;
     bool sticky = false;
     auto take = [&](uint32_t chunk, int width) {  // `width` digits of chunk, most significant first
-        for (int q = width - 1; q >= 0; --q) {
-            const uint32_t dg = (chunk / pow10u(q)) % 10;
-            if (cnt < 18) d[cnt++] = (uint8_t)dg;
-            else if (dg) sticky = true;
+        uint8_t dg[9];
+        split9(chunk, dg);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            if (q < 9 - width) continue;
+            if (cnt < 18) d[cnt++] = dg[q];
+            else if (dg[q]) sticky = true;
         }
     };
     if (x.nl) {
