@@ -66,9 +66,12 @@ struct HbmSink {
     __device__ void put(uint8_t b) { p[n++] = b; }
 };
 
-template <class S>
-__device__ inline void lit(S& s, const char* t) {
-    while (*t) s.put((uint8_t)*t++);
+// A literal run: the length is a compile-time constant, so the copy unrolls into immediate
+// stores at constant offsets from one address (no scalar character loop).
+template <class S, size_t N>
+__device__ inline void lit(S& s, const char (&t)[N]) {
+#pragma unroll
+    for (size_t k = 0; k + 1 < N; ++k) s.put((uint8_t)t[k]);
 }
 
 // jsoncpp json_writer.cpp utf8ToCodepoint (lead byte decides the length; continuation bytes are
@@ -175,14 +178,6 @@ __device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
     }
     s.put('"');
     return s;
-}
-
-template <class S>
-__device__ inline void key(S& s, const char* k) {
-    s.put('"');
-    lit(s, k);
-    s.put('"');
-    s.put(':');
 }
 
 template <class S>
@@ -394,7 +389,8 @@ __device__ __noinline__ S fmt_g17(S s, double v) {
     }
     const bool neg = (bits >> 63) != 0;
     if (__builtin_isinf(v)) {
-        lit(s, neg ? "-1e+9999" : "1e+9999");
+        if (neg) lit(s, "-1e+9999");
+        else lit(s, "1e+9999");
         return s;
     }
     if (neg) s.put('-');
@@ -493,7 +489,8 @@ __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFi
         const bool upd = eq_lit(f[7], l[7], "UPDATED") || eq_lit(f[7], l[7], "CANCELLED");
         lit(s, "{\"messageId\":");
         s = quoted(s, f[6], l[6]);
-        lit(s, upd ? ",\"messageType\":\"UPDATE_ORDER\",\"orderId\":" : ",\"messageType\":\"CREATE_ORDER\",\"orderId\":");
+        if (upd) lit(s, ",\"messageType\":\"UPDATE_ORDER\",\"orderId\":");
+        else lit(s, ",\"messageType\":\"CREATE_ORDER\",\"orderId\":");
         s = quoted(s, f[5], l[5]);
         s.put('}');
         return;
