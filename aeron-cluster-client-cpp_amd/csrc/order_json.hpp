@@ -146,8 +146,24 @@ __device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
     BlockReader rd;
     uint64_t i = 0;
     while (i < len) {
+        {  // the common case: a run of plain bytes inside the current 16-byte block (32-bit offsets)
+            (void)rd.at(p + i);  // loads the block holding p + i
+            uint32_t o = (uint32_t)((uintptr_t)(p + i) & 15);
+            const uint64_t left = len - i;
+            const uint32_t stop = left < 16 - o ? o + (uint32_t)left : 16;
+            const uint32_t o0 = o;
+            for (; o < stop; ++o) {
+                const uint32_t w = o < 8 ? (o < 4 ? rd.v.x : rd.v.y) : (o < 12 ? rd.v.z : rd.v.w);
+                const uint32_t b = (w >> (8 * (o & 3))) & 0xFF;
+                if (!(b >= 0x20 && b < 0x80 && b != '"' && b != '\\')) break;
+                s.put((uint8_t)b);
+            }
+            i += o - o0;
+            if (i >= len) break;
+            if (o == 16) continue;  // the block was all plain: next block
+        }
         const uint8_t c = (uint8_t)rd.at(p + i);
-        if (c >= 0x20 && c < 0x80 && c != '"' && c != '\\') {  // the common case
+        if (c >= 0x20 && c < 0x80 && c != '"' && c != '\\') {
             s.put(c);
             ++i;
             continue;
