@@ -227,6 +227,20 @@ struct Exact {
     int nl;            // 0 when I == 0
     uint32_t fw[35];   // fraction numerator, little-endian words (k bits)
     int nfw, k;
+    // Register mode for price-like values (k <= 64 and I < 1e17): I as u64 in two limbs l0 l1,
+    // F as one u64, digits through a 128-bit product.  The arrays above are then never touched
+    // (they live in scratch).
+    bool small;
+    uint64_t sI, sF;
+    uint32_t l0, l1;
+
+    __device__ void set_small_int(uint64_t ip) {
+        sI = ip;
+        nl = ip == 0 ? 0 : (ip >= kE9 ? 2 : 1);
+        l0 = nl == 2 ? (uint32_t)(ip / kE9) : (uint32_t)ip;
+        l1 = nl == 2 ? (uint32_t)(ip % kE9) : 0;
+    }
+    __device__ uint32_t limb(int j) const { return small ? (j == 0 ? l0 : l1) : lim[j]; }
 
     __device__ void init(double v) {
         const uint64_t bits = (uint64_t)__double_as_longlong(v) & ~(1ull << 63);
@@ -241,6 +255,20 @@ struct Exact {
         nl = 0;
         nfw = 0;
         k = 0;
+        small = false;
+        if (e < 0 && e >= -64) {
+            small = true;
+            k = -e;
+            sF = k >= 64 ? m : (m & ((1ull << k) - 1));
+            set_small_int(k >= 64 ? 0 : (m >> k));
+            return;
+        }
+        if (e >= 0 && e <= 10 && (m << e) < 100000000000000000ull) {
+            small = true;
+            sF = 0;
+            set_small_int(m << e);
+            return;
+        }
         if (e < 0) {
             k = -e;
             const uint64_t ip = k >= 64 ? 0 : (m >> k);
@@ -294,6 +322,7 @@ struct Exact {
     }
 
     __device__ bool frac_nonzero() const {
+        if (small) return sF != 0;
         uint32_t o = 0;
         for (int j = 0; j < nfw; ++j) o |= fw[j];
         return o != 0;
@@ -301,6 +330,12 @@ struct Exact {
 
     // The next nine fraction digits, as an integer < 1e9 (F ← F·1e9 mod 2^k).
     __device__ uint32_t frac_next9() {
+        if (small) {
+            if (k == 0) return 0;
+            const unsigned __int128 t = (unsigned __int128)sF * kE9;
+            sF = k == 64 ? (uint64_t)t : ((uint64_t)t & ((1ull << k) - 1));
+            return (uint32_t)(t >> k);
+        }
         if (nfw == 0) return 0;
         uint64_t carry = 0;
         for (int j = 0; j < nfw; ++j) {
@@ -370,7 +405,9 @@ __device__ __noinline__ S fmt_fixed6(S s, double v) {
     const bool up = rest > 500 || (rest == 500 && (x.frac_nonzero() || (kept & 1)));
     bool carry = false;
     if (up && ++kept == 1000000) kept = 0, carry = true;
-    if (carry) {  // add one to the integer limbs
+    if (carry && x.small) {
+        x.set_small_int(x.sI + 1);
+    } else if (carry) {  // add one to the integer limbs
         int j = x.nl - 1;
         for (; j >= 0; --j) {
             if (++x.lim[j] < kE9) break;
@@ -385,9 +422,9 @@ __device__ __noinline__ S fmt_fixed6(S s, double v) {
     if (x.nl == 0) {
         s.put('0');
     } else {
-        dec_u64(s, x.lim[0]);
+        dec_u64(s, x.limb(0));
         for (int j = 1; j < x.nl; ++j)
-            put_digits(s, x.lim[j], 9);
+            put_digits(s, x.limb(j), 9);
     }
     s.put('.');
     put_digits(s, kept, 6);
@@ -431,10 +468,10 @@ __device__ __noinline__ S fmt_g17(S s, double v) {
         }
     };
     if (x.nl) {
-        const int w0 = ndig9(x.lim[0]);
+        const int w0 = ndig9(x.limb(0));
         X = w0 - 1 + 9 * (x.nl - 1);
-        take(x.lim[0], w0);
-        for (int j = 1; j < x.nl; ++j) take(x.lim[j], 9);
+        take(x.limb(0), w0);
+        for (int j = 1; j < x.nl; ++j) take(x.limb(j), 9);
     } else {
         X = -1;
         uint32_t c;
