@@ -21,8 +21,10 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_scan.hpp>
+#include <rccl/rccl.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 
 #include "../../include/sbecodec.h"
@@ -207,27 +209,33 @@ constexpr int kSinkBytes = 16 * 64;
 #define SBE_OUT_AUX 2
 #endif
 
+// Record length modes of the TopicMessage encoders:
+//   kLenWire  the wire record, 34+Σlen (computeLength's E109 above 65534 B)
+//   kLenRef   SBEEncoder::encode_topic_message's 26+Σlen prefix (src/sbe_encoder.cpp:163-164)
+//   kLenPub   ClusterClient::publish_topic (src/cluster_client.cpp:1850-1857): wire length, each
+//             length taken mod 65536 by put*(const char*, std::uint16_t) (TopicMessage.h:515-529),
+//             no E109; the packed input still advances by the full lengths
+enum : int { kLenWire = 0, kLenRef = 1, kLenPub = 2 };
+
 // Sizes of record r: output bytes (0 on E109) and packed-input bytes (its strings, always).
-template <class LY, bool kTrunc>
-__device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t (&L)[5], uint32_t& out_b,
-                                          uint32_t& in_b, uint8_t& st) {
+template <class LY, int kLen>
+__device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t& out_b, uint64_t& in_b,
+                                          uint8_t& st) {
     uint32_t sum = 0;
+    uint64_t sum_in = 0;
     st = SBE_ENC_OK;
-#pragma unroll
-    for (int f = 0; f < 5; ++f) L[f] = 0;
     if (r < a.n) {
 #pragma unroll
-        for (int f = 0; f < LY::kNF; ++f) {
-            L[f] = a.str_len[LY::kNF * r + f];
-            sum += L[f];
+        for (int f = LY::kNF - 1; f >= 0; --f) {  // first failing field in wire order (TopicMessage.h:1396-1428)
+            const uint32_t L = a.str_len[LY::kNF * r + f];
+            sum += kLen == kLenPub ? (L & 0xffffu) : L;
+            sum_in += L;
+            if (kLen != kLenPub && L > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
         }
-#pragma unroll
-        for (int f = LY::kNF - 1; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
-            if (L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
     }
-    const uint32_t ovh = (uint32_t)LY::ovh(kTrunc);
+    const uint32_t ovh = (uint32_t)LY::ovh(kLen == kLenRef);
     out_b = (r < a.n && st == SBE_ENC_OK) ? ovh + sum : 0u;
-    in_b = r < a.n ? sum : 0u;
+    in_b = r < a.n ? sum_in : 0u;
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
@@ -243,7 +251,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
 // t+3072 of it (each load instruction of a wave then covers 1280 contiguous bytes of lengths); the
 // 32 records of a tile are 32 consecutive threads.  Tile sums go through LDS to one wave, which
 // writes the 128 tile prefixes and the superblock's totals.
-template <class LY, bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
     __shared__ uint64_t tl[2][kTilesPerSb];
     const int tid = threadIdx.x;
@@ -251,9 +259,10 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
 #pragma unroll
     for (int j = 0; j < kSbRec / kSbThreads; ++j) {
         const uint64_t r = sb * kSbRec + (uint64_t)j * kSbThreads + tid;
-        uint32_t L[5], ob, ib;
+        uint32_t ob;
+        uint64_t ib;
         uint8_t st;
-        rec_sizes<LY, kTrunc>(a, r, L, ob, ib, st);
+        rec_sizes<LY, kLen>(a, r, ob, ib, st);
         // per tile (kRpt consecutive lanes): sums via shuffles (input side in 64 bits: E109
         // records may carry up to 5 x 4 GiB of strings)
         uint32_t to = ob;
@@ -469,7 +478,9 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
     uint32_t len;                  // tile output bytes, clipped to the capacity (uniform)
     uint32_t agg_in;               // packed: staged-input limit, bytes from in_tile (uniform)
     uintptr_t in_tile;             // packed: absolute address of the tile's first input byte (uniform)
-    uintptr_t gsrc[5];             // gather mode: absolute string addresses
+    uintptr_t gsrc[5];             // gather mode (and kLenPub packed): absolute string addresses
+    bool wrapped;                  // kLenPub packed: some record's input strings are longer than its
+                                   // output ones (a length >= 65536): compose from gsrc (uniform)
 };
 
 // sb_next: the first superblock whose total this workgroup has not loaded yet (tiles come in
@@ -502,26 +513,31 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
 }
 
 // sp_out / sp_in: running totals of the superblocks before this workgroup's current tile
-template <class LY, bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, int kLen>
 __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
                                                uint64_t& sp_out, uint64_t& sp_in) {
     TileSt S;
     const int q = lane % kLpr, lead = lane - q;
     const uint64_t r = tile * kRpt + lane / kLpr;
     const bool valid = r < a.n;
-    uint64_t sum = 0;
+    uint64_t sum = 0, sum_in = 0;
     uint8_t st = SBE_ENC_OK;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-        S.L[f] = valid ? x.L[f] : 0u;
+        const uint32_t Lx = valid ? x.L[f] : 0u;
+        S.L[f] = kLen == kLenPub ? (Lx & 0xffffu) : Lx;
         sum += S.L[f];
+        sum_in += Lx;
     }
+    if (kLen != kLenPub) {
 #pragma unroll
-    for (int f = LY::kNF - 1; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
-        if (S.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
-    const uint32_t ovh = (uint32_t)LY::ovh(kTrunc);
+        for (int f = LY::kNF - 1; f >= 0; --f)  // first failing field in wire order (TopicMessage.h:1396-1428)
+            if (S.L[f] > SBE_VAR_MAX_LEN) st = (uint8_t)(SBE_ENC_E109_TOPIC + f);
+    }
+    const uint32_t ovh = (uint32_t)LY::ovh(kLen == kLenRef);
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
-    const uint64_t rec_in = (kPacked && valid) ? sum : 0ull;
+    const uint64_t rec_in = (kPacked && valid) ? sum_in : 0ull;
+    S.wrapped = kLen == kLenPub && kPacked && __ballot(sum_in != sum) != 0;
     sp_out += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull));
     if (kPacked) sp_in += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull));
     const uint64_t base_out = uniform64(sp_out + x.to);
@@ -534,7 +550,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     if (kPacked) {
         // every record of the tile encodable: input offsets follow the output ones (34 B apart
         // per record); otherwise (E109 / past the end) a 64-bit scan of the input sizes
-        if (__ballot(!(valid && st == SBE_ENC_OK)) == 0) {
+        if (__ballot(!(valid && st == SBE_ENC_OK)) == 0 && !S.wrapped) {
             const uint32_t ovh0 = ovh;
             S.in0 = S.rs - ovh0 * (uint32_t)(lane / kLpr);
             const uint64_t agg_in = agg_out - (uint64_t)ovh0 * kRpt;
@@ -570,6 +586,14 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     S.T0 = base_out;
     S.len = cap_rel;
     S.in_tile = reinterpret_cast<uintptr_t>(a.arena) + base_in;
+    if (kPacked && kLen == kLenPub) {  // string f of the record at its full-length input offset
+        uintptr_t g = S.in_tile + S.in0;
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+            S.gsrc[f] = g;
+            g += (valid && f < LY::kNF) ? x.L[f] : 0u;
+        }
+    }
     if (!kPacked) {
 #pragma unroll
         for (int f = 0; f < 5; ++f)
@@ -1136,7 +1160,7 @@ __device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, ui
     return W;
 }
 
-template <class LY, bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
@@ -1155,11 +1179,11 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
 
     uint64_t sb_next = 0, sp_out = 0, sp_in = 0;
     TileIn x = tile_load<LY, kPacked>(a, t, lane, sb_next);
-    TileSt S = tile_prepare<LY, kPacked, kTrunc>(a, x, t, lane, sp_out, sp_in);
+    TileSt S = tile_prepare<LY, kPacked, kLen>(a, x, t, lane, sp_out, sp_in);
     uint4 I[kStageRegs];
     const uintptr_t sink = reinterpret_cast<uintptr_t>(a.sink);
     Win W{0, kRpt, 0, 0, 0, sink, 0};
-    bool fast = kPacked && !tile_big(S, lane);
+    bool fast = kPacked && !S.wrapped && !tile_big(S, lane);
     if (fast) W = tile_window(S, 0, lane, sink);
     if (kPacked) {
         stage_issue(W.swb, W.nb, lane, I);
@@ -1182,10 +1206,10 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
             Wn = tile_window(S, W.rb, lane, sink);
             fast_n = true;
         } else if (have_next) {
-            Sn = tile_prepare<LY, kPacked, kTrunc>(a, x, tn, lane, sp_out, sp_in);
+            Sn = tile_prepare<LY, kPacked, kLen>(a, x, tn, lane, sp_out, sp_in);
             const uint64_t t2 = tn + G;
             x = tile_load<LY, kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
-            fast_n = kPacked && !tile_big(Sn, lane);
+            fast_n = kPacked && !Sn.wrapped && !tile_big(Sn, lane);
             if (fast_n) Wn = tile_window(Sn, 0, lane, sink);
         }
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
@@ -1204,7 +1228,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                 const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
                 uintptr_t sw = 0;
                 int32_t nbw = 0;
-                if (kPacked) {
+                if (kPacked && !S.wrapped) {
                     stage_range<LY>(S, wrel, lane, sw, nbw);
                     // I holds the next item's prefetch: stage this window in batches of 3 chunks
                     for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
@@ -1221,9 +1245,9 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                         }
                     }
                 }
-                if (kPacked) {
+                if (kPacked && !S.wrapped) {
                     pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
-                } else {
+                } else {  // gather mode, or a kLenPub tile whose outputs are shorter than its inputs
                     wsync();
                     compose<LY, false>(a, wout, win_in, S, wrel, we_rel, sw, nbw);
                 }
@@ -2272,6 +2296,29 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Gather of encoded shards to one rank: the {bytes, n} of every rank go round in
+// one ncclAllGather, then the shards move in one group of ncclSend / ncclRecv at the prefix
+// offsets, and the root rebases each received offset array by its shard's byte prefix.
+// ------------------------------------------------------------------------------------------
+__global__ void shard_size_put(uint64_t* dst, const uint64_t* out_off, uint64_t n, uint64_t cap) {
+    if (threadIdx.x == 0) {
+        dst[0] = out_off[n];
+        dst[1] = n;
+        dst[2] = cap;  // the root's receive capacity (0 elsewhere)
+        dst[3] = 0;
+    }
+}
+
+__global__ void u64_put(uint64_t* dst, uint64_t v) {
+    if (threadIdx.x == 0) *dst = v;
+}
+
+__global__ __launch_bounds__(256) void offsets_rebase(uint64_t* dst, const uint64_t* src, uint64_t count, uint64_t base) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) dst[i] = src[i] + base;
+}
+
 size_t frag_scan_temp(uint64_t n, hipStream_t s) {
     size_t t1 = 0, t2 = 0;
     (void)hipcub::DeviceScan::InclusiveScan(nullptr, t1, (FragScan*)nullptr, (FragScan*)nullptr, FragScanOp{}, n, s);
@@ -2296,13 +2343,13 @@ size_t enc_workspace_size(uint64_t n) {
     return (size_t)(16 * (tiles + sbs) + kSinkBytes + 16);
 }
 
-template <class LY, bool kPacked, bool kTrunc>
+template <class LY, bool kPacked, int kLen>
 void enc_launch_k(const EncArgs& a, uint64_t sbs, uint64_t tiles, hipStream_t s) {
-    const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<LY, kPacked, kTrunc>), tiles);
-    hipLaunchKernelGGL((sbe_enc_sums<LY, kPacked, kTrunc>), dim3((uint32_t)sbs), dim3(kSbThreads), 0, s, a);
+    const uint64_t grid = pack_grid(reinterpret_cast<const void*>(&sbe_enc_pack<LY, kPacked, kLen>), tiles);
+    hipLaunchKernelGGL((sbe_enc_sums<LY, kPacked, kLen>), dim3((uint32_t)sbs), dim3(kSbThreads), 0, s, a);
     hipEvent_t e0, e1;
     prof_slot(0, &e0, &e1);
-    hipExtLaunchKernelGGL((sbe_enc_pack<LY, kPacked, kTrunc>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL((sbe_enc_pack<LY, kPacked, kLen>), dim3((uint32_t)grid), dim3(kWave), 0, s, e0, e1, 0, a);
     prof_commit(0, e0);
 }
 
@@ -2311,8 +2358,9 @@ template <class LY>
 int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out, uint64_t out_capacity,
                uint64_t* out_off, uint8_t* status, void* workspace, size_t workspace_bytes, void* stream) {
     if (!out_off) return SBE_EINVAL;
-    if (flags & ~SBE_ENC_REF_TRUNCATE8) return SBE_EINVAL;
+    if (flags & ~(SBE_ENC_REF_TRUNCATE8 | SBE_ENC_PUBLISH_TOPIC)) return SBE_EINVAL;
     if (!LY::kTM && flags) return SBE_EINVAL;
+    if ((flags & SBE_ENC_PUBLISH_TOPIC) && ((flags & SBE_ENC_REF_TRUNCATE8) || LY::kPre)) return SBE_EINVAL;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
     if (!q.str_len || !q.ts || !q.arena || !out) return SBE_EINVAL;
@@ -2327,15 +2375,20 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
               out,     out_capacity, out_off, status, ws, ws + 2 * sbs * kTilesPerSb,
               reinterpret_cast<uint8_t*>(ws + 2 * sbs * (kTilesPerSb + 1))};
     const bool packed = q.str_off == nullptr;
-    const bool trunc = (flags & SBE_ENC_REF_TRUNCATE8) != 0;
-    if (LY::kTM) {
-        if (packed && !trunc) enc_launch_k<LY, true, false>(a, sbs, tiles, s);
-        else if (packed && trunc) enc_launch_k<LY, true, true>(a, sbs, tiles, s);
-        else if (!packed && !trunc) enc_launch_k<LY, false, false>(a, sbs, tiles, s);
-        else enc_launch_k<LY, false, true>(a, sbs, tiles, s);
+    const int len = (flags & SBE_ENC_REF_TRUNCATE8) ? kLenRef : (flags & SBE_ENC_PUBLISH_TOPIC) ? kLenPub : kLenWire;
+    if constexpr (LY::kTM) {
+        if (packed) {
+            if (len == kLenWire) enc_launch_k<LY, true, kLenWire>(a, sbs, tiles, s);
+            else if (len == kLenRef) enc_launch_k<LY, true, kLenRef>(a, sbs, tiles, s);
+            else if constexpr (LY::kPre == 0) enc_launch_k<LY, true, kLenPub>(a, sbs, tiles, s);
+        } else {
+            if (len == kLenWire) enc_launch_k<LY, false, kLenWire>(a, sbs, tiles, s);
+            else if (len == kLenRef) enc_launch_k<LY, false, kLenRef>(a, sbs, tiles, s);
+            else if constexpr (LY::kPre == 0) enc_launch_k<LY, false, kLenPub>(a, sbs, tiles, s);
+        }
     } else {
-        if (packed) enc_launch_k<LY, true, false>(a, sbs, tiles, s);
-        else enc_launch_k<LY, false, false>(a, sbs, tiles, s);
+        if (packed) enc_launch_k<LY, true, kLenWire>(a, sbs, tiles, s);
+        else enc_launch_k<LY, false, kLenWire>(a, sbs, tiles, s);
     }
     return record_hip(hipGetLastError());
 }
@@ -2561,6 +2614,134 @@ int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what
         hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_PUBLISH_HEADERS>, dim3(wblocks), dim3(oj::kWWave), 0, s, a);
     else
         hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_ORDER_PAYLOAD>, dim3(wblocks), dim3(oj::kWWave), 0, s, a);
+    return record_hip(hipGetLastError());
+}
+
+struct sbe_comm {
+    ncclComm_t nc = nullptr;
+    int world = 0, rank = 0;
+    uint64_t* d_mine = nullptr;   // {bytes, n, root capacity, 0} of this rank (device, 32 B)
+    uint64_t* d_all = nullptr;    // the same of every rank (device, 32 B per rank)
+    uint64_t* h_all = nullptr;    // pinned host copy of d_all
+};
+
+static int record_nccl(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return SBE_OK;
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, ncclGetErrorString(r));
+    return SBE_ECOMM;
+}
+
+int sbe_comm_unique_id(uint8_t id[SBE_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == SBE_COMM_ID_BYTES, "RCCL unique id size");
+    if (!id) return SBE_EINVAL;
+    ncclUniqueId u;
+    const int rc = record_nccl(ncclGetUniqueId(&u), "ncclGetUniqueId");
+    if (rc == SBE_OK) std::memcpy(id, &u, sizeof(u));
+    return rc;
+}
+
+int sbe_comm_init(sbe_comm** comm, int world, int rank, const uint8_t id[SBE_COMM_ID_BYTES]) {
+    if (!comm || !id || world < 1 || rank < 0 || rank >= world) return SBE_EINVAL;
+    *comm = nullptr;
+    sbe_comm* c = new sbe_comm;
+    c->world = world;
+    c->rank = rank;
+    int rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_mine), 32));
+    if (rc == SBE_OK) rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_all), 32 * (size_t)world));
+    if (rc == SBE_OK) rc = record_hip(hipHostMalloc(reinterpret_cast<void**>(&c->h_all), 32 * (size_t)world, 0));
+    if (rc == SBE_OK) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        rc = record_nccl(ncclCommInitRank(&c->nc, world, u, rank), "ncclCommInitRank");
+    }
+    if (rc != SBE_OK) {
+        sbe_comm_destroy(c);
+        return rc;
+    }
+    *comm = c;
+    return SBE_OK;
+}
+
+int sbe_comm_destroy(sbe_comm* c) {
+    if (!c) return SBE_OK;
+    int rc = SBE_OK;
+    if (c->nc) rc = record_nccl(ncclCommDestroy(c->nc), "ncclCommDestroy");
+    if (c->d_mine) (void)hipFree(c->d_mine);
+    if (c->d_all) (void)hipFree(c->d_all);
+    if (c->h_all) (void)hipHostFree(c->h_all);
+    delete c;
+    return rc;
+}
+
+int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t* out_off, uint64_t n,
+                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t* totals, void* stream) {
+    if (!c || !out_off || root < 0 || root >= c->world) return SBE_EINVAL;
+    const bool am_root = c->rank == root;
+    if (am_root && !dst_off) return SBE_EINVAL;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // 1. every rank's {bytes, n} and the root's capacity
+    hipLaunchKernelGGL(shard_size_put, dim3(1), dim3(64), 0, s, c->d_mine, out_off, n,
+                       am_root && dst ? dst_capacity : 0ull);
+    int rc = record_hip(hipGetLastError());
+    if (rc != SBE_OK) return rc;
+    rc = record_nccl(ncclAllGather(c->d_mine, c->d_all, 4, ncclUint64, c->nc, s), "ncclAllGather");
+    if (rc != SBE_OK) return rc;
+    rc = record_hip(hipMemcpyAsync(c->h_all, c->d_all, 32 * (size_t)c->world, hipMemcpyDeviceToHost, s));
+    if (rc == SBE_OK) rc = record_hip(hipStreamSynchronize(s));
+    if (rc != SBE_OK) return rc;
+    uint64_t total_b = 0, total_n = 0;
+    for (int r = 0; r < c->world; ++r) {
+        total_b += c->h_all[4 * r];
+        total_n += c->h_all[4 * r + 1];
+    }
+    if (totals) {
+        totals[0] = total_b;
+        totals[1] = total_n;
+    }
+    // every rank sees the root's capacity: a short root buffer stops all of them before any send
+    const uint64_t root_cap = c->h_all[4 * root + 2];
+    if (total_b > root_cap) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "gather: root buffer holds %llu of %llu bytes",
+                      (unsigned long long)root_cap, (unsigned long long)total_b);
+        return SBE_ENOSPC;
+    }
+    // 2. the shards and their offsets, in one group
+    rc = record_nccl(ncclGroupStart(), "ncclGroupStart");
+    if (rc != SBE_OK) return rc;
+    uint64_t base = 0, rbase = 0;
+    for (int r = 0; r < c->world && rc == SBE_OK; ++r) {
+        const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
+        if (r == c->rank && !am_root) {
+            if (b) rc = record_nccl(ncclSend(out, b, ncclUint8, root, c->nc, s), "ncclSend");
+            if (m && rc == SBE_OK) rc = record_nccl(ncclSend(out_off, m, ncclUint64, root, c->nc, s), "ncclSend");
+        } else if (am_root && r != root) {
+            if (b) rc = record_nccl(ncclRecv(dst + base, b, ncclUint8, r, c->nc, s), "ncclRecv");
+            if (m && rc == SBE_OK) rc = record_nccl(ncclRecv(dst_off + rbase, m, ncclUint64, r, c->nc, s), "ncclRecv");
+        }
+        base += b;
+        rbase += m;
+    }
+    const int rc_end = record_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    if (rc != SBE_OK) return rc;
+    if (rc_end != SBE_OK) return rc_end;
+    if (!am_root) return SBE_OK;
+    // 3. root: its own shard, the offset rebase, the closing offset
+    base = rbase = 0;
+    for (int r = 0; r < c->world; ++r) {
+        const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
+        if (r == root && b) rc = record_hip(hipMemcpyAsync(dst + base, out, b, hipMemcpyDeviceToDevice, s));
+        if (rc != SBE_OK) return rc;
+        if (m) {
+            const uint64_t blocks = (m + 255) / 256;
+            hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
+                               dst_off + rbase, r == root ? out_off : dst_off + rbase, m, base);
+            rc = record_hip(hipGetLastError());
+            if (rc != SBE_OK) return rc;
+        }
+        base += b;
+        rbase += m;
+    }
+    hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + total_n, total_b);
     return record_hip(hipGetLastError());
 }
 

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <iostream>
 #include <mutex>
 #include <stdexcept>
 
@@ -317,7 +318,9 @@ uint64_t clock_ns() {
 
 EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength length, bool session, int64_t term,
                        int64_t sess, uint64_t ts_default) {
-    const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8 : 0u;
+    const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8
+                         : length == EncodeLength::Publish   ? SBE_ENC_PUBLISH_TOPIC
+                                                             : 0u;
     return run_encode(
         msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
         [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; },
@@ -355,6 +358,33 @@ std::vector<std::uint8_t> SessionFrameEncoder::create_combined_message(const std
     if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
     if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
     return b.bytes;
+}
+
+static uint64_t now_nanos_sys() {  // include/aeron_cluster/protocol.hpp:31-34
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+std::vector<std::string> TopicPublisher::publish_topic_batch(const std::vector<TopicMessageFields>& msgs) {
+    const size_t n = msgs.size();
+    std::vector<std::string> uuids(n);
+    std::vector<TopicMessageFields> f(msgs);
+    for (size_t i = 0; i < n; ++i) {
+        uuids[i] = std::string("pub_") + std::to_string(now_nanos_sys());  // src/cluster_client.cpp:1818
+        f[i].uuid = uuids[i];
+        if (f[i].headers.empty()) f[i].headers = "{}";                     // :1821
+        f[i].timestamp = (int64_t)now_nanos_sys();                         // :1845
+    }
+    EncodedBatch b = encode_tm(f, EncodeLength::Publish, false, 0, 0, now_nanos_sys());
+    for (size_t i = 0; i < n; ++i) (void)offer_(b.bytes.data() + b.offsets[i], b.offsets[i + 1] - b.offsets[i]);
+    return uuids;
+}
+
+std::string TopicPublisher::publish_topic(std::string_view topic, std::string_view message_type,
+                                          std::string_view json_payload, std::string_view headers_json) {
+    TopicMessageFields m{topic, message_type, {}, json_payload, headers_json, 0};
+    return publish_topic_batch({m})[0];
 }
 
 std::uint32_t CommitManager::topic_to_id(const std::string& topic) {
@@ -448,10 +478,12 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
         q[i] = orders[i].quantity;
     }
     const size_t small = ((nlen + 7) & ~(size_t)7) + nnum;
-    const uint64_t cap = 12 * (uint64_t)arena + 700 * (uint64_t)n + 16;  // escapes ≤ 6x, strings used ≤ twice
+    // a record is at most ~800 B besides its strings (428 fixed, 316 for "%f" of a quantity near
+    // DBL_MAX, 24 for "%.17g", 34 for two integers); strings escape to <= 6x and appear <= twice.
+    // out_off always holds the full sizes, so a record past the capacity is redone below.
+    uint64_t cap = 12 * (uint64_t)arena + 900 * (uint64_t)n + 16;
     c.d_arena.need(arena + 16);
     c.d_len.need(small);
-    c.d_out.need(2 * cap);
     c.d_off.need(2 * (n + 1) * 8);
     c.d_st.need(2 * n);
     c.d_ws.need(sbe_order_json_workspace_size(n));
@@ -463,15 +495,23 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
                        d_cid, d_cid + n, reinterpret_cast<const double*>(d_cid + 2 * n)};
     for (int w = 0; w < 2; ++w) {
         EncodedBatch& b = w ? r.headers : r.payload;
-        uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
         uint64_t* off = static_cast<uint64_t*>(c.d_off.p) + w * (n + 1);
         uint8_t* st = static_cast<uint8_t*>(c.d_st.p) + w * n;
-        if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, out, cap, off, st,
-                                    c.d_ws.p, c.d_ws.cap, c.stream) != SBE_OK)
-            fail("sbe_order_to_json_batch");
-        hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
-        hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, c.stream), "D2H");
-        hip_check(hipStreamSynchronize(c.stream), "sync");
+        for (int attempt = 0;; ++attempt) {
+            c.d_out.need(2 * cap);
+            uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
+            if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, out, cap, off,
+                                        st, c.d_ws.p, c.d_ws.cap, c.stream) != SBE_OK)
+                fail("sbe_order_to_json_batch");
+            hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
+            hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, c.stream), "D2H");
+            hip_check(hipStreamSynchronize(c.stream), "sync");
+            if (b.offsets[n] <= cap || attempt > 0) break;
+            cap = b.offsets[n];  // the measured size: one rerun
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (b.status[i] != SBE_JSON_OK) throw std::runtime_error("sbecodec: order JSON record did not fit");
+        uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
         b.bytes.resize(b.offsets[n]);
         if (b.offsets[n]) {
             hip_check(hipMemcpyAsync(b.bytes.data(), out, b.offsets[n], hipMemcpyDeviceToHost, c.stream), "D2H");
@@ -621,11 +661,12 @@ MessageHandler::MessageHandler() = default;
 MessageHandler::~MessageHandler() = default;
 
 void MessageHandler::handleMessage(const ParseResult& result) {
-    // src/message_handler.cpp:10-16
+    // src/message_handler.cpp:10-16: std::cout << std::string, so every byte of the string is
+    // written (embedded NULs included), then std::endl
     if (result.success)
-        std::printf("[MessageHandler] Handled message: %s\n", result.message_type.c_str());
+        std::cout << "[MessageHandler] Handled message: " << result.message_type << std::endl;
     else
-        std::printf("[MessageHandler] Failed to handle message: %s\n", result.error_message.c_str());
+        std::cout << "[MessageHandler] Failed to handle message: " << result.error_message << std::endl;
 }
 
 void MessageHandler::on_egress(const std::uint8_t* data, std::size_t len) {

@@ -103,7 +103,9 @@ struct EncodedBatch {
 
 enum class EncodeLength {
     Reference,  // exactly what SBEEncoder::encode_topic_message returns (26+Σlen)
-    Wire        // the full wire record (34+Σlen), as ClusterClient::publish_topic emits
+    Wire,       // the full wire record (34+Σlen), computeLength's E109 above 65534 B
+    Publish     // ClusterClient::publish_topic's put*(const char*, int) calls (src/cluster_client.cpp:
+                // 1850-1854): wire length, each length mod 65536 with that many bytes, no E109
 };
 
 class SBEEncoder {
@@ -170,6 +172,27 @@ public:
 
 private:
     std::int64_t leadership_term_id_ = 0, cluster_session_id_ = 0;
+};
+
+// The raw ingress sink (ClusterClient::offer_ingress signature, include/aeron_cluster/cluster_client.hpp:409).
+using OfferFn = std::function<bool(const std::uint8_t* data, std::size_t len)>;
+
+// ClusterClient::publish_topic (src/cluster_client.cpp:1809-1864) minus the connection checks:
+// uuid = "pub_" + now_nanos() (:1818), headers "{}" when empty (:1821), timestamp now_nanos()
+// (:1845), sequenceNumber 0, the put*(const char*, int) length wrap (EncodeLength::Publish), and
+// the record handed to the offer_ingress-shaped sink (:1860).  Returns the uuid, as the reference
+// does whether or not the offer succeeded.
+class TopicPublisher {
+public:
+    explicit TopicPublisher(OfferFn offer) : offer_(std::move(offer)) {}
+    std::string publish_topic(std::string_view topic, std::string_view message_type, std::string_view json_payload,
+                              std::string_view headers_json);
+    // Batch form: one GPU launch for all records, offered in order; each message gets its own uuid
+    // and timestamp (msgs[i].uuid / .timestamp are ignored).  Returns the uuids.
+    std::vector<std::string> publish_topic_batch(const std::vector<TopicMessageFields>& msgs);
+
+private:
+    OfferFn offer_;
 };
 
 // include/aeron_cluster/commit_manager.hpp:17-24
@@ -245,9 +268,8 @@ struct OrderJsonBatch {
 };
 OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vector<std::string>& message_ids);
 
-// The raw ingress sink (ClusterClient::offer_ingress signature).  Feeds every encoded record of a
-// batch to it in order; returns the number accepted before the first refusal.
-using OfferFn = std::function<bool(const std::uint8_t* data, std::size_t len)>;
+// Feeds every encoded record of a batch to an offer_ingress-shaped sink in order; returns the
+// number accepted before the first refusal.
 std::size_t offer_batch(const EncodedBatch& batch, const OfferFn& offer);
 
 // true when a gfx950 device is usable (all entry points above need one).

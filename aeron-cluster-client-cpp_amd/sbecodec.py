@@ -30,8 +30,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 4
+ABI_VERSION = 5
 ENC_REF_TRUNCATE8 = 0x1
+ENC_PUBLISH_TOPIC = 0x2
 ENC_OK, ENC_OVERFLOW = 0, 6
 DEC_PARSE_MESSAGE, DEC_ON_EGRESS, DEC_LITE = 0, 1, 2
 TM_WIRE_OVERHEAD, TM_REF_OVERHEAD = 34, 26
@@ -52,7 +53,8 @@ ST_ERR_TM_E100, ST_ERR_ACK_SHORT = 25, 26
 ST_EG_ACK_SIMPLE, ST_EG_ACK, ST_EG_TM, ST_EG_NONE, ST_EG_THROW_E100 = 32, 33, 34, 35, 36
 FL_ID_DEFAULT, FL_PAYLOAD_DEFAULT, FL_HEADERS_E100, FL_SEQ_KEY, FL_WRAPPED, FL_SEQ_ESC = 1, 2, 4, 8, 16, 32
 
-_ERRORS = {0: "ok", -1: "EINVAL", -2: "EHIP", -3: "ENOSPC", -4: "ENODEV"}
+_ERRORS = {0: "ok", -1: "EINVAL", -2: "EHIP", -3: "ENOSPC", -4: "ENODEV", -5: "ECOMM"}
+COMM_ID_BYTES = 128
 
 
 class SbeError(RuntimeError):
@@ -137,6 +139,16 @@ def _load():
     lib.sbe_profile_enable.argtypes = [ctypes.c_int]
     lib.sbe_profile_read.restype = ctypes.c_int
     lib.sbe_profile_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    lib.sbe_comm_unique_id.restype = ctypes.c_int
+    lib.sbe_comm_unique_id.argtypes = [ctypes.c_void_p]
+    lib.sbe_comm_init.restype = ctypes.c_int
+    lib.sbe_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    lib.sbe_comm_destroy.restype = ctypes.c_int
+    lib.sbe_comm_destroy.argtypes = [ctypes.c_void_p]
+    lib.sbe_gather_encoded.restype = ctypes.c_int
+    lib.sbe_gather_encoded.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
     if lib.sbe_abi_version() != ABI_VERSION:
         _abi_mismatch()
     return lib
@@ -430,6 +442,11 @@ def reassemble(data, frag_off, flags, out=None, msg_off=None, workspace=None, st
     return Reassembled(out, msg_off, counts)
 
 
+# bytes per order of the default output bound (a record is at most ~800 B plus its escaped strings:
+# 428 fixed, 316 for a "%f" quantity near DBL_MAX, 24 for "%.17g", 34 for the two integers)
+ORDER_JSON_BOUND = 900
+
+
 @dataclass
 class OrderJson:
     out: torch.Tensor      # u8 text, record i = out[out_off[i]:out_off[i+1]]
@@ -459,10 +476,13 @@ def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=J
         if str_off.numel() != ORDER_FIELDS * n:
             raise SbeError("str_off must be [n][8]")
     dev = arena.device
+    grow = out is None  # a buffer this call owns may be regrown to the measured size
     if out is None:
-        cap = out_capacity if out_capacity is not None else 600 * n + 6 * 3 * int(arena.numel()) + 64
+        cap = out_capacity if out_capacity is not None else ORDER_JSON_BOUND * n + 6 * 3 * int(arena.numel()) + 64
         out = torch.empty(max(int(cap), 16), dtype=torch.uint8, device=dev)
     cap = int(out.numel()) if out_capacity is None else int(out_capacity)
+    if cap > out.numel():
+        raise SbeError(f"out_capacity {cap} exceeds the out tensor ({out.numel()} bytes)")
     if out_off is None:
         out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
     if status is None:
@@ -472,7 +492,72 @@ def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=J
         workspace = torch.empty(max(need, 16), dtype=torch.uint8, device=dev)
     b = _OrderBatch(_ptr(arena), _ptr(str_off) if str_off is not None else None, _ptr(str_len),
                     _ptr(customer_id), _ptr(timestamp), _ptr(quantity))
-    rc = lib().sbe_order_to_json_batch(ctypes.byref(b), n, what, _ptr(out), cap, _ptr(out_off), _ptr(status),
-                                       _ptr(workspace), workspace.numel(), _stream(stream))
-    _check(rc, "sbe_order_to_json_batch")
+
+    def run(o, c):
+        rc = lib().sbe_order_to_json_batch(ctypes.byref(b), n, what, _ptr(o), c, _ptr(out_off), _ptr(status),
+                                           _ptr(workspace), workspace.numel(), _stream(stream))
+        _check(rc, "sbe_order_to_json_batch")
+
+    run(out, cap)
+    if grow and n:  # out_off always holds the full sizes: one rerun at the measured size
+        total = int(out_off[n].item())
+        if total > cap:
+            out = torch.empty(total, dtype=torch.uint8, device=dev)
+            run(out, total)
     return OrderJson(out, out_off, status)
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-GPU gather of encoded shards over RCCL (sbe_gather_encoded)
+# ---------------------------------------------------------------------------------------------
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id, made on one rank and handed to every rank out of band."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().sbe_comm_unique_id(buf), "sbe_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """One rank's communicator for sbe_gather_encoded (collective creation on the current device)."""
+
+    def __init__(self, world: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise SbeError("communicator id must be 128 bytes")
+        self.world, self.rank = int(world), int(rank)
+        self._h = ctypes.c_void_p()
+        idbuf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _check(lib().sbe_comm_init(ctypes.byref(self._h), self.world, self.rank, idbuf), "sbe_comm_init")
+
+    def close(self):
+        if self._h:
+            _check(lib().sbe_comm_destroy(self._h), "sbe_comm_destroy")
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, dst_off=None, stream=None):
+    """Collective: every rank's encoded shard (out, out_off [n+1]) back to back on `root`, offsets
+    rebased.  The root passes dst (uint8, large enough for every shard) and dst_off (int64 [N+1]);
+    returns (dst[:bytes], dst_off, bytes, N) on the root and (None, None, bytes, N) elsewhere."""
+    out = _dev(out, torch.uint8, "out")
+    out_off = _dev(out_off, torch.int64, "out_off")
+    am_root = comm.rank == root
+    if am_root:
+        dst = _dev(dst, torch.uint8, "dst")
+        dst_off = _dev(dst_off, torch.int64, "dst_off")
+        if dst is None or dst_off is None:
+            raise SbeError("the root passes dst and dst_off")
+    totals = (ctypes.c_uint64 * 2)()
+    rc = lib().sbe_gather_encoded(comm._h, int(root), _ptr(out), _ptr(out_off), int(n),
+                                  _ptr(dst) if am_root else None, int(dst.numel()) if am_root else 0,
+                                  _ptr(dst_off) if am_root else None, totals, _stream(stream))
+    _check(rc, "sbe_gather_encoded")
+    nbytes, nrec = int(totals[0]), int(totals[1])
+    if am_root:
+        return dst[:nbytes], dst_off[: nrec + 1], nbytes, nrec
+    return None, None, nbytes, nrec

@@ -9,19 +9,25 @@ One step = one round trip of the hot path over one batch resident in HBM:
 Workload (BASELINE.json configs[1] extended to the metric's encode+decode): 1,000,000 fixed-256 B
 Order TopicMessages per GPU (seed 0x5EED0002 + rank), synthetic.
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL), records sharded by contiguous ranges,
-no data-path collective: weak scaling (the optional --gather leg times the RCCL gather of the
-encoded shards to rank 0 separately, never inside `value`).
+Multi-GPU: one process per GPU (torch.distributed, RCCL).  `--gpus N` outside a launcher starts
+N ranks through torch.distributed.run before touching the GPU.  The headline shards records by
+contiguous ranges with no data-path collective: weak scaling, `value` = all ranks' records ÷ the
+slowest rank's time.  The `config5` object (BASELINE.json configs[4]) is strong
+scaling: one 134,217,728-record fixed-256 batch split over the ranks with shard.shard_range,
+encode-only and encode + the RCCL gather of the encoded shards to rank 0 (sbe_gather_encoded),
+each with absolute rec/s and its fraction of the HBM / xGMI roofline.
 
-Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (algorithmic bytes per
-launch ÷ its average duration from HIP events on the launch stream) and the CPU baseline (the
-oracle restatement, OpenMP, timed on a bounded sample on rank 0).
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (SURVEY §8(d)'s
+algorithmic bytes per launch ÷ its average duration from HIP events on the launch stream) and the
+CPU baseline (the oracle restatement, OpenMP, timed on a bounded sample on rank 0 at N=1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,13 +38,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "aeron-cluster-client-cpp_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-import sbecodec  # noqa: E402
+import sbecodec  # noqa: E402  (lazy: the library loads on first use)
 
 METRIC = "SBE records encoded+decoded/sec (device-resident), 256 B Order msgs"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# algorithmic bytes per 256-B record
-ENC_BYTES = 222 + 20 + 8 + 256 + 8 + 1  # pack kernel: strings + lengths + ts read; record + out_off + status written
-DEC_BYTES = 256 + 8 + 2 + 8 + 8 + 40    # record + rec_off read; status,flags + hdr + ts + 5 views written
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+XGMI_ROOT_GBS = 7 * 153.0  # root ingress: 7 xGMI links x ~153 GB/s
+# algorithmic bytes per 256-B record, SURVEY §8(d) (the roofline figures):
+#   encode 8 ts + 10 lengths + 222 strings read + 256 record written; decode 256 record + 8
+#   rec_off read + 48 descriptor written
+ENC_BYTES = 496
+DEC_BYTES = 312
+# the same with what the kernels also move: u32 lengths (20 B, not 10), out_off + status written;
+# the decode descriptor as laid out here (58 B)
+ENC_BYTES_ALL = 222 + 20 + 8 + 256 + 8 + 1
+DEC_BYTES_ALL = 256 + 8 + 2 + 8 + 8 + 40
 
 
 def parse_args():
@@ -46,13 +59,15 @@ def parse_args():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--records", type=int, default=1_000_000, help="records per GPU")
+    p.add_argument("--records", type=int, default=1_000_000, help="records per GPU (headline)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0)")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-config5", action="store_true", help="skip the config-5 strong-scaling leg")
+    p.add_argument("--config5-records", type=int, default=134_217_728)
+    p.add_argument("--config5-steps", type=int, default=3)
     p.add_argument("--separate-seq", action="store_true",
                    help="sequence_number evaluation as its own launch (sbe_eval_sequence_numbers)")
-    p.add_argument("--gather", action="store_true", help="also time the RCCL gather of encoded shards")
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
     p.add_argument("--event-every", type=int, default=4,
                    help="HIP events on the pack / decode dispatches of every k-th timed step (0: none, "
@@ -64,6 +79,17 @@ def launched_distributed():
     """Started by torch.distributed.run (even at one process): RCCL is initialised, so a one-GPU
     run exercises the same barrier / max-over-ranks path the multi-GPU runs take."""
     return "LOCAL_RANK" in os.environ and "MASTER_ADDR" in os.environ
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: run this script under torch.distributed.run with N ranks, one
+    per GPU, as a child process (nothing here has touched the GPU), and exit with its status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def setup_dist(args):
@@ -107,8 +133,10 @@ def make_inputs(n, rank, dev):
 
 
 def cpu_baseline(n_sample, budget_s, threads):
-    """Oracle restatement (port of src/sbe_encoder.cpp encode + parse_message) on the host cores:
-    repeat the round trip over an n_sample-record slice of the same workload until budget_s."""
+    """Oracle restatement (a C port of src/sbe_encoder.cpp encode + parse_message) on the host
+    cores: repeat the round trip over an n_sample-record slice of the same workload until budget_s.
+    It is NOT the reference's own speed: the reference builds std::strings, runs jsoncpp and
+    evaluates DEBUG_LOG arguments per record, so this flatters the CPU."""
     import sbe_testlib as T
     arena, L, ts = T.fixed256_orders(n_sample)
     T.oracle_encode(arena[:222], L[:1], ts[:1])  # load/build
@@ -128,12 +156,97 @@ def cpu_baseline(n_sample, budget_s, threads):
     rt = run(threads, budget_s * 0.75)
     return dict(value=rt, unit="records/s", cores=threads, kind="port",
                 sample=f"{n_sample} fixed-256 records, encode+parse_message round trip repeated for "
-                       f"{budget_s:.0f} s (oracle/sbe_oracle.c, OpenMP {threads} threads; 1 thread: {r1:.4g} rec/s)",
-                value_1thread=r1)
+                       f"{budget_s:.0f} s (oracle/sbe_oracle.c, a C restatement, OpenMP {threads} threads; "
+                       f"1 thread: {r1:.4g} rec/s)",
+                value_1thread=r1,
+                reference_indicative={
+                    "note": "the reference's own functions, survey container (Xeon, 8 vCPU), BASELINE.md §2; "
+                            "the restatement runs without their std::string / jsoncpp / DEBUG_LOG costs",
+                    "encode_topic_message_1thread": "20-24 M rec/s",
+                    "parse_message_tm_1thread": "2.4-2.6 M rec/s (jsoncpp stubbed)",
+                    "parse_message_tm_8threads": "2.3 M rec/s"})
+
+
+def config5(args, world, rank, dev):
+    """BASELINE.json configs[4] / SURVEY §8(e): one config5_records fixed-256 batch split over the
+    ranks (shard.shard_range), encoded on every rank at once (no collective), then gathered to
+    rank 0 over RCCL with sbe_gather_encoded.  Strong scaling: the batch size is fixed."""
+    import shard
+    import sbe_testlib as T
+    N = args.config5_records
+    lo, hi = shard.shard_range(N, world, rank)
+    m = hi - lo
+    arena, L, ts = T.config5_shard(lo, hi, dev)
+    out = torch.empty(sbecodec.output_bound(m, int(arena.numel())), dtype=torch.uint8, device=dev)
+    out_off = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(max(m, 1), dtype=torch.uint8, device=dev)
+    ws = sbecodec.alloc_workspace(m, dev)
+
+    def enc():
+        sbecodec.encode_topic_batch(arena, L, ts, out=out, out_off=out_off, status=status, workspace=ws)
+
+    enc()
+    torch.cuda.synchronize()
+    reps = max(1, args.config5_steps)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc()
+    torch.cuda.synchronize()
+    barrier(world)
+    t_enc = max_over_ranks((time.perf_counter() - t0) / reps, world)
+    ok = int(out_off[m].item()) == 256 * m and int((status[:m] != 0).sum().item()) == 0
+    res = {"workload": "config5_fixed256_sharded", "records": N, "records_per_rank_max": -(-N // world),
+           "scaling": "strong", "split": "shard.shard_range (contiguous)",
+           "encode": {"seconds": t_enc, "records_per_s": N / t_enc,
+                      "GBps": N * ENC_BYTES / t_enc / 1e9,
+                      "frac_of_hbm_aggregate": N * ENC_BYTES / t_enc / 1e9 / (HBM_PEAK_GBS * world)}}
+    if world > 1:
+        g = shard.RcclGather()
+        dst = dst_off = None
+        if rank == 0:
+            dst = torch.empty(sbecodec.output_bound(N, 222 * N), dtype=torch.uint8, device=dev)
+            dst_off = torch.empty(N + 1, dtype=torch.int64, device=dev)
+        g.gather(out, out_off, m, root=0, dst=dst, dst_off=dst_off)  # warm the RCCL connections
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            enc()
+            _, _, nbytes, nrec = g.gather(out, out_off, m, root=0, dst=dst, dst_off=dst_off)
+        torch.cuda.synchronize()
+        barrier(world)
+        t_eg = max_over_ranks((time.perf_counter() - t0) / reps, world)
+        if rank == 0:
+            ok = ok and nbytes == 256 * N and nrec == N and int(dst_off[N].item()) == 256 * N
+            # spot check: the last record of each shard sits where a single-GPU encode puts it
+            for r in range(world):
+                a, b = shard.shard_range(N, world, r)
+                ok = ok and int(dst_off[b - 1].item()) == 256 * (b - 1)
+        into_root = 256 * (N - m) if rank == 0 else 0
+        into_root = int(max_over_ranks(float(into_root), world))
+        res["encode_gather"] = {"seconds": t_eg, "records_per_s": N / t_eg,
+                                "gather_seconds": max(t_eg - t_enc, 0.0),
+                                "GBps_into_root": into_root / max(t_eg - t_enc, 1e-9) / 1e9,
+                                "frac_of_xgmi_root_ingress": into_root / max(t_eg - t_enc, 1e-9) / 1e9 / XGMI_ROOT_GBS,
+                                "collective": "sbe_gather_encoded (ncclAllGather of sizes + grouped ncclSend/ncclRecv)"}
+        g.close()
+        del dst, dst_off
+    else:
+        res["encode_gather"] = {"seconds": t_enc, "records_per_s": N / t_enc,
+                                "note": "one GPU: the encoded batch already sits on the root"}
+    res["ok"] = bool(ok)
+    del arena, L, ts, out, out_off, status, ws
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
     args = parse_args()
+    if args.gpus > 1 and not launched_distributed():
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local = setup_dist(args)
     sbecodec.require_device()
     dev = torch.device("cuda", local)
@@ -198,7 +311,7 @@ def main():
     deck_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_DECODE)))
     sbecodec.profile_enable(0)
 
-    # informational, untimed: whole-call encode (sums + scan + pack) and decode times
+    # informational, untimed: whole-call encode (sums + pack) and decode times
     for k in range(args.steps):
         step(k)
     torch.cuda.synchronize()
@@ -207,44 +320,51 @@ def main():
     total = n * world * args.steps
     value = total / el
 
-    gather = None
-    if args.gather and world > 1:
-        gather = time_gather(out, out_off, n, world, rank, dev)
+    c5 = None
+    if not args.no_config5:
+        del arena, L, ts, out, dec, seq
+        torch.cuda.empty_cache()
+        c5 = config5(args, world, rank, dev)
 
     if rank == 0:
-        enc_gbs = n * ENC_BYTES / (enc_ms * 1e-3) / 1e9
-        dec_gbs = n * DEC_BYTES / (dec_ms * 1e-3) / 1e9
-        pack_gbs = n * ENC_BYTES / (pack_ms * 1e-3) / 1e9
-        deck_gbs = n * DEC_BYTES / (deck_ms * 1e-3) / 1e9
+        def gbs(b, ms):
+            return n * b / (ms * 1e-3) / 1e9
+
         if pack_ms >= deck_ms:
-            dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, ms=pack_ms, gbs=pack_gbs)
+            dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, bytes_all=ENC_BYTES_ALL,
+                       ms=pack_ms)
         else:
-            dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES, ms=deck_ms,
-                       gbs=deck_gbs)
+            dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES,
+                       bytes_all=DEC_BYTES_ALL, ms=deck_ms)
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
             cpu = cpu_baseline(min(n, 200_000), args.cpu_seconds, args.cpu_threads)
+        ach = gbs(dom["bytes_per_record"], dom["ms"])
         line = {
             "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": "roundtrip_fixed256_orders", "records_per_gpu": n, "record_bytes": 256,
                        "encode": "wire-correct TopicMessage, packed SoA input",
-                       "decode": "parse_message descriptors (views) + sequence_number evaluation", "parallelism": f"shard{world}"},
-            "roofline": {"bound": "hbm", "achieved": dom["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": dom["gbs"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
+                       "decode": "parse_message descriptors (views) + sequence_number evaluation",
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
                          "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"],
+                         "bytes_source": "SURVEY §8(d) algorithmic bytes per 256-B record",
+                         "achieved_incl_offsets": gbs(dom["bytes_all"], dom["ms"]),
+                         "bytes_per_record_incl_offsets": dom["bytes_all"],
                          "timing": (f"HIP events on the kernel's dispatch in every {args.event_every}th timed step"
                                     if args.event_every else "HIP events, untimed pass (diagnosis run)")},
-            "kernels": {"encode_ms": enc_ms, "encode_gbs": enc_gbs, "decode_ms": dec_ms, "decode_gbs": dec_gbs,
-                        "pack_ms": pack_ms, "pack_gbs": pack_gbs, "decode_kernel_ms": deck_ms,
-                        "decode_kernel_gbs": deck_gbs,
+            "kernels": {"encode_ms": enc_ms, "decode_ms": dec_ms, "pack_ms": pack_ms,
+                        "pack_gbs": gbs(ENC_BYTES, pack_ms), "decode_kernel_ms": deck_ms,
+                        "decode_kernel_gbs": gbs(DEC_BYTES, deck_ms),
                         "roundtrip_gbs": n * (ENC_BYTES + DEC_BYTES) / ((enc_ms + dec_ms) * 1e-3) / 1e9},
             "cpu_baseline": cpu,
         }
-        if gather is not None:
-            line["gather"] = gather
+        if c5 is not None:
+            line["config5"] = c5
         print(json.dumps(line), flush=True)
     if dist_on():
         import torch.distributed as dist
@@ -252,31 +372,15 @@ def main():
 
 
 def measured_traffic(kernel, n):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/gpu_counters.sh →
-    profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), scaled from the
-    records per launch it was measured at; None when no summary covers the kernel."""
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/traffic.json:
+    FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), scaled from the records per launch it
+    was measured at; None when no summary covers the kernel."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(path))[kernel]
     except (OSError, KeyError, ValueError):
         return None
     return d["bytes_per_launch"] * n / d["records"]
-
-
-def time_gather(out, out_off, n, world, rank, dev):
-    """RCCL gatherv of the encoded shards to rank 0 (grouped send/recv at prefix offsets)."""
-    sys.path.insert(0, os.path.join(ROOT, "aeron-cluster-client-cpp_amd"))
-    import shard
-    torch.cuda.synchronize()
-    barrier(world)
-    t0 = time.perf_counter()
-    g = shard.gather_encoded(out, out_off, n, root=0)
-    torch.cuda.synchronize()
-    barrier(world)
-    el = max_over_ranks(time.perf_counter() - t0, world)
-    nbytes = int(out_off[n].item()) * world
-    return {"seconds": el, "bytes": nbytes, "GBps_into_root": nbytes * (world - 1) / world / el / 1e9,
-            "ok": bool(g is not None) if rank == 0 else True}
 
 
 if __name__ == "__main__":

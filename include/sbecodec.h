@@ -43,6 +43,9 @@
  * sbe_order_to_json_batch()       Order::to_json src/order_types.cpp:122-181 and publish_order's
  *                                  headers JSON src/cluster_client.cpp:308-323 (the strings that
  *                                  become the TopicMessage payload / headers)
+ * sbe_gather_encoded()            no reference counterpart (its transport is Aeron,
+ *                                  src/session_manager.cpp:1180): the RCCL gather of encoded shards
+ *                                  to one ingress rank
  */
 #ifndef SBECODEC_H
 #define SBECODEC_H
@@ -54,7 +57,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 4
+#define SBECODEC_ABI_VERSION 5
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -92,6 +95,15 @@ extern "C" {
 #define SBE_ENC_REF_TRUNCATE8 0x1u /* emit exactly what SBEEncoder::encode_topic_message returns:
                                       buffer.resize(encodedLength()) keeps only the first
                                       26+Σlen bytes of the wire record (src/sbe_encoder.cpp:163-164) */
+#define SBE_ENC_PUBLISH_TOPIC 0x2u /* the encoder block of ClusterClient::publish_topic
+                                      (src/cluster_client.cpp:1823-1858): wire length, and the
+                                      put*(const char*, int) overloads (TopicMessage.h:515-529) that
+                                      take the length as std::uint16_t: a field of L bytes writes
+                                      length L mod 65536 followed by its first L mod 65536 bytes; no
+                                      E109 (computeLength is never called).  Topic batches only; not
+                                      with SBE_ENC_REF_TRUNCATE8.  The caller supplies the uuid
+                                      ("pub_" + now_nanos(), :1818) and "{}" for empty headers (:1821),
+                                      as the host mirror's publish_topic does. */
 
 /* Lite records: 8 header {12, template, 1, 1} + 12 block + nf x (u16 length + bytes), nf = 2
  * (301) or 3 (201, 202).  Wire overhead 20 + 2 nf; no truncation (8 + encodedLength() is the
@@ -325,6 +337,37 @@ size_t sbe_order_json_workspace_size(uint64_t n);
 int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what, uint8_t* out,
                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
                             size_t workspace_bytes, void* stream);
+
+/* ======================= multi-GPU gather of encoded shards (RCCL) ======================= */
+/* A batch sharded over the GPUs of one node (records [lo_r, hi_r) on rank r, contiguous, in rank
+ * order) is encoded per rank with no collective; sbe_gather_encoded then assembles on one rank the
+ * stream and offsets a single-GPU encode of the whole batch produces, over RCCL (xGMI inside a
+ * node).  The reference has no counterpart: its only transport is Aeron
+ * (src/session_manager.cpp:1180); the gathered stream is what one ingress publisher offers
+ * record by record (ClusterClient::offer_ingress, include/aeron_cluster/cluster_client.hpp:409).
+ * One process per GPU; a communicator serves one stream at a time. */
+#define SBE_ECOMM (-5)       /* an RCCL call failed (sbe_last_error names it) */
+#define SBE_COMM_ID_BYTES 128u
+typedef struct sbe_comm sbe_comm;
+
+/* A fresh communicator id (ncclGetUniqueId), made on one rank and passed to every rank out of band. */
+int sbe_comm_unique_id(uint8_t id[SBE_COMM_ID_BYTES]);
+/* Collective over the `world` processes: create this rank's communicator on the current HIP device. */
+int sbe_comm_init(sbe_comm** comm, int world, int rank, const uint8_t id[SBE_COMM_ID_BYTES]);
+int sbe_comm_destroy(sbe_comm* comm);
+
+/* Collective over the communicator.  Every rank passes its shard: out (its encoded stream, 16-B
+ * aligned) with out_off [n+1] (device u64, out_off[0] == 0) as sbe_encode_*_batch wrote them.
+ * The root receives the shards back to back in rank order into dst (dst_capacity bytes) and the
+ * rebased offsets into dst_off ([N+1] device u64, N = Σ n_r: record j of rank r at
+ * Σ_{q<r} bytes_q + out_off_r[j]); other ranks pass dst = dst_off = NULL.  totals (host u64[2], or
+ * NULL) = {Σ bytes, N} on every rank.  On `stream`: an all-gather of the ranks' {bytes, n}, one
+ * 32-B-per-rank device→host copy and a synchronisation of `stream` (the root sizes its receives
+ * from it), then one group of ncclSend / ncclRecv at the prefix offsets (RCCL has no gatherv) and
+ * the root's offset rebase; returns once those are enqueued.  SBE_ENOSPC (nothing sent) when the
+ * root's dst_capacity is too small. */
+int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint64_t* out_off, uint64_t n,
+                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t* totals, void* stream);
 
 /* ================================== profiling ================================== */
 /* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every

@@ -15,6 +15,8 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <string_view>
+#include <vector>
 
 #include "model/Acknowledgment.h"
 #include "model/CommitOffsetLite.h"
@@ -204,6 +206,47 @@ int ref_tm_encode(const uint8_t* const* s, const uint32_t* len, uint64_t ts, int
     if (n > cap) return 98;
     std::memcpy(out, buffer.data(), n);
     *out_len = n;
+    return 0;
+}
+
+// The encoder block of ClusterClient::publish_topic (src/cluster_client.cpp:1823-1858) in its call
+// order, with the protocol.hpp:8-12 constants: buffer of 8+8+Σ+128 zero bytes, MessageHeader
+// wrap(buf, 0, SBE_VERSION, size) and the four setters, TopicMessage wrapForEncode(buf, 8,
+// size - 8), timestamp, sequenceNumber(0), putX(const char*, static_cast<int>(size)) per field
+// (the int becomes put*'s std::uint16_t), resize to 8 + encodedLength().  uuid / headers are the
+// caller's ("pub_" + now_nanos(), "{}" for empty headers: :1818-1821).  Returns 0, or 2 if a
+// flyweight bounds check threw (never, for these buffer sizes).
+int ref_publish_topic(const uint8_t* const* s, const uint32_t* len, uint64_t ts, uint8_t* out, uint64_t cap,
+                      uint64_t* out_len) {
+    std::string_view f[5];
+    for (int i = 0; i < 5; ++i) f[i] = std::string_view(reinterpret_cast<const char*>(s[i]), len[i]);
+    std::vector<std::uint8_t> buf;
+    buf.resize(8 + 8 + f[0].size() + f[1].size() + f[2].size() + f[3].size() + f[4].size() + 128);
+    try {
+        sbe::MessageHeader hdr;
+        hdr.wrap(reinterpret_cast<char*>(buf.data()), 0, 1, static_cast<std::uint64_t>(buf.size()));
+        hdr.blockLength(16);
+        hdr.templateId(1);
+        hdr.schemaId(1);
+        hdr.version(1);
+        sbe::TopicMessage msg;
+        msg.wrapForEncode(reinterpret_cast<char*>(buf.data()), 8, static_cast<std::uint64_t>(buf.size() - 8));
+        msg.timestamp(ts);
+        msg.sequenceNumber(0);
+        msg.putTopic(f[0].data(), static_cast<int>(f[0].size()));
+        msg.putMessageType(f[1].data(), static_cast<int>(f[1].size()));
+        msg.putUuid(f[2].data(), static_cast<int>(f[2].size()));
+        msg.putPayload(f[3].data(), static_cast<int>(f[3].size()));
+        msg.putHeaders(f[4].data(), static_cast<int>(f[4].size()));
+        const int encodedLen = 8 + msg.encodedLength();
+        buf.resize(encodedLen);
+    } catch (const std::exception&) {
+        *out_len = 0;
+        return 2;
+    }
+    if (buf.size() > cap) return 98;
+    std::memcpy(out, buf.data(), buf.size());
+    *out_len = buf.size();
     return 0;
 }
 

@@ -36,9 +36,15 @@ uint64_t orc_to_nanos_auto(uint64_t ts) { return ts < 100000000000000ULL ? ts * 
  *   buffer.resize(encodedLength()) with encodedLength = position - m_offset and m_offset = 8
  *   (:281-284), i.e. the wire record minus its last 8 bytes.
  * ------------------------------------------------------------------------------------------ */
-uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len[5], uint64_t ts,
+uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len_in[5], uint64_t ts,
                         uint32_t flags, uint8_t* out, uint8_t* status) {
-    for (int f = 0; f < 5; ++f) {
+    /* SBE_ENC_PUBLISH_TOPIC: ClusterClient::publish_topic (src/cluster_client.cpp:1850-1854) calls
+     * putX(const char*, int); the int converts to the std::uint16_t parameter (TopicMessage.h:515),
+     * so length and copied bytes are L mod 65536 and computeLength (E109) is never called */
+    const int pub = (flags & SBE_ENC_PUBLISH_TOPIC) != 0;
+    uint32_t len[5];
+    for (int f = 0; f < 5; ++f) len[f] = pub ? (len_in[f] & 0xffffu) : len_in[f];
+    for (int f = 0; f < 5 && !pub; ++f) {
         if (len[f] > SBE_VAR_MAX_LEN) { /* TopicMessage.h:1396-1428 */
             if (status) *status = (uint8_t)(SBE_ENC_E109_TOPIC + f);
             return 0;
@@ -79,8 +85,10 @@ uint64_t orc_encode_one(const uint8_t* const s[5], const uint32_t len[5], uint64
  * nf u16-length-prefixed strings; the last `cut` bytes of the wire record are dropped
  * (REF_TRUNCATE8).  E109 on the first field above 65534 in wire order (computeLength). */
 static uint64_t enc_record(const uint8_t* lit, uint32_t nlit, int nf, const uint8_t* const* s,
-                           const uint32_t* len, uint32_t cut, uint8_t* out, uint8_t* status) {
-    for (int f = 0; f < nf; ++f) {
+                           const uint32_t* len_in, uint32_t cut, int wrap16, uint8_t* out, uint8_t* status) {
+    uint32_t len[5];
+    for (int f = 0; f < nf; ++f) len[f] = wrap16 ? (len_in[f] & 0xffffu) : len_in[f];
+    for (int f = 0; f < nf && !wrap16; ++f) {
         if (len[f] > SBE_VAR_MAX_LEN) {
             if (status) *status = (uint8_t)(SBE_ENC_E109_TOPIC + f);
             return 0;
@@ -113,6 +121,7 @@ enum { LAY_TM = 0, LAY_TM_SESSION = 1, LAY_LITE = 2 };
 typedef struct {
     int kind, nf;
     uint32_t cut, tmpl;
+    int wrap16; /* SBE_ENC_PUBLISH_TOPIC: lengths mod 65536, no E109 (see orc_encode_one) */
     int64_t term, sess;
     uint64_t ts_default;
     const uint64_t* ts;   /* timestamp / sequence */
@@ -170,8 +179,8 @@ static int encode_batch_lay(const layout_t* Ly, const uint8_t* arena, const uint
         uint64_t sum = 0;
         int bad = 0;
         for (int f = 0; f < nf; ++f) {
-            sum += L[f];
-            if (L[f] > SBE_VAR_MAX_LEN) bad = 1;
+            sum += Ly->wrap16 ? (L[f] & 0xffffu) : L[f];
+            if (!Ly->wrap16 && L[f] > SBE_VAR_MAX_LEN) bad = 1;
         }
         out_off[i] = acc;
         acc += bad ? 0 : ovh + sum;
@@ -200,7 +209,7 @@ static int encode_batch_lay(const layout_t* Ly, const uint8_t* arena, const uint
             }
             uint8_t lit[64], st;
             const uint32_t nlit = lay_prefix(Ly, i, lit);
-            enc_record(lit, nlit, nf, s, L, Ly->cut, out + out_off[i], &st);
+            enc_record(lit, nlit, nf, s, L, Ly->cut, Ly->wrap16, out + out_off[i], &st);
             if (status) status[i] = st;
         }
     }
@@ -210,7 +219,9 @@ static int encode_batch_lay(const layout_t* Ly, const uint8_t* arena, const uint
 int orc_encode_batch(const uint8_t* arena, const uint32_t* str_off, const uint32_t* str_len,
                      const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
                      uint8_t* out, uint64_t* out_off, uint8_t* status, int nthreads) {
-    layout_t Ly = {LAY_TM, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0, 0, 0, ts_default, timestamp, NULL};
+    if ((flags & SBE_ENC_PUBLISH_TOPIC) && (flags & SBE_ENC_REF_TRUNCATE8)) return -1;
+    layout_t Ly = {LAY_TM, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0, (flags & SBE_ENC_PUBLISH_TOPIC) != 0,
+                   0, 0, ts_default, timestamp, NULL};
     return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
 }
 
@@ -218,7 +229,8 @@ int orc_encode_session_batch(const uint8_t* arena, const uint32_t* str_off, cons
                              const uint64_t* timestamp, uint64_t n, uint64_t ts_default, uint32_t flags,
                              int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
                              uint64_t* out_off, uint8_t* status, int nthreads) {
-    layout_t Ly = {LAY_TM_SESSION, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0,
+    if (flags & SBE_ENC_PUBLISH_TOPIC) return -1;
+    layout_t Ly = {LAY_TM_SESSION, 5, (flags & SBE_ENC_REF_TRUNCATE8) ? 8u : 0u, 0, 0,
                    leadership_term_id, cluster_session_id, ts_default, timestamp, NULL};
     return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
 }
@@ -234,7 +246,7 @@ int orc_encode_lite_batch(const uint8_t* arena, const uint32_t* str_off, const u
                           int nthreads) {
     const int nf = lite_fields(template_id);
     if (!nf) return -1;
-    layout_t Ly = {LAY_LITE, nf, 0, template_id, 0, 0, 0, sequence, topic_id};
+    layout_t Ly = {LAY_LITE, nf, 0, template_id, 0, 0, 0, 0, sequence, topic_id};
     return encode_batch_lay(&Ly, arena, str_off, str_len, n, out, out_off, status, nthreads);
 }
 

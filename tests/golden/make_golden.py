@@ -73,6 +73,23 @@ def encode_cases():
     return cases
 
 
+def publish_cases():
+    """ClusterClient::publish_topic inputs: typical publishes (uuid "pub_<ns>", headers "{}" when the
+    caller's were empty) and every field at lengths 65534 / 65535 / 65536 / 70000 / 131073 (the
+    put*(const char*, int) overloads write the length mod 65536 and that many bytes)."""
+    cases = []
+    uid = b"pub_1760000000123456789"
+    cases.append(([b"orders", b"CREATE_ORDER", uid, b'{"side":"BUY","qty":"1"}', b"{}"], 1760000000123456789))
+    cases.append(([b"", b"", uid, b"", b"{}"], 1))
+    cases.append(([b"_subscriptions", b"SUBSCRIPTION", uid, b'{"topic":"orders"}', b'{"h":2}'], 2**64 - 1))
+    for L in (65534, 65535, 65536, 70000, 131073):
+        for k in range(5):
+            f = [b"orders", b"CREATE_ORDER", uid, b'{"a":1}', b"{}"]
+            f[k] = bytes([0x41 + k]) * L
+            cases.append((f, 7 + L))
+    return cases
+
+
 def main():
     if not T.ref_available():
         sys.exit("oracle/_ref/libsbe_ref_fw.so is missing: run `make -C oracle` with /root/reference present")
@@ -86,6 +103,16 @@ def main():
     json.dump({"source": "reference flyweights via oracle/_ref (SBEEncoder::encode_topic_message call order, "
                          "src/sbe_encoder.cpp:141-164; wire length per src/cluster_client.cpp:1857)",
                "cases": out}, open(os.path.join(HERE, "encode_ref.json"), "w"), indent=1)
+
+    pub = []
+    for fields, ts in publish_cases():
+        rc, rec = T.ref_publish(fields, ts)
+        assert rc == 0
+        pub.append({"fields": [field_spec(f) for f in fields], "ts": str(ts), "record": blob(rec)})
+    json.dump({"source": "reference flyweights via oracle/_ref (ClusterClient::publish_topic encoder block, "
+                         "src/cluster_client.cpp:1823-1858: MessageHeader setters, wrapForEncode(buf, 8, size-8), "
+                         "put*(const char*, int), 8 + encodedLength())",
+               "cases": pub}, open(os.path.join(HERE, "publish_ref.json"), "w"), indent=1)
 
     recs = T.edge_records()
     tm, ack, eg = [], [], []
@@ -109,7 +136,7 @@ def main():
                "cases": ack}, open(os.path.join(HERE, "ack_ref.json"), "w"), indent=1)
     json.dump({"source": src + " (MessageHandler::on_egress TopicMessage sequence, message_handler.hpp:47-60)",
                "cases": eg}, open(os.path.join(HERE, "egress_tm_ref.json"), "w"), indent=1)
-    print(f"encode {len(out)}, tm {len(tm)}, ack {len(ack)}, egress {len(eg)}")
+    print(f"encode {len(out)}, publish {len(pub)}, tm {len(tm)}, ack {len(ack)}, egress {len(eg)}")
     lite = lite_cases()
     json.dump({"source": src + " (CommitOffsetLite / OrderRequestLite / OrderNotificationLite: "
                                "build_commit_offset_message call order src/commit_manager.cpp:114-130 for encode; "

@@ -25,6 +25,7 @@ if PKG not in sys.path:
 
 # status / flag constants (include/sbecodec.h)
 ENC_REF_TRUNCATE8 = 1
+ENC_PUBLISH_TOPIC = 2
 ENC_OVERFLOW = 6
 DEC_PARSE, DEC_EGRESS, DEC_LITE = 0, 1, 2
 ST_LITE, ST_LITE_E100, ST_LITE_NOT_LITE = 48, 49, 50
@@ -240,6 +241,7 @@ def ref():
         L.ref_egress_tm.argtypes = [vp, u64, vp, vp]
         L.ref_lite_encode.argtypes = [ctypes.c_uint32, vp, vp, ctypes.c_uint32, u64, vp, u64, vp]
         L.ref_lite_decode.argtypes = [vp, u64, vp, vp, vp, vp]
+        L.ref_publish_topic.argtypes = [vp, vp, u64, vp, u64, vp]
         _ref = L
     return _ref
 
@@ -252,6 +254,20 @@ def ref_encode(fields, ts, wire):
     out = ctypes.create_string_buffer(cap)
     n = ctypes.c_uint64(0)
     rc = ref().ref_tm_encode(ptrs, lens, ts, 1 if wire else 0, out, cap, ctypes.byref(n))
+    return rc, out.raw[: n.value]
+
+
+def ref_publish(fields, ts):
+    """ClusterClient::publish_topic's encoder block (src/cluster_client.cpp:1823-1858) through the
+    reference flyweights: fields are (topic, type, uuid, payload, headers) as publish_topic passes
+    them to put*(const char*, int)."""
+    bufs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in fields]
+    ptrs = (ctypes.c_void_p * 5)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint32 * 5)(*[len(f) for f in fields])
+    cap = 34 + sum(len(f) for f in fields) + 16
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_uint64(0)
+    rc = ref().ref_publish_topic(ptrs, lens, ts, out, cap, ctypes.byref(n))
     return rc, out.raw[: n.value]
 
 
@@ -497,6 +513,61 @@ def fixed256_orders(n: int, seed: int = 0x5EED0002):
                           uuid, pay, np.tile(np.frombuffer(_HEADERS_T, np.uint8), (n, 1))], axis=1)
     str_len = np.tile(np.array([6, 12, 29, 143, 32], np.uint32), (n, 1))
     return rec.reshape(-1), str_len, ts
+
+
+CONFIG5_RECORDS = 134_217_728  # 128 M fixed-256 records (32 GiB encoded)
+CONFIG5_SEED = 0x5EED0005
+
+
+def _h31(i, k: int, seed: int):
+    """31-bit hash of record index i (int64 tensor) and field k, in int64 arithmetic that never
+    overflows (products of < 2^31 values by < 2^31 constants)."""
+    import torch
+    m = 0x7FFFFFFF
+    x = (i * 0x9E3779B1 + (k + 1) * 0x85EBCA77 + seed) & m
+    x = ((x ^ (x >> 15)) * 0x2C1B3C6D) & m
+    x = ((x ^ (x >> 12)) * 0x297A2D39) & m
+    return x ^ (x >> 15)
+
+
+def _digits_t(v, width: int):
+    import torch
+    p = torch.tensor([10 ** (width - 1 - k) for k in range(width)], dtype=torch.int64, device=v.device)
+    return ((v[:, None] // p[None, :]) % 10 + 48).to(torch.uint8)
+
+
+def config5_shard(lo: int, hi: int, device, seed: int = CONFIG5_SEED, chunk: int = 1 << 22):
+    """Records [lo, hi) of the config-5 batch, generated on `device` (torch ops, chunked): the
+    config-2 record shape (topic "orders", type "CREATE_ORDER", uuid msg_<19d ts>_<5d>, the
+    143-B order payload with qty / price / client_order_id digits, 32-B headers; Σlen = 222, wire
+    record 256 B), every byte a function of the GLOBAL record index, so any split into shards
+    concatenates to the same batch.  Returns packed SoA (arena uint8 [222 m], str_len int32 [m,5],
+    timestamp int64 [m])."""
+    import torch
+    m = hi - lo
+    arena = torch.empty((m, 222), dtype=torch.uint8, device=device)
+    tmpl = np.concatenate([np.frombuffer(b"orders", np.uint8), np.frombuffer(b"CREATE_ORDER", np.uint8),
+                           np.frombuffer(b"msg_" + b"0" * 19 + b"_" + b"0" * 5, np.uint8),
+                           np.frombuffer(_PAYLOAD_T, np.uint8), np.frombuffer(_HEADERS_T, np.uint8)])
+    tmpl_t = torch.from_numpy(tmpl.copy()).to(device)
+    hol = [47 + i for i, c in enumerate(_PAYLOAD_T) if c == ord("#")]
+    qty, price, cid = hol[:9], hol[9:20], hol[20:]
+    ts = torch.arange(lo, hi, dtype=torch.int64, device=device) + 1_760_000_000_000_000_000
+    for a in range(0, m, chunk):
+        b = min(m, a + chunk)
+        i = torch.arange(lo + a, lo + b, dtype=torch.int64, device=device)
+        blk = arena[a:b]
+        blk.copy_(tmpl_t.expand(b - a, 222))
+        blk[:, 22:41] = _digits_t(ts[a:b], 19)
+        blk[:, 42:47] = _digits_t(_h31(i, 0, seed) % 100_000, 5)
+        blk[:, qty[0]:qty[-1] + 1] = _digits_t(_h31(i, 1, seed) % 1_000_000_000, 9)
+        pv = (_h31(i, 2, seed) * 37 + _h31(i, 3, seed)) % 100_000_000_000
+        pd = _digits_t(pv, 11)
+        blk[:, price[0]:price[8] + 1] = pd[:, :9]
+        blk[:, price[9]:price[10] + 1] = pd[:, 9:]
+        blk[:, cid[0]:cid[-1] + 1] = _digits_t((_h31(i, 4, seed) * 0x80000000 + _h31(i, 5, seed)) % 10 ** 17, 17)
+    L = torch.tensor([6, 12, 29, 143, 32], dtype=torch.int32, device=device).expand(m, 5).contiguous()
+    return arena.reshape(-1), L, ts
 
 
 _TOPICS = [b"orders", b"order_request_topic", b"order_notification_topic"]

@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_side_entry_points(lib):
     lib.sbe_abi_version.restype = ctypes.c_int
-    assert lib.sbe_abi_version() == 4
+    assert lib.sbe_abi_version() == 5
     lib.sbe_encode_workspace_size.restype = ctypes.c_size_t
     lib.sbe_encode_workspace_size.argtypes = [ctypes.c_uint64]
     assert lib.sbe_encode_workspace_size(1_000_000) >= 16 * (1_000_000 // 256)
@@ -57,6 +57,18 @@ def test_host_side_entry_points(lib):
     assert lib.sbe_order_json_workspace_size(1000) >= 3 * 8 * 1001
     lib.sbe_last_error.restype = ctypes.c_char_p
     assert lib.sbe_last_error() == b""
+    # the RCCL gather's argument checks (no communicator is created without a device)
+    vp = ctypes.c_void_p
+    lib.sbe_comm_init.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, vp]
+    h = vp()
+    uid = ctypes.create_string_buffer(128)
+    assert lib.sbe_comm_init(ctypes.byref(h), 0, 0, uid) == -1
+    assert lib.sbe_comm_init(ctypes.byref(h), 2, 2, uid) == -1
+    assert lib.sbe_comm_init(None, 1, 0, uid) == -1
+    lib.sbe_gather_encoded.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp, vp]
+    assert lib.sbe_gather_encoded(None, 0, None, None, 0, None, 0, None, None, None) == -1
+    lib.sbe_comm_destroy.argtypes = [vp]
+    assert lib.sbe_comm_destroy(None) == 0
 
 
 def test_invalid_arguments_are_rejected_before_any_launch(lib):

@@ -108,6 +108,63 @@ def test_encode_edges(codec):
         check_encode(codec, arena, L, ts, flags=flags, ts_default=1_760_000_000_123)
 
 
+def _publish_lens(rng, n_small):
+    """Lengths of ClusterClient::publish_topic records: the u16 wrap edges on every field, mixed
+    into ordinary records so tiles hold both wrapped and plain records."""
+    lens = []
+    for L in (65534, 65535, 65536, 65537, 70000, 131072, 131073):
+        for k in range(5):
+            f = [6, 12, 23, int(rng.integers(0, 300)), 2]
+            f[k] = L
+            lens.append(f)
+    for _ in range(n_small):
+        lens.append([int(rng.integers(0, 30)), 12, 23, int(rng.integers(0, 500)), int(rng.integers(2, 40))])
+    rng.shuffle(lens)
+    return np.array(lens, np.uint32)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_encode_publish_topic(codec, gather):
+    """SBE_ENC_PUBLISH_TOPIC (src/cluster_client.cpp:1850-1857, TopicMessage.h:515-529): lengths mod
+    65536, no E109, wire length; packed and gather input."""
+    rng = np.random.default_rng(11)
+    L = _publish_lens(rng, 600)
+    n = len(L)
+    arena = rng.integers(0, 256, int(L.sum(dtype=np.int64)), dtype=np.uint8)
+    ts = rng.integers(1, 2**63, n, dtype=np.uint64)
+    if not gather:
+        check_encode(codec, arena, L, ts, flags=T.ENC_PUBLISH_TOPIC)
+        return
+    starts = np.zeros(n * 5 + 1, np.int64)
+    starts[1:] = np.cumsum(L.reshape(-1).astype(np.int64))
+    perm = rng.permutation(n * 5)
+    new = np.zeros(len(arena) + 3 * n * 5 + 5, np.uint8)
+    off = np.zeros(n * 5, np.uint32)
+    at = 5
+    for k in perm:
+        off[k] = at
+        new[at: at + starts[k + 1] - starts[k]] = arena[starts[k]: starts[k + 1]]
+        at += int(starts[k + 1] - starts[k]) + int(k % 3)
+    check_encode(codec, new, L, ts, str_off=off, flags=T.ENC_PUBLISH_TOPIC)
+
+
+def test_encode_publish_topic_plain_records(codec):
+    """Publish mode on records below 65536 B per field is the wire encoding (config-2 records)."""
+    arena, L, ts = T.fixed256_orders(64 * 37 + 5)
+    go, goff = check_encode(codec, arena, L, ts, flags=T.ENC_PUBLISH_TOPIC)
+    wo, woff, _ = T.oracle_encode(arena, L, ts)
+    assert np.array_equal(go, wo) and np.array_equal(goff, woff)
+
+
+def test_encode_publish_flag_rules(codec):
+    arena, L, ts = T.fixed256_orders(4)
+    a, Ld, t = to_dev(arena, torch.uint8), to_dev(L, torch.int32), to_dev(ts, torch.int64)
+    with pytest.raises(codec.SbeError):
+        codec.encode_topic_batch(a, Ld, t, flags=T.ENC_PUBLISH_TOPIC | T.ENC_REF_TRUNCATE8)
+    with pytest.raises(codec.SbeError):
+        codec.encode_session_batch(a, Ld, t, 1, 2, flags=T.ENC_PUBLISH_TOPIC)
+
+
 def test_encode_empty_batch(codec):
     out, off, st = gpu_encode(codec, np.zeros(0, np.uint8), np.zeros((0, 5), np.uint32), np.zeros(0, np.uint64))
     assert off.tolist() == [0] and out.size == 0

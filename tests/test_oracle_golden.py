@@ -50,6 +50,15 @@ def test_encode_matches_reference_flyweights(case):
         assert got_t == b"" and got_w == b""
 
 
+@pytest.mark.parametrize("case", load("publish_ref.json")["cases"], ids=lambda c: str(c["ts"]))
+def test_publish_topic_matches_reference_flyweights(case):
+    """SBE_ENC_PUBLISH_TOPIC against ClusterClient::publish_topic's own flyweight sequence
+    (src/cluster_client.cpp:1823-1858): lengths mod 65536, no E109."""
+    fields, ts = fields_of(case["fields"]), int(case["ts"])
+    got, st = encode_one(fields, ts, T.ENC_PUBLISH_TOPIC)
+    assert st == 0 and same(case["record"], got)
+
+
 def _records():
     return dict(T.edge_records())
 
