@@ -942,10 +942,38 @@ __device__ __forceinline__ int32_t zone_of(const RecEnt& E, int32_t X) {
     return (X >= E.z1) + (X >= E.z2) + (X >= E.z3) + (X >= E.z4);
 }
 
-// Every chunk of the lane from the staged input (chunks of not-staged records get don't-care
-// data, redone by chunk_pass_global).  Three phases so the LDS latency is paid once, not per
-// chunk: source offsets (walking the record table, next entry prefetched), all source reads,
-// then v_alignbyte + one ds_write_b128 per chunk.
+// Zone boundaries inside a chunk: for the chunk at record-relative X (its first byte in string
+// zone f0 = zone_of(X)), the starts z_f of strings f > f0 that fall on bytes 1..15 of the chunk
+// (before the record's composed end), as 4-bit byte offsets: nibble f-1 = z_f - X, 0 = none.  The
+// bytes from z_f on come from zone f (2 bytes further along the input per zone).
+__device__ __forceinline__ uint32_t zone_marks(const RecEnt& E, int32_t X) {
+    const int32_t last = min(X + 15, E.rend - E.rw - 1);
+    uint32_t m = 0;
+    m |= (E.z1 > X && E.z1 <= last) ? (uint32_t)(E.z1 - X) : 0u;
+    m |= (E.z2 > X && E.z2 <= last) ? (uint32_t)(E.z2 - X) << 4 : 0u;
+    m |= (E.z3 > X && E.z3 <= last) ? (uint32_t)(E.z3 - X) << 8 : 0u;
+    m |= (E.z4 > X && E.z4 <= last) ? (uint32_t)(E.z4 - X) << 12 : 0u;
+    return m;
+}
+
+// bytes b0..15 of v replaced by w's (b0 in 1..15): one v_bfi per dword
+__device__ __forceinline__ u32x4 merge_tail(u32x4 v, u32x4 w, int32_t b0) {
+    u32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int32_t t = b0 - 4 * j;
+        const uint32_t m = t <= 0 ? 0xffffffffu : (t >= 4 ? 0u : (0xffffffffu << (8 * t)));
+        r[j] = (v[j] & ~m) | (w[j] & m);
+    }
+    return r;
+}
+
+// Every chunk of the lane from the staged input, string bytes exact (chunks of not-staged records
+// get don't-care data, redone by chunk_pass_global; literal bytes are don't-care until the literal
+// pass).  Phases, so the LDS latency is paid a few times per window, not per chunk: source offsets
+// (walking the record table, next entry prefetched), all source reads, v_alignbyte, then the rare
+// chunks with a string start inside (zone_marks) merge their tail from the next zone, then one
+// ds_write_b128 per chunk.
 // Lane l owns the kk chunks [l kk, (l+1) kk) of the window: kk = 8 for a full window, fewer for
 // a window that carries less (kk a power of two, so a lane never straddles a padded 256-B row).
 __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk, int32_t wlen,
@@ -954,7 +982,9 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
     RecEnt N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
+    int32_t base[kCpl];  // p - sh0: the staged-input position of zone 0 for this chunk
     int32_t u[kCpl];
+    uint32_t zm[kCpl];
     const int32_t lb = lane << lg;  // the lane's first byte
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
@@ -967,7 +997,9 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
                 N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
             } while (p >= E.rend && r + 1 < kRpt);
         }
-        u[k] = p - E.sh0 - 2 * zone_of(E, p - E.rw);
+        base[k] = p - E.sh0;
+        u[k] = base[k] - 2 * zone_of(E, p - E.rw);
+        zm[k] = zone_marks(E, p - E.rw);
     }
     uint32_t d[kCpl][5];
 #pragma unroll
@@ -989,6 +1021,16 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
         v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
         v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
         v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
+        // string starts inside the chunk (a few chunks per record): later zones overwrite the tail
+        uint32_t m = zm[k];
+        while (__ballot(m != 0)) {
+            if (m) {
+                const int32_t nib = __builtin_ctz(m) >> 2;  // zone f = nib + 1
+                const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
+                m &= ~(15u << (4 * nib));
+                v = merge_tail(v, chunk_lds(inb, base[k] - 2 * (nib + 1), imax), b0);
+            }
+        }
         if (lb + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
@@ -1012,62 +1054,55 @@ __device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i3
         }
         if (!(E.z5 & kNotStaged)) continue;
         const int32_t X = p - E.rw;
-        const int32_t f = zone_of(E, X);
         const uint64_t s0 = sbase[r];
         const uint32_t nstr = (uint32_t)((E.z5 & ~kNotStaged) - LY::kOvh);
-        const u32x4 v = chunk_glb(s0 + (uint64_t)(int64_t)(X - LY::kS0 - 2 * f), s0 & ~3ull,
-                                  (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
+        const uint64_t lo4 = s0 & ~3ull, hi4 = (s0 + (nstr ? nstr - 1 : 0)) & ~3ull;
+        // string f's byte at record-relative x sits at s0 + x - kS0 - 2f
+        const int64_t at0 = (int64_t)X - LY::kS0;
+        u32x4 v = chunk_glb(s0 + (uint64_t)(at0 - 2 * zone_of(E, X)), lo4, hi4);
+        for (uint32_t m = zone_marks(E, X); m; ) {
+            const int32_t nib = __builtin_ctz(m) >> 2;
+            const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
+            m &= ~(15u << (4 * nib));
+            v = merge_tail(v, chunk_glb(s0 + (uint64_t)(at0 - 2 * (nib + 1)), lo4, hi4), b0);
+        }
         *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
 
-// string starts 1..4 inside a chunk: bytes [z_f, min(chunk end, end of string f)) from zone f
+// The literal words of one record: lit_word's inputs, small enough to pass by value.
+struct LitIn {
+    uint64_t ts;   // timestamp (default applied) / Lite sequence
+    int64_t term, sess;
+    uint32_t tid, tmpl;
+    uint32_t L[5];
+};
+
+// Dword j (compile-time after unrolling) of a record's literal prefix (see lit_word).
 template <class LY>
-__device__ __forceinline__ void fixup_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, const uint64_t* sbase,
-                                           const TileSt& S, int32_t wlen, int32_t nb, int lane) {
-    const int q = lane % kLpr, r = lane / kLpr;
-    if (!S.rec_out) return;
-    const RecEnt E = rec_load(rt, r);
-    const bool staged = !(E.z5 & kNotStaged);
-    const int32_t zend = E.z5 & ~kNotStaged;
-    const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
-    const int32_t imax = (nb + kInSlack) / 4 - 5;
-#pragma unroll
-    for (int j = 0; j < LY::kNF - 1; ++j) {
-        if (j % kLpr != q) continue;
-        const int f = j + 1;
-        const int32_t A = E.rw + zat(E, j);
-        const int32_t Lf = (j + 1 < LY::kNF - 1 ? zat(E, j + 1) - 2 : zend) - zat(E, j);  // length of string f
-        int32_t B = (A | 15) + 1;
-        if (A + Lf < B) B = A + Lf;
-        if (hi_all < B) B = hi_all;
-        const int32_t lo = A > 0 ? A : 0;
-        if ((A & 15) == 0 || lo >= B) continue;
-        const int32_t d0 = lo & ~3;
-        u32x4 v;
-        if (staged) {
-            v = chunk_lds(inb, d0 - E.sh0 - 2 * f, imax);
-        } else {
-            const uint64_t s0 = sbase[r];
-            const uint32_t nstr = (uint32_t)(zend - LY::kOvh);
-            v = chunk_glb(s0 + (uint64_t)(int64_t)(d0 - E.rw - LY::kS0 - 2 * f), s0 & ~3ull,
-                          (s0 + (nstr ? nstr - 1 : 0)) & ~3ull);
+__device__ __forceinline__ uint32_t lit_word_v(const LitIn& I, int j) {
+    if (j < LY::kPre / 4) {
+        switch (j) {
+            case 0: return SBE_SESSION_BLOCK_LEN | (SBE_SESSION_TEMPLATE_ID << 16);
+            case 1: return SBE_CLUSTER_SCHEMA_ID | (SBE_CLUSTER_SCHEMA_VERSION << 16);
+            case 2: return (uint32_t)(uint64_t)I.term;
+            case 3: return (uint32_t)((uint64_t)I.term >> 32);
+            case 4: return (uint32_t)(uint64_t)I.sess;
+            case 5: return (uint32_t)((uint64_t)I.sess >> 32);
+            default: return 0u;
         }
-        put_clip(wout, d0, v.x, lo, B);
-        put_clip(wout, d0 + 4, v.y, lo, B);
-        put_clip(wout, d0 + 8, v.z, lo, B);
-        put_clip(wout, d0 + 12, v.w, lo, B);
     }
+    j -= LY::kPre / 4;
+    if (j == 0) return (uint32_t)LY::kBlk | ((LY::kTM ? SBE_TM_TEMPLATE_ID : I.tmpl) << 16);
+    if (j == 1) return SBE_TOPIC_SCHEMA_ID | (1u << 16);
+    if (LY::kTM) return j == 2 ? (uint32_t)I.ts : (j == 3 ? (uint32_t)(I.ts >> 32) : 0u);
+    return j == 2 ? I.tid : (j == 3 ? (uint32_t)I.ts : (uint32_t)(I.ts >> 32));
 }
 
-// the literal prefix (lit_word) and the u16 lengths (TopicMessage.h:515-1231), clipped to the
-// window and the record's composed bytes
+// the literal prefix and the u16 lengths (TopicMessage.h:515-1231) of a record whose literal bytes
+// may be clipped by the window or the capacity: dword writes with byte-wise edges (rare, out of line)
 template <class LY>
-__device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, lds_i32* rt, const TileSt& S,
-                                             int32_t wlen, int lane) {
-    const int q = lane % kLpr, r = lane / kLpr;
-    if (!S.rec_out) return;
-    const RecEnt E = rec_load(rt, r);
+__device__ __noinline__ void literal_clip(lds_u8* wout, RecEnt E, LitIn I, int32_t wlen, int q) {
     const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
     const int32_t lo_all = E.rw > 0 ? E.rw : 0;
     if (q == 0) {
@@ -1076,7 +1111,7 @@ __device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, ld
         const int32_t hi = E.rw + LY::kLit < hi_all ? E.rw + LY::kLit : hi_all;
 #pragma unroll
         for (int j = 0; j <= kW; ++j) {
-            const uint32_t cur = j < kW ? lit_word<LY>(ea, S, j) : 0u, prv = j > 0 ? lit_word<LY>(ea, S, j - 1) : 0u;
+            const uint32_t cur = j < kW ? lit_word_v<LY>(I, j) : 0u, prv = j > 0 ? lit_word_v<LY>(I, j - 1) : 0u;
             const uint32_t v = a ? __builtin_amdgcn_alignbyte(cur, prv, 4u - (uint32_t)a) : cur;
             put_clip(wout, d0 + 4 * j, v, lo_all, hi);
         }
@@ -1085,16 +1120,67 @@ __device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, ld
 #pragma unroll
         for (int f = 0; f < LY::kNF; ++f) {
             const int32_t P = E.rw + (f == 0 ? LY::kLit : zat(E, f - 1) - 2);
-            const uint32_t L = S.L[f] & 0xffffu;
-            const int32_t lo = P > lo_all ? P : lo_all;
-            const int32_t hi = P + 2 < hi_all ? P + 2 : hi_all;
-            if (lo >= hi) continue;
-            if (lo == P && hi == P + 2 && (P & 1) == 0) {
-                *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wout + wout_addr(P)) = (uint16_t)L;
+            const uint32_t L = I.L[f] & 0xffffu;
+            if (P >= lo_all && P < hi_all) wout[wout_addr(P)] = (uint8_t)L;
+            if (P + 1 >= lo_all && P + 1 < hi_all) wout[wout_addr(P + 1)] = (uint8_t)(L >> 8);
+        }
+    }
+}
+
+// the 4 bytes of v at consecutive byte addresses from p
+__device__ __forceinline__ void put_b4(lds_u8* p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+// The literal prefix and the u16 lengths of every record of the window.  A record whose composed
+// bytes lie whole inside the window (the common case) writes them as byte stores (no alignment
+// assumption, no clipping; a dword that crosses a padded row goes byte by byte); others go through
+// literal_clip.
+template <class LY>
+__device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, lds_i32* rt, const TileSt& S,
+                                             int32_t wlen, int lane) {
+    const int q = lane % kLpr, r = lane / kLpr;
+    if (!S.rec_out) return;
+    const RecEnt E = rec_load(rt, r);
+    if (E.rend <= (E.rw > 0 ? E.rw : 0) || E.rw >= wlen) return;  // nothing of the record in this window
+    LitIn I;
+    I.ts = S.ts;
+    I.tid = S.tid;
+    I.term = ea.term_id;
+    I.sess = ea.sess_id;
+    I.tmpl = ea.tmpl;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) I.L[f] = S.L[f];
+    const bool whole = E.rw >= 0 && E.rend <= wlen && S.pe_rec == S.rs + S.rec_out;
+    if (!whole) {
+        literal_clip<LY>(wout, E, I, wlen, q);
+        return;
+    }
+    if (q == 0) {
+#pragma unroll
+        for (int j = 0; j < LY::kLit / 4; ++j) {
+            const uint32_t w = lit_word_v<LY>(I, j);
+            const int32_t x = E.rw + 4 * j;
+            if (((x ^ (x + 3)) >> 8) == 0) {
+                put_b4(wout + wout_addr(x), w);
             } else {
-                if (P >= lo && P < hi) wout[wout_addr(P)] = (uint8_t)L;
-                if (P + 1 >= lo && P + 1 < hi) wout[wout_addr(P + 1)] = (uint8_t)(L >> 8);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wout[wout_addr(x + k)] = (uint8_t)(w >> (8 * k));
             }
+        }
+    }
+    if (q == (kLpr > 1 ? 1 : 0)) {
+#pragma unroll
+        for (int f = 0; f < LY::kNF; ++f) {
+            // the length bytes inside the record's composed bytes (a REF_TRUNCATE8 record ends 8
+            // bytes short of the wire record, cutting trailing lengths)
+            const int32_t P = E.rw + (f == 0 ? LY::kLit : zat(E, f - 1) - 2);
+            const uint32_t L = I.L[f];
+            if (P < E.rend) wout[wout_addr(P)] = (uint8_t)L;
+            if (P + 1 < E.rend) wout[wout_addr(P + 1)] = (uint8_t)(L >> 8);
         }
     }
 }
@@ -1109,17 +1195,146 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
     static_assert(kCpl == 8, "chunk ownership sizes");
     const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);
     wsync();
-#ifndef SBE_ABL_NO_CHUNK
     chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
     if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, kk, lg, lane);
-#endif
     wsync();
-#ifndef SBE_ABL_NO_FIXUP
-    fixup_pass<LY>(wout, inb, rt, sbase, S, wlen, nb, lane);
-#endif
-#ifndef SBE_ABL_NO_LITERAL
     literal_pass<LY>(ea, wout, rt, S, wlen, lane);
-#endif
+}
+
+// ---- record-lane composition (the fast path) ---------------------------------------------
+// For a window holding whole, staged, unclipped records [ra, rb): lane 2j+q composes half of
+// record j's own chunks (the 16-byte chunks whose first byte lies in the record; a chunk's string
+// bytes always belong to that record, string bytes starting >= 26 B in): zone of the chunk's
+// first byte, five LDS dword reads and four v_alignbyte, later zones merged over the tail where a
+// string starts inside the chunk; then the record's literal bytes (session / SBE header, fixed
+// block, u16 lengths) as byte stores.  No record table, no walk: every lane works from its own
+// record's registers.
+static_assert(kLpr == 2, "record-lane composition splits a record between two lanes");
+
+// n literal bytes (dwords w) at window position x (padded rows: a run that reaches a row end
+// continues kRowPad bytes further)
+template <int N>
+__device__ __forceinline__ void put_lit(lds_u8* wout, int32_t x, const uint32_t* w) {
+    lds_u8* const b = wout + wout_addr(x);
+    const int32_t split = 256 - (x & 255);
+    if (split >= N) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) b[j + (j >= split ? kRowPad : 0)] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    }
+}
+
+template <class LY>
+__device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, const TileSt& S,
+                                                int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int lane,
+                                                int ra, int rb) {
+    const int q = lane % kLpr, r = lane / kLpr;
+    const bool live = S.rec_out != 0 && r >= ra && r < rb;
+    const int32_t rw = (int32_t)S.rs - wrel;  // record start in the window
+    const int32_t rl = (int32_t)S.rec_out;
+    const int64_t src0l = (int64_t)(S.in_tile + S.in0) - (int64_t)swb;  // staged position of string 0
+    uint32_t nstr = 0;
+#pragma unroll
+    for (int f = 0; f < LY::kNF; ++f) nstr += S.L[f];
+    const bool ok = !live || (src0l >= 0 && src0l + (int64_t)nstr <= (int64_t)nb && S.pe_rec == S.rs + S.rec_out &&
+                              rw >= 0 && rw + rl <= wlen);
+    if (__ballot(!ok)) return false;
+    const int32_t src0 = (int32_t)src0l - LY::kS0;  // input position of zone-0 byte x: src0 + x
+    // record-relative string starts z1..z4 (absent fields start at the end of the last string)
+    int32_t zs[5];
+    {
+        int32_t z = LY::kS0;
+#pragma unroll
+        for (int f = 1; f < 5; ++f) {
+            if (f < LY::kNF) z += (int32_t)S.L[f - 1] + 2;
+            zs[f - 1] = z;
+        }
+        zs[4] = z + (int32_t)S.L[LY::kNF - 1];
+#pragma unroll
+        for (int f = LY::kNF; f < 5; ++f) zs[f - 1] = zs[4];
+    }
+    const int32_t z1 = zs[0], z2 = zs[1], z3 = zs[2], z4 = zs[3];
+    // this lane's chunks: the first (q = 0) or second half of the record's own chunks
+    const int32_t c0 = (rw + 15) >> 4, nc = live ? ((rw + rl + 15) >> 4) - c0 : 0;
+    const int32_t h = (nc + 1) >> 1;
+    const int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
+    // records of > 256 B make some lanes loop longer than the window's other lanes (the chunk-owner
+    // passes of pack_window keep every lane at 8 chunks): those windows go there
+    if (__ballot(n_mine > kCpl)) return false;
+    const int32_t xlast = rl - 1;
+    const int32_t imax = (nb + kInSlack) / 4 - 5;
+    constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
+    for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
+        int32_t X[kG], u[kG];
+        uint32_t d[kG][5];
+#pragma unroll
+        for (int k = 0; k < kG; ++k) {
+            X[k] = 16 * (cb + i0 + k) - rw;
+            const int32_t f = (X[k] >= z1) + (X[k] >= z2) + (X[k] >= z3) + (X[k] >= z4);
+            u[k] = src0 + X[k] - 2 * f;
+            int32_t i = u[k] >> 2;
+            i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
+        }
+#pragma unroll
+        for (int k = 0; k < kG; ++k) {
+            const uint32_t sh = (uint32_t)u[k] & 3u;
+            u32x4 v;
+            v.x = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], sh);
+            v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
+            v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
+            v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
+            // a string starting on bytes 1..15 of the chunk (inside the record): merge the tail
+            const int32_t lim = min(X[k] + 15, xlast);
+            uint32_t m = 0;
+            m |= (z1 > X[k] && z1 <= lim) ? (uint32_t)(z1 - X[k]) : 0u;
+            m |= (z2 > X[k] && z2 <= lim) ? (uint32_t)(z2 - X[k]) << 4 : 0u;
+            m |= (z3 > X[k] && z3 <= lim) ? (uint32_t)(z3 - X[k]) << 8 : 0u;
+            m |= (z4 > X[k] && z4 <= lim) ? (uint32_t)(z4 - X[k]) << 12 : 0u;
+            const int32_t base = src0 + X[k];
+            while (__ballot(m != 0)) {
+                if (m) {
+                    const int32_t nib = __builtin_ctz(m) >> 2;  // zone nib + 1 from byte b0 on
+                    const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
+                    m &= ~(15u << (4 * nib));
+                    v = merge_tail(v, chunk_lds(inb, base - 2 * (nib + 1), imax), b0);
+                }
+            }
+            if (i0 + k < n_mine) {
+                const int32_t p = 16 * (cb + i0 + k);
+                *reinterpret_cast<lds_u32x4*>(wout + wout_addr(p)) = v;
+            }
+        }
+    }
+    wsync();
+    if (!live) return true;
+    // literal bytes: q = 0 the header prefix (TopicMessage.h:221-238, :362-437), q = 1 the lengths
+    // (:515-1231; a REF_TRUNCATE8 record ends 8 bytes short of the wire record, cutting trailing ones)
+    LitIn I;
+    I.ts = S.ts;
+    I.tid = S.tid;
+    I.term = ea.term_id;
+    I.sess = ea.sess_id;
+    I.tmpl = ea.tmpl;
+    if (q == 0) {
+        uint32_t w[LY::kLit / 4];
+#pragma unroll
+        for (int j = 0; j < LY::kLit / 4; ++j) w[j] = lit_word_v<LY>(I, j);
+        put_lit<LY::kLit>(wout, rw, w);
+    } else {
+#pragma unroll
+        for (int f = 0; f < LY::kNF; ++f) {
+            const int32_t P = f == 0 ? LY::kLit : zs[f - 1] - 2;
+            const uint32_t L = S.L[f];
+            if (P < rl) wout[wout_addr(rw + P)] = (uint8_t)L;
+            if (P + 1 < rl) wout[wout_addr(rw + P + 1)] = (uint8_t)(L >> 8);
+        }
+    }
+    return true;
 }
 
 // A tile whose output exceeds the window is split at record boundaries: window [ra, rb) holds
@@ -1215,7 +1430,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         // current window (fast) or the whole tile window by window
         if (fast) {
-            pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
+            if (!compose_records<LY>(a, wout, win_in, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
+                pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
 #ifndef SBE_ABL_NO_STORE
             store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, S.T0 + (int64_t)(W.wrel + W.wlen),

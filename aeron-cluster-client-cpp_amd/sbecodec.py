@@ -476,7 +476,7 @@ def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=J
         if str_off.numel() != ORDER_FIELDS * n:
             raise SbeError("str_off must be [n][8]")
     dev = arena.device
-    grow = out is None  # a buffer this call owns may be regrown to the measured size
+    grow = out is None and out_capacity is None  # a buffer this call sizes itself is regrown if short
     if out is None:
         cap = out_capacity if out_capacity is not None else ORDER_JSON_BOUND * n + 6 * 3 * int(arena.numel()) + 64
         out = torch.empty(max(int(cap), 16), dtype=torch.uint8, device=dev)

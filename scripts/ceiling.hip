@@ -1,0 +1,89 @@
+// ceiling.hip — achievable-bandwidth probe for the pack kernel's traffic shape (not product code).
+// Per 32-record tile: read 7,104 B (32 x 222 string bytes, contiguous), write 8,192 B (32 x 256),
+// i.e. the fixed-256 encode's 250 MB in / 256 MB out at 1 M records, with no composition work.
+// Variants: persistent grid (one wave per WG, tiles t += G) vs one WG per tile group; nt stores.
+// Build: hipcc --offload-arch=gfx950 -O3 -o ceiling scripts/ceiling.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                         \
+        }                                                                         \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kIn = 7104, kOut = 8192;
+constexpr int kInCh = (kIn + 15) / 16;  // 444 chunks
+constexpr int kOutCh = kOut / 16;       // 512 chunks
+
+template <int kAux, int kTilesPerWave>
+__global__ __launch_bounds__(256) void copy_tiles(const uint8_t* in, uint8_t* out, long tiles, long stride_tiles) {
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    for (long t0 = wave * kTilesPerWave; t0 < tiles; t0 += stride_tiles * kTilesPerWave) {
+#pragma unroll
+        for (int tt = 0; tt < kTilesPerWave; ++tt) {
+            const long t = t0 + tt;
+            if (t >= tiles) break;
+            const u32x4* src = reinterpret_cast<const u32x4*>(in + t * (long)kIn);
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int c = lane + 64 * k;
+                v[k] = c < kInCh ? src[c < kInCh - 1 ? c : kInCh - 1] : v[k > 0 ? k - 1 : 0];
+            }
+            uint8_t* dst = out + t * (long)kOut;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, kOut, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ (u32x4)(k), rs, 16 * (lane + 64 * k), 0, kAux);
+        }
+    }
+}
+
+template <int kAux, int kTpw>
+float run(const uint8_t* in, uint8_t* out, long tiles, int blocks, int threads, int reps) {
+    const long waves = (long)blocks * threads / 64;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((copy_tiles<kAux, kTpw>), dim3(blocks), dim3(threads), 0, 0, in, out, tiles, waves);
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((copy_tiles<kAux, kTpw>), dim3(blocks), dim3(threads), 0, 0, in, out, tiles, waves);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const long n = argc > 1 ? atol(argv[1]) : 1000000;
+    const long tiles = (n + 31) / 32;
+    uint8_t *in, *out;
+    CK(hipMalloc(&in, tiles * kIn + 64));
+    CK(hipMalloc(&out, tiles * kOut + 64));
+    CK(hipMemset(in, 1, tiles * kIn + 64));
+    const double bytes = (double)tiles * (kIn + kOut);
+    auto rep = [&](const char* name, float ms) {
+        std::printf("%-44s %8.1f us  %6.0f GB/s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+    };
+    for (int g : {1024, 2048, 4096}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "persistent 1-wave WGs G=%d nt", g);
+        rep(nm, run<2, 1>(in, out, tiles, g, 64, 20));
+        std::snprintf(nm, sizeof nm, "persistent 1-wave WGs G=%d default", g);
+        rep(nm, run<0, 1>(in, out, tiles, g, 64, 20));
+    }
+    rep("one wave per tile (64-thr WGs) nt", run<2, 1>(in, out, tiles, (int)tiles, 64, 20));
+    rep("one wave per tile (256-thr WGs) nt", run<2, 1>(in, out, tiles, (int)((tiles + 3) / 4), 256, 20));
+    rep("one wave per tile (256-thr WGs) default", run<0, 1>(in, out, tiles, (int)((tiles + 3) / 4), 256, 20));
+    rep("2 tiles per wave (256-thr WGs) nt", run<2, 2>(in, out, tiles, (int)((tiles + 7) / 8), 256, 20));
+    return 0;
+}

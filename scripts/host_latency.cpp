@@ -1,0 +1,90 @@
+// host_latency.cpp — per-call latency of the drop-in C++ mirror (host memory in, host memory out)
+// against the CPU restatement, for the reference's per-fragment call site
+// (MessageParser::parse_message at src/cluster_client.cpp:1185, one call per Aeron fragment) and
+// for batches.  Prints one JSON line per (operation, batch size): mirror µs per call, µs per record,
+// the oracle's µs per record on one host thread, and whether the GPU path is ahead.
+// Build + run (GPU box): make -C scripts host_latency && scripts/host_latency
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "aeron_cluster_amd.hpp"
+#include "../oracle/sbe_oracle.h"
+
+using namespace aeron_cluster;
+using clk = std::chrono::steady_clock;
+
+static double us_since(clk::time_point t0) {
+    return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+}
+
+int main() {
+    if (!gpu_codec_available()) {
+        std::fprintf(stderr, "no gfx950 device\n");
+        return 2;
+    }
+    const std::string topic = "orders", type = "CREATE_ORDER", uuid = "msg_1760000000000000000_00042";
+    const std::string payload(143, 'p'), headers(32, 'h');
+    // warm up the device context
+    for (int i = 0; i < 20; ++i) (void)SBEEncoder::encode_topic_message(topic, type, uuid, payload, headers, 1);
+    const std::vector<uint8_t> rec = SBEEncoder::encode_topic_batch(
+        {TopicMessageFields{topic, type, uuid, payload, headers, 1760000000000000000LL}}, EncodeLength::Wire).bytes;
+
+    // single-record calls: the reference's per-call surface
+    {
+        const int iters = 2000;
+        auto t0 = clk::now();
+        for (int i = 0; i < iters; ++i) (void)SBEEncoder::encode_topic_message(topic, type, uuid, payload, headers, 1);
+        const double enc = us_since(t0) / iters;
+        t0 = clk::now();
+        for (int i = 0; i < iters; ++i) (void)MessageParser::parse_message(rec.data(), rec.size());
+        const double par = us_since(t0) / iters;
+        t0 = clk::now();
+        for (int i = 0; i < iters; ++i) (void)decode_ack(rec.data(), rec.size());
+        const double ack = us_since(t0) / iters;
+        std::printf("{\"op\": \"single_call\", \"encode_topic_message_us\": %.2f, \"parse_message_us\": %.2f, "
+                    "\"decode_ack_us\": %.2f}\n", enc, par, ack);
+    }
+    // batches: mirror (stage + H2D + kernels + D2H + host materialisation) vs the oracle on one thread
+    for (size_t n : {1, 4, 16, 64, 256, 1024, 4096, 16384, 65536, 262144}) {
+        std::vector<TopicMessageFields> msgs(n, TopicMessageFields{topic, type, uuid, payload, headers, 1760000000000000000LL});
+        const int reps = n <= 1024 ? 200 : (n <= 16384 ? 20 : 4);
+        EncodedBatch b;
+        auto t0 = clk::now();
+        for (int r = 0; r < reps; ++r) b = SBEEncoder::encode_topic_batch(msgs, EncodeLength::Wire);
+        const double enc = us_since(t0) / reps;
+        t0 = clk::now();
+        for (int r = 0; r < reps; ++r) (void)MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), n);
+        const double dec = us_since(t0) / reps;
+        // oracle (CPU restatement, 1 thread) on the same records
+        std::vector<uint8_t> arena;
+        std::vector<uint32_t> lens;
+        std::vector<uint64_t> ts(n, 1760000000000000000ULL);
+        for (size_t i = 0; i < n; ++i)
+            for (const std::string* f : {&topic, &type, &uuid, &payload, &headers}) {
+                arena.insert(arena.end(), f->begin(), f->end());
+                lens.push_back((uint32_t)f->size());
+            }
+        std::vector<uint8_t> out(b.bytes.size() + 64), st(n), dst(n), dfl(n);
+        std::vector<uint64_t> off(n + 1), dts(n);
+        std::vector<uint16_t> dh(4 * n);
+        std::vector<uint32_t> vo(5 * n), vl(5 * n);
+        t0 = clk::now();
+        for (int r = 0; r < reps; ++r)
+            orc_encode_batch(arena.data(), nullptr, lens.data(), ts.data(), n, 0, 0, out.data(), off.data(), st.data(), 1);
+        const double cenc = us_since(t0) / reps;
+        t0 = clk::now();
+        for (int r = 0; r < reps; ++r)
+            orc_decode_batch(out.data(), off.data(), n, SBE_DEC_PARSE_MESSAGE, dst.data(), dfl.data(), dh.data(),
+                             dts.data(), vo.data(), vl.data(), 1);
+        const double cdec = us_since(t0) / reps;
+        std::printf("{\"op\": \"batch\", \"records\": %zu, \"mirror_encode_us\": %.1f, \"mirror_parse_us\": %.1f, "
+                    "\"oracle_encode_us\": %.1f, \"oracle_parse_us\": %.1f, \"mirror_rec_per_s\": %.4g, "
+                    "\"oracle_rec_per_s\": %.4g, \"gpu_ahead\": %s}\n",
+                    n, enc, dec, cenc, cdec, n / ((enc + dec) * 1e-6), n / ((cenc + cdec) * 1e-6),
+                    (enc + dec) < (cenc + cdec) ? "true" : "false");
+    }
+    return 0;
+}
