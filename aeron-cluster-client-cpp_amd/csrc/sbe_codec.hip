@@ -2272,17 +2272,23 @@ thread_local ProfRing g_prof[2];
 
 // The ring slot's (start, stop) events for this launch of `which`, or nulls when it is not
 // sampled.  They are handed to hipExtLaunchKernel, which timestamps the kernel's own dispatch.
+// The ring's events, created once (by sbe_profile_enable, outside any timed region).
+bool prof_ready(ProfRing& R) {
+    if (!R.ready) {
+        for (int i = 0; i < ProfRing::kCap; ++i)
+            for (int j = 0; j < 2; ++j)
+                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return false;
+        R.ready = true;
+    }
+    return true;
+}
+
 void prof_slot(int which, hipEvent_t* start, hipEvent_t* stop) {
     *start = *stop = nullptr;
     if (g_prof_every <= 0) return;
     ProfRing& R = g_prof[which];
     if (R.launches++ % (uint64_t)g_prof_every != 0) return;
-    if (!R.ready) {
-        for (int i = 0; i < ProfRing::kCap; ++i)
-            for (int j = 0; j < 2; ++j)
-                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return;
-        R.ready = true;
-    }
+    if (!prof_ready(R)) return;
     *start = R.ev[R.head][0];
     *stop = R.ev[R.head][1];
 }
@@ -2964,7 +2970,10 @@ int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t
 int sbe_profile_enable(int every) {
     if (every < 0) return SBE_EINVAL;
     g_prof_every = every;
-    for (auto& R : g_prof) R.head = R.count = 0, R.launches = 0;
+    for (auto& R : g_prof) {
+        R.head = R.count = 0, R.launches = 0;
+        if (every > 0 && !prof_ready(R)) return record_hip(hipGetLastError());
+    }
     return SBE_OK;
 }
 

@@ -69,7 +69,9 @@ def parse_args():
     p.add_argument("--separate-seq", action="store_true",
                    help="sequence_number evaluation as its own launch (sbe_eval_sequence_numbers)")
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
-    p.add_argument("--event-every", type=int, default=4,
+    p.add_argument("--settle-ms", type=float, default=60.0,
+                   help="untimed round trips before the warmup steps, until the GPU has run this long")
+    p.add_argument("--event-every", type=int, default=10,
                    help="HIP events on the pack / decode dispatches of every k-th timed step (0: none, "
                         "diagnosis only: kernel times then come from an extra untimed pass)")
     return p.parse_args()
@@ -282,16 +284,32 @@ def main():
         if k is not None:
             ev_dec[k][1].record(stream)
 
-    for _ in range(args.warmup):
-        step()
-    sbecodec.profile_enable(args.event_every)  # events on the pack / decode dispatches
     if args.verify:
+        step()
         torch.cuda.synchronize()
         import sbe_testlib as T
         eo, eoff, _ = T.oracle_encode(arena.cpu().numpy(), L.cpu().numpy().view(np.uint32),
                                       ts.cpu().numpy().view(np.uint64))
         assert np.array_equal(out_off.cpu().numpy().view(np.uint64), eoff)
         assert np.array_equal(out[: int(eoff[-1])].cpu().numpy(), eo)
+    # host-side setup before the warmup, so the GPU goes from the warmup steps straight into the
+    # timed ones: creating the profiling events takes ~1 ms of host time, during which an idle GPU
+    # lowers its clocks
+    sbecodec.profile_enable(args.event_every)  # events on the pack / decode dispatches
+    # settle: untimed round trips until the GPU has run the workload for settle_ms (its clocks ramp
+    # up over the first tens of milliseconds of sustained load; a 5-step warmup is ~1 ms), then the
+    # W warmup steps, then the timed K steps, with no host gap in between
+    settle_steps, t_set = 0, time.perf_counter()
+    while args.settle_ms > 0 and settle_steps < 1000:
+        for _ in range(10):
+            step()
+        settle_steps += 10
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t_set) * 1e3 >= args.settle_ms:
+            break
+    for _ in range(args.warmup):
+        step()
+    sbecodec.profile_enable(args.event_every)  # restart the rings: warmup launches are not sampled
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -348,7 +366,7 @@ def main():
             "config": {"workload": "roundtrip_fixed256_orders", "records_per_gpu": n, "record_bytes": 256,
                        "encode": "wire-correct TopicMessage, packed SoA input",
                        "decode": "parse_message descriptors (views) + sequence_number evaluation",
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world}", "settle": {"ms": args.settle_ms, "steps": settle_steps}},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
                          "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"],
