@@ -77,20 +77,55 @@ __device__ __forceinline__ uint4 lds_read_chunk_raw(const uint32_t* win, uint32_
 // ------------------------------------------------------------------------------------------
 // wave helpers
 // ------------------------------------------------------------------------------------------
+// Cross-lane steps on DPP (VALU data movement, no LDS round trip):
+//   row_shr:n (0x110 + n) within rows of 16 lanes; row_bcast:15 (0x142) / row_bcast:31 (0x143)
+//   carry lane 15 / lane 31 into the following rows; quad_perm (0x00-0xff) within quads.
+// update_dpp(old, src, ...) yields `old` (0 here) where the source lane is out of range or the
+// row is masked off, so the adds below are Hillis-Steele steps.
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, false);
+}
+
+// inclusive prefix sum over the 64 lanes
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane >= d) v += t;
-    }
+    (void)lane;
+    v += dpp0<0x111>(v);
+    v += dpp0<0x112>(v);
+    v += dpp0<0x114>(v);
+    v += dpp0<0x118>(v);
+    v += dpp0<0x142, 0xa>(v);
+    v += dpp0<0x143, 0xc>(v);
     return v;
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+// the same on 64-bit values (lo / hi halves with the carries of the lo adds)
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ uint64_t dpp_add64(uint64_t v) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    const uint32_t tlo = dpp0<kCtrl, kRowMask>(lo), thi = dpp0<kCtrl, kRowMask>(hi);
+    const uint32_t nlo = lo + tlo;
+    return ((uint64_t)(hi + thi + (nlo < lo ? 1u : 0u)) << 32) | nlo;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
+    (void)lane;
+    v = dpp_add64<0x111>(v);
+    v = dpp_add64<0x112>(v);
+    v = dpp_add64<0x114>(v);
+    v = dpp_add64<0x118>(v);
+    v = dpp_add64<0x142, 0xa>(v);
+    v = dpp_add64<0x143, 0xc>(v);
     return v;
 }
+
+// lane-uniform value of lane `l` (l uniform)
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+// sum over the 64 lanes, uniform
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) { return lane_u64(wave_incl_scan64(v, 0), kWave - 1); }
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -238,14 +273,6 @@ __device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t
     in_b = r < a.n ? sum_in : 0u;
 }
 
-__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint64_t t = __shfl_up(v, d, kWave);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
 
 // K1: superblock sb = records [4096 sb, 4096 (sb+1)).  Thread t takes records t, t+1024, t+2048,
 // t+3072 of it (each load instruction of a wave then covers 1280 contiguous bytes of lengths); the
@@ -517,7 +544,7 @@ template <class LY, bool kPacked, int kLen>
 __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
                                                uint64_t& sp_out, uint64_t& sp_in) {
     TileSt S;
-    const int q = lane % kLpr, lead = lane - q;
+    const int q = lane % kLpr;
     const uint64_t r = tile * kRpt + lane / kLpr;
     const bool valid = r < a.n;
     uint64_t sum = 0, sum_in = 0;
@@ -538,14 +565,15 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum_in : 0ull;
     S.wrapped = kLen == kLenPub && kPacked && __ballot(sum_in != sum) != 0;
-    sp_out += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull));
-    if (kPacked) sp_in += uniform64(wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull));
+    sp_out += wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull);
+    if (kPacked) sp_in += wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull);
     const uint64_t base_out = uniform64(sp_out + x.to);
     const uint64_t base_in = kPacked ? uniform64(sp_in + x.ti) : 0ull;
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
-    const uint32_t agg_out = __builtin_amdgcn_readfirstlane(__shfl(inc_out, kWave - 1, kWave));
-    S.rs = __shfl(inc_out - lo_out, lead, kWave);
+    const uint32_t agg_out = lane_u32(inc_out, kWave - 1);
+    static_assert(kLpr == 2, "record lead lane via quad_perm [0,0,2,2]");
+    S.rs = dpp0<0xa0>(inc_out - lo_out);  // the lead (even) lane's value
     S.rec_out = rec_out;
     if (kPacked) {
         // every record of the tile encodable: input offsets follow the output ones (34 B apart
@@ -558,9 +586,10 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
         } else {
             const uint64_t lo_in = q == 0 ? rec_in : 0ull;
             const uint64_t inc_in = wave_incl_scan64(lo_in, lane);
-            const uint64_t agg_in = uniform64(__shfl(inc_in, kWave - 1, kWave));
+            const uint64_t agg_in = lane_u64(inc_in, kWave - 1);
             S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
-            S.in0 = __shfl(inc_in - lo_in, lead, kWave);
+            const uint64_t ex = inc_in - lo_in;
+            S.in0 = ((uint64_t)dpp0<0xa0>((uint32_t)(ex >> 32)) << 32) | dpp0<0xa0>((uint32_t)ex);
         }
     } else {
         S.agg_in = 0;
@@ -614,8 +643,8 @@ __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int l
     const int q = lane % kLpr;
     const uint64_t mine = __ballot(q == 0 && S.rec_out && S.rs <= g && g < S.rs + S.rec_out);
     const int ra = mine ? __builtin_ctzll(mine) : 0;
-    const uint32_t ra_rs = __builtin_amdgcn_readfirstlane(__shfl(S.rs, ra, kWave));
-    const uint64_t ra_in = uniform64(__shfl(S.in0, ra, kWave));
+    const uint32_t ra_rs = lane_u32(S.rs, ra);
+    const uint64_t ra_in = lane_u64(S.in0, ra);
     const uint32_t p = g - ra_rs;
     const uintptr_t first = S.in_tile + ra_in + (p > (uint32_t)LY::kOvh ? p - (uint32_t)LY::kOvh : 0);
     swb = first & ~(uintptr_t)15;
@@ -1358,16 +1387,16 @@ __device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, ui
     Win W;
     const int q = lane % kLpr, r = lane / kLpr;
     W.ra = ra;
-    W.A = __builtin_amdgcn_readfirstlane(__shfl(S.rs, ra * kLpr, kWave));
+    W.A = lane_u32(S.rs, ra * kLpr);
     W.wrel = (int32_t)W.A - (int32_t)((S.T0 + W.A) & 15u);
     // records from ra whose (capacity-clipped) end fits: ends are non-decreasing, so a prefix
     const bool fits = q == 0 && r >= ra && (int32_t)S.pe_rec - W.wrel <= kEW;
     const int cnt = __builtin_popcountll(__ballot(fits));
     W.rb = ra + (cnt > 0 ? cnt : 1);
-    const uint32_t B = __builtin_amdgcn_readfirstlane(__shfl(S.pe_rec, (W.rb - 1) * kLpr, kWave));
+    const uint32_t B = lane_u32(S.pe_rec, (W.rb - 1) * kLpr);
     W.wlen = (int32_t)B - W.wrel;
-    const uint64_t ia = uniform64(__shfl(S.in0, ra * kLpr, kWave));
-    const uint64_t ib = W.rb < kRpt ? uniform64(__shfl(S.in0, W.rb * kLpr, kWave)) : (uint64_t)S.agg_in;
+    const uint64_t ia = lane_u64(S.in0, ra * kLpr);
+    const uint64_t ib = W.rb < kRpt ? lane_u64(S.in0, W.rb * kLpr) : (uint64_t)S.agg_in;
     W.swb = (S.in_tile + ia) & ~(uintptr_t)15;
     const uintptr_t end = (S.in_tile + ib + 15) & ~(uintptr_t)15;
     W.nb = (int32_t)(end - W.swb < (uintptr_t)kEWIn ? end - W.swb : (uintptr_t)kEWIn);
