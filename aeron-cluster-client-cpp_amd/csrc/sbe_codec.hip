@@ -997,6 +997,50 @@ __device__ __forceinline__ u32x4 merge_tail(u32x4 v, u32x4 w, int32_t b0) {
     return r;
 }
 
+// A chunk at staged position u = 4 i + sh, from the six dwords d = i-1 .. i+4: its zone-f0 bytes
+// (u), and the string starts inside it (marks m, zone_marks' nibbles) merged over the tail.  The
+// first two later zones read 2 and 4 bytes further back (u - 2, u - 4), which the same six dwords
+// hold; a third one (strings shorter than 12 bytes) reads the LDS again.  A lane without a mark
+// merges at byte 16, i.e. not at all, so the common steps run without branches.
+__device__ __forceinline__ u32x4 align4(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t e4, uint32_t s) {
+    u32x4 v;
+    v.x = __builtin_amdgcn_alignbyte(e1, e0, s);
+    v.y = __builtin_amdgcn_alignbyte(e2, e1, s);
+    v.z = __builtin_amdgcn_alignbyte(e3, e2, s);
+    v.w = __builtin_amdgcn_alignbyte(e4, e3, s);
+    return v;
+}
+__device__ __forceinline__ u32x4 chunk_zones(const uint32_t (&d)[6], uint32_t sh, uint32_t m, lds_cu8* inb,
+                                             int32_t u, int32_t imax) {
+    u32x4 v = align4(d[1], d[2], d[3], d[4], d[5], sh);
+    if (__ballot(m != 0)) {
+        const int32_t n1 = m ? __builtin_ctz(m) >> 2 : 0;
+        const int32_t b1 = m ? (int32_t)((m >> (4 * n1)) & 15u) : 16;
+        m &= ~(15u << (4 * n1));
+        const bool hi = sh >= 2;  // u - 2 = 4 i + (sh - 2), or 4 (i - 1) + (sh + 2)
+        const uint32_t s1 = hi ? sh - 2 : sh + 2;
+        v = merge_tail(v, align4(hi ? d[1] : d[0], hi ? d[2] : d[1], hi ? d[3] : d[2], hi ? d[4] : d[3],
+                                 hi ? d[5] : d[4], s1), b1);
+        if (__ballot(m != 0)) {
+            const int32_t n2 = m ? __builtin_ctz(m) >> 2 : 0;
+            const int32_t b2 = m ? (int32_t)((m >> (4 * n2)) & 15u) : 16;
+            m &= ~(15u << (4 * n2));
+            v = merge_tail(v, align4(d[0], d[1], d[2], d[3], d[4], sh), b2);  // u - 4 = 4 (i - 1) + sh
+            int32_t j = 3;
+            while (__ballot(m != 0)) {  // zone f0 + j at u - 2 j
+                if (m) {
+                    const int32_t nib = __builtin_ctz(m) >> 2;
+                    const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
+                    m &= ~(15u << (4 * nib));
+                    v = merge_tail(v, chunk_lds(inb, u - 2 * j, imax), b0);
+                }
+                ++j;
+            }
+        }
+    }
+    return v;
+}
+
 // Every chunk of the lane from the staged input, string bytes exact (chunks of not-staged records
 // get don't-care data, redone by chunk_pass_global; literal bytes are don't-care until the literal
 // pass).  Phases, so the LDS latency is paid a few times per window, not per chunk: source offsets
@@ -1030,36 +1074,22 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
         u[k] = base[k] - 2 * zone_of(E, p - E.rw);
         zm[k] = zone_marks(E, p - E.rw);
     }
-    uint32_t d[kCpl][5];
+    uint32_t d[kCpl][6];
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
         int32_t i = u[k] >> 2;
-        i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
-        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
+        i = i < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (i > imax ? imax : i);
+        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i - 1;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) d[k][j] = q[j];
+        for (int j = 0; j < 6; ++j) d[k][j] = q[j];
     }
     lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;  // padded rows never split a lane
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
-        const uint32_t sh = (uint32_t)u[k] & 3u;
-        u32x4 v;
-        v.x = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], sh);
-        v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
-        v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
-        v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
         // string starts inside the chunk (a few chunks per record): later zones overwrite the tail
-        uint32_t m = zm[k];
-        while (__ballot(m != 0)) {
-            if (m) {
-                const int32_t nib = __builtin_ctz(m) >> 2;  // zone f = nib + 1
-                const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
-                m &= ~(15u << (4 * nib));
-                v = merge_tail(v, chunk_lds(inb, base[k] - 2 * (nib + 1), imax), b0);
-            }
-        }
+        const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, zm[k], inb, u[k], imax);
         if (lb + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
@@ -1297,26 +1327,20 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
     for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
         int32_t X[kG], u[kG];
-        uint32_t d[kG][5];
+        uint32_t d[kG][6];
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
             X[k] = 16 * (cb + i0 + k) - rw;
             const int32_t f = (X[k] >= z1) + (X[k] >= z2) + (X[k] >= z3) + (X[k] >= z4);
             u[k] = src0 + X[k] - 2 * f;
             int32_t i = u[k] >> 2;
-            i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
-            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
+            i = i < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (i > imax ? imax : i);
+            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i - 1;
 #pragma unroll
-            for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
+            for (int j = 0; j < 6; ++j) d[k][j] = qd[j];
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
-            const uint32_t sh = (uint32_t)u[k] & 3u;
-            u32x4 v;
-            v.x = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], sh);
-            v.y = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], sh);
-            v.z = __builtin_amdgcn_alignbyte(d[k][3], d[k][2], sh);
-            v.w = __builtin_amdgcn_alignbyte(d[k][4], d[k][3], sh);
             // a string starting on bytes 1..15 of the chunk (inside the record): merge the tail
             const int32_t lim = min(X[k] + 15, xlast);
             uint32_t m = 0;
@@ -1324,15 +1348,7 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
             m |= (z2 > X[k] && z2 <= lim) ? (uint32_t)(z2 - X[k]) << 4 : 0u;
             m |= (z3 > X[k] && z3 <= lim) ? (uint32_t)(z3 - X[k]) << 8 : 0u;
             m |= (z4 > X[k] && z4 <= lim) ? (uint32_t)(z4 - X[k]) << 12 : 0u;
-            const int32_t base = src0 + X[k];
-            while (__ballot(m != 0)) {
-                if (m) {
-                    const int32_t nib = __builtin_ctz(m) >> 2;  // zone nib + 1 from byte b0 on
-                    const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
-                    m &= ~(15u << (4 * nib));
-                    v = merge_tail(v, chunk_lds(inb, base - 2 * (nib + 1), imax), b0);
-                }
-            }
+            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, m, inb, u[k], imax);
             if (i0 + k < n_mine) {
                 const int32_t p = 16 * (cb + i0 + k);
                 *reinterpret_cast<lds_u32x4*>(wout + wout_addr(p)) = v;
@@ -1462,10 +1478,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
             if (!compose_records<LY>(a, wout, win_in, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
-#ifndef SBE_ABL_NO_STORE
             store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, S.T0 + (int64_t)(W.wrel + W.wlen),
                          lane);
-#endif
             wsync();
         } else {
             const int32_t wrel0 = -(int32_t)(S.T0 & 15);
@@ -1661,6 +1675,29 @@ __device__ uint32_t has_seq_key(const R_t& R, uint32_t p, uint32_t n) {
     return fl;
 }
 
+// Suspect bytes, accumulated branch-free over a lane's chunks (the decode kernel is issue-bound:
+// every VALU / SALU instruction of the scan costs its slot, so the common no-hit case is pure
+// VALU, no compares into masks, no per-chunk branch):
+//   km = min over the dwords w of min(w ^ K0, w ^ S1, w ^ S2, w ^ S3): 0 iff some dword equals a
+//        key slice (the candidates of seq_key_at);
+//   bz |= (x - 0x01010101) & ~x with x = w ^ 0x5c5c5c5c: bit 7 of some byte set iff some byte is a
+//        backslash (borrow noise only sits above a real zero byte, so it is exact as an any-test).
+// The in-chunk swizzle only permutes dwords, which neither test cares about.  A suspect lane then
+// rescans its chunks with the exact per-dword tests (rare: real key slices or escapes).
+struct Suspect {
+    uint32_t km = ~0u, bz = 0u;
+    __device__ __forceinline__ void add(uint4 v) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            km = min(km, min(min(w[j] ^ kSeqK0, w[j] ^ kSeqS1), min(w[j] ^ kSeqS2, w[j] ^ kSeqS3)));
+            const uint32_t x = w[j] ^ 0x5c5c5c5cu;
+            bz |= (x - 0x01010101u) & ~x;
+        }
+    }
+    __device__ __forceinline__ bool any() const { return km == 0u || (bz & 0x80808080u) != 0u; }
+};
+
 // 0 iff some dword of v equals one of the four key slices (the candidates of seq_key_at); the
 // in-chunk swizzle only permutes dwords, which this membership test does not care about
 __device__ __forceinline__ uint32_t slice_dist(uint32_t w) {
@@ -1678,8 +1715,8 @@ __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte 
 
 // Staged records: every key dword contains 'q' (key[3]), so a 16-byte chunk (one ds_read_b128; the
 // in-chunk swizzle permutes dwords, which a membership test does not care about) without a 'q'
-// byte holds no candidate.  Only flagged chunks run the exact per-dword test.  Per lane: the
-// fallback of the window-wide scan below (more hits in one window than its list holds).
+// byte holds no candidate.  Only flagged chunks run the exact per-dword test.  Per lane: tiles of
+// records up to kSeqLaneRec bytes, and the fallback of window_exact (two hits in one lane).
 __device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
     if (n < 16) return 0u;
     const uint32_t a0 = R.base + p, a1 = a0 + n;  // window byte range
@@ -1708,14 +1745,16 @@ __device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
     return fl;
 }
 
-// Staged records are not scanned while parsing: the wave scans the whole window once
-// (window_seq_scan) and each lane then looks its payload up in the hit list.
-// per-lane scans cost the longest payload of the wave (divergence), the window-wide scan a fixed
-// 16 chunks per lane: payloads up to kSeqLaneMax bytes are scanned per lane
-constexpr uint32_t kSeqLaneMax = 256;
+// Staged records are not scanned while parsing.  Tiles of short records (all <= kSeqLaneRec bytes):
+// each lane scans its own payload afterwards (has_seq_key_lane; payloads are a minority of the
+// window's bytes and the lanes' loops are about equally long).  Tiles with longer records: dec_stage
+// classifies every staged 16-byte chunk from its staging registers (Suspect, one bit per chunk of
+// the lane; no LDS pass, no divergence between records of different lengths), and dec_window
+// resolves the pending payloads from those bits: none set in the wave (the usual case) clears them
+// all; else the flagged chunks alone get the exact tests (window_exact) and each lane looks its
+// payload up in the hit list.
+constexpr uint32_t kSeqLaneRec = 256;
 // _sequence_number flag of a payload: SBE_FL_SEQ_KEY or 0; staged payloads return kFlSeqPending
-// (dec_window resolves them: per lane, or with one window-wide scan when some payload of the
-// window is longer than kSeqLaneMax)
 constexpr uint32_t kFlSeqPending = 0x80u;
 template <typename R_t>
 __device__ __forceinline__ uint32_t seq_key_state(const R_t& R, uint32_t p, uint32_t n) {
@@ -1726,46 +1765,38 @@ __device__ __forceinline__ uint32_t seq_key_state<LdsRec>(const LdsRec&, uint32_
     return n >= 16 ? kFlSeqPending : 0u;
 }
 
-// Window-wide "_sequence_number" scan: lane l takes 16-byte chunks l, l+64, ... of the staged
-// window (coalesced, no divergence between records); a chunk with a 'q' byte has its aligned
-// dwords tested against the four key slices, and a candidate start is verified (16 bytes at that
-// window offset, inside the window).  Each lane keeps the start of its first hit in `hit`
-// (~0u: none) and sets `more` if it found a second one.
+// Exact tests of the flagged chunks (bit k of sm: chunk lane + 64 k) of a staged window of nbytes:
+// every backslash byte and every verified key start (16 bytes at that window offset, inside the
+// window) is a hit.  Each lane keeps the position of its first hit in `hit` (~0u: none; kHitEsc
+// marks a backslash) and sets `more` if it found a second one.
 __device__ __forceinline__ uint32_t win_bytes4(const uint32_t* win, uint32_t s) {  // 4 bytes at window offset s
     const uint32_t lo = lds_dw(win, s >> 2), sh = s & 3u;
     return sh ? __builtin_amdgcn_alignbyte(lds_dw(win, (s >> 2) + 1), lo, sh) : lo;
 }
 constexpr uint32_t kHitEsc = 0x80000000u;  // hit kind bit: a '\\' byte (else a key start)
-__device__ __forceinline__ void window_seq_scan(const uint32_t* win, uint32_t nbytes, int lane, uint32_t& hit,
-                                                bool& more) {
+__device__ __noinline__ void window_exact(const uint32_t* win, uint32_t sm, uint32_t nbytes, int lane,
+                                          uint32_t& hit, bool& more) {
     hit = ~0u;
     more = false;
-    const uint32_t nch = (nbytes + 15) >> 4;
-#pragma unroll 4
-    for (int k = 0; k < kWin / 16 / kWave; ++k) {
-        const uint32_t c = lane + kWave * k;
-        const uint4 v = c < nch ? lds_read_chunk_raw(win, c) : make_uint4(0, 0, 0, 0);
-        const uint32_t t = (q_bytes(v.x) | q_bytes(v.y) | q_bytes(v.z) | q_bytes(v.w)) & 0x80808080u;
-        const uint32_t b = bs_bytes_exact(v.x) | bs_bytes_exact(v.y) | bs_bytes_exact(v.z) | bs_bytes_exact(v.w);
-        if ((t && has_slice(v)) || b) {
+    for (; sm; sm &= sm - 1) {
+        const uint32_t c = (uint32_t)lane + kWave * (uint32_t)__builtin_ctz(sm);
 #pragma nounroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t A = 16 * c + 4 * j;
-                const uint32_t w = lds_dw(win, A >> 2);
-                for (uint32_t m = bs_bytes_exact(w) & range_bytes(A, 0, nbytes); m; m &= m - 1) {
-                    const uint32_t x = (A + (__builtin_ctz(m) >> 3)) | kHitEsc;
-                    if (hit == ~0u) hit = x;
-                    else more = true;
-                }
-                if (!(w == kSeqK0 || w == kSeqS1 || w == kSeqS2 || w == kSeqS3)) continue;
-                const uint32_t off = w == kSeqK0 ? 0u : w == kSeqS1 ? 1u : w == kSeqS2 ? 2u : 3u;
-                if (A < off || A - off + 16 > nbytes) continue;
-                const uint32_t st = A - off;
-                if (win_bytes4(win, st) == kSeqK0 && win_bytes4(win, st + 4) == kSeqK1 &&
-                    win_bytes4(win, st + 8) == kSeqK2 && win_bytes4(win, st + 12) == kSeqK3) {
-                    if (hit == ~0u) hit = st;
-                    else more = true;
-                }
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t A = 16 * c + 4 * j;
+            const uint32_t w = lds_dw(win, A >> 2);
+            for (uint32_t m = bs_bytes_exact(w) & range_bytes(A, 0, nbytes); m; m &= m - 1) {
+                const uint32_t x = (A + (__builtin_ctz(m) >> 3)) | kHitEsc;
+                if (hit == ~0u) hit = x;
+                else more = true;
+            }
+            if (!(w == kSeqK0 || w == kSeqS1 || w == kSeqS2 || w == kSeqS3)) continue;
+            const uint32_t off = w == kSeqK0 ? 0u : w == kSeqS1 ? 1u : w == kSeqS2 ? 2u : 3u;
+            if (A < off || A - off + 16 > nbytes) continue;
+            const uint32_t st = A - off;
+            if (win_bytes4(win, st) == kSeqK0 && win_bytes4(win, st + 4) == kSeqK1 &&
+                win_bytes4(win, st + 8) == kSeqK2 && win_bytes4(win, st + 12) == kSeqK3) {
+                if (hit == ~0u) hit = st;
+                else more = true;
             }
         }
     }
@@ -1795,9 +1826,7 @@ __device__ void dec_tm_parse(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
     d.hdr[3] = (uint16_t)ver;
     d.ts = R.u64(b + 8);
     if (b) d.flags |= SBE_FL_WRAPPED;
-#ifndef SBE_DABL_NOSEQ
     d.flags |= seq_key_state(R, d.off[3], d.len[3]);
-#endif
     if (pos + 2 > len || pos + 2 + (uint64_t)R.u16(b + pos) > len) {
         d.flags |= SBE_FL_HEADERS_E100;
     } else {
@@ -2075,8 +2104,13 @@ Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint32_t rl) {
 }
 
 // Stage window [wb, we) (16-B aligned, <= kWin bytes) into LDS: every 16-B load issued before
-// the first LDS write, one HBM round trip per window.
-__device__ __forceinline__ void dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, int lane) {
+// the first LDS write, one HBM round trip per window.  Parse mode: returns the lane's Suspect bits
+// (bit k: chunk lane + 64 k holds a key-slice dword or a backslash byte), classified from the
+// staging registers (tiles with records over kSeqLaneRec bytes: `wide`), so the "_sequence_number"
+// scan needs no LDS pass of its own.
+template <uint32_t kMode>
+__device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, bool wide,
+                                              int lane) {
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
     const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
     uint4 I[kDecRegs];
@@ -2094,6 +2128,16 @@ __device__ __forceinline__ void dec_stage(const DecArgs& a, uint32_t* win, uint6
         const uint32_t ch = lane + kWave * k;
         if (ch < nch) lds_write_chunk(win, ch, I[k]);
     }
+    uint32_t sm = 0;
+    if (kMode == SBE_DEC_PARSE_MESSAGE && wide) {
+#pragma unroll
+        for (int k = 0; k < kDecRegs; ++k) {  // zero chunks (past the window) are never suspect
+            Suspect S;
+            S.add(I[k]);
+            sm |= S.any() ? 1u << k : 0u;
+        }
+    }
+    return sm;
 }
 
 // One workgroup (one wave) per 64-record tile.  The tile's bytes are staged window by window:
@@ -2106,10 +2150,10 @@ __device__ __forceinline__ void dec_stage(const DecArgs& a, uint32_t* win, uint6
 // 3 waves per SIMD (<= 168 VGPRs): with 16 KiB of LDS per workgroup the CU holds 10 workgroups,
 // which 3 waves/SIMD still allow.
 // Parse the records that lie whole in the staged window [wb, we); in parse mode, then resolve the
-// _sequence_number flags left pending (long payloads) with one window-wide scan.
+// _sequence_number flags left pending from the window's Suspect bits sm (dec_stage).
 template <uint32_t kMode>
 __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uint64_t we, uint64_t rs, uint64_t rl,
-                                           bool& done, Desc& d, int lane) {
+                                           bool wide, uint32_t sm, bool& done, Desc& d, int lane) {
     bool here = false;
     if (!done && rs >= wb && rs + rl <= we) {
         dec_record<kMode>(LdsRec{win, (uint32_t)(rs - wb)}, (uint32_t)rl, d);
@@ -2118,23 +2162,25 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
     }
     if (kMode == SBE_DEC_PARSE_MESSAGE) {
         const bool pend = here && (d.flags & kFlSeqPending);
-        if (__ballot(pend) && !__ballot(pend && d.len[3] > kSeqLaneMax)) {
+        if (!wide) {
             if (pend)
                 d.flags = (d.flags & ~kFlSeqPending) | has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
         } else if (__ballot(pend)) {
-            uint32_t hpos;
-            bool more;
-            window_seq_scan(win, (uint32_t)(we - wb), lane, hpos, more);
-            const uint32_t p0 = (uint32_t)(rs - wb) + d.off[3], p1 = p0 + d.len[3];
             uint32_t hit = 0;
-            if (__ballot(more)) {  // two hits among one lane's chunks: pending lanes scan themselves
-                if (pend) hit = has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
-            } else {
-                for (uint64_t m = __ballot(hpos != ~0u); m; m &= m - 1) {  // broadcast each hit
-                    const uint32_t x = __builtin_amdgcn_readlane(hpos, __builtin_ctzll(m));
-                    const uint32_t xa = x & ~kHitEsc;
-                    if (x & kHitEsc) hit |= xa >= p0 && xa < p1 ? SBE_FL_SEQ_ESC : 0u;
-                    else hit |= x >= p0 && x + 16 <= p1 ? SBE_FL_SEQ_KEY : 0u;
+            if (__ballot(sm != 0)) {  // some staged chunk holds a key slice or a backslash
+                uint32_t hpos;
+                bool more;
+                window_exact(win, sm, (uint32_t)(we - wb), lane, hpos, more);
+                const uint32_t p0 = (uint32_t)(rs - wb) + d.off[3], p1 = p0 + d.len[3];
+                if (__ballot(more)) {  // two hits among one lane's chunks: pending lanes scan themselves
+                    if (pend) hit = has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
+                } else {
+                    for (uint64_t m = __ballot(hpos != ~0u); m; m &= m - 1) {  // broadcast each hit
+                        const uint32_t x = __builtin_amdgcn_readlane(hpos, __builtin_ctzll(m));
+                        const uint32_t xa = x & ~kHitEsc;
+                        if (x & kHitEsc) hit |= xa >= p0 && xa < p1 ? SBE_FL_SEQ_ESC : 0u;
+                        else hit |= x >= p0 && x + 16 <= p1 ? SBE_FL_SEQ_KEY : 0u;
+                    }
                 }
             }
             if (pend) d.flags = (d.flags & ~kFlSeqPending) | hit;
@@ -2171,9 +2217,10 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     // first window: the whole tile when its records are at most 256 B on average
     uint64_t wb = T0 & ~15ull;
     uint64_t we = wb + kWin < end ? wb + kWin : (end > wb ? end : wb);
-    dec_stage(a, win, wb, we, lane);
+    const bool wide = __ballot(valid && rl > kSeqLaneRec) != 0;
+    uint32_t sm = dec_stage<kMode>(a, win, wb, we, wide, lane);
     wsync();
-    dec_window<kMode>(win, wb, we, rs, rl, done, d, lane);
+    dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
     if (__ballot(!done)) {
         // later windows start at the first record still to parse; records no window can hold are
         // parsed from HBM
@@ -2199,9 +2246,9 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
             if (!again) break;
             we = wb + kWin < end ? wb + kWin : end;
             wsync();
-            dec_stage(a, win, wb, we, lane);
+            sm = dec_stage<kMode>(a, win, wb, we, wide, lane);
             wsync();
-            dec_window<kMode>(win, wb, we, rs, rl, done, d, lane);
+            dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
         }
     }
     if (valid) {

@@ -375,7 +375,7 @@ int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint6
  * events on its main kernel's dispatch (kernel 0 = the encode pack kernel, 1 = the decode
  * kernel; hipExtLaunchKernel timestamps), kept in a ring of the last 256 per kernel; 0 turns it
  * off.  Each call resets the rings and launch counters (the first enabling call creates the events,
- * so none is created inside a timed region).  sbe_profile_read copies the elapsed
+ * so none is created inside a timed region; SBE_EHIP when they cannot be created, e.g. no device).  sbe_profile_read copies the elapsed
  * milliseconds of up to `max` most recent sampled launches (oldest first) into ms[], clears the
  * ring and returns the count; the caller synchronises the streams first.  Used by bench.py to
  * time the dominant kernel inside its timed region (a timed dispatch costs the GPU several us,

@@ -28,11 +28,14 @@ sbecodec.use_library(os.path.abspath(args.libs[0]))
 sbecodec.require_device()
 dev = torch.device("cuda:0")
 n = args.records
-arena, L, ts = (T.var_orders if args.var else T.fixed256_orders)(n)
-a = torch.from_numpy(arena).to(dev)
-l = torch.from_numpy(L.view(np.int32)).to(dev)
-t = torch.from_numpy(ts.view(np.int64)).to(dev)
-cap = int(L.sum(dtype=np.uint64)) + 34 * n
+if args.var:
+    a, l, t = T.var_orders_t(n, dev)
+else:
+    arena, L, ts = T.fixed256_orders(n)
+    a = torch.from_numpy(arena).to(dev)
+    l = torch.from_numpy(L.view(np.int32)).to(dev)
+    t = torch.from_numpy(ts.view(np.int64)).to(dev)
+cap = int(l.sum()) + 34 * n
 out = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
 off = torch.empty(n + 1, dtype=torch.int64, device=dev)
 st = torch.empty(n, dtype=torch.uint8, device=dev)

@@ -52,11 +52,14 @@ def timed(fn, steps, warmup):
 
 CPU_THREADS = 16
 CPU_SECONDS = 3.0
+NO_CPU = False  # --no-cpu: skip the CPU baselines (profiling runs)
 
 
 def cpu_rate(fn, n_sample, budget=CPU_SECONDS):
     """records/s of fn() (the oracle restatement of the row on an n_sample-record slice of the same
     workload) repeated for about `budget` seconds on the host cores."""
+    if NO_CPU:
+        return None
     fn()
     done, t0 = 0, time.perf_counter()
     while True:
@@ -86,6 +89,8 @@ def line(row, n, step_s, kernels):
 
 def set_cpu(value, sample, cores=CPU_THREADS):
     global _cpu
+    if value is None:
+        return
     _cpu = {"value": value, "unit": "records/s", "cores": cores, "kind": "port", "sample": sample}
 
 
@@ -104,9 +109,8 @@ def row_mixed(steps, warmup):
 
 def row_var(steps, warmup):
     n = 16_777_216
-    arena, L, ts = T.var_orders(n)
-    a, l, t = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32), dev(ts.view(np.int64), torch.int64)
-    cap = sbecodec.output_bound(n, arena.size)
+    a, l, t = T.var_orders_t(n, "cuda")  # == T.var_orders(n), generated on the device
+    cap = sbecodec.output_bound(n, a.numel())
     ob = torch.empty(cap, dtype=torch.uint8, device="cuda")
     oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -118,7 +122,7 @@ def row_var(steps, warmup):
         sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec)
 
     s, pk, dk = timed(step, steps, warmup)
-    outb = int(arena.size) + 34 * n
+    outb = int(a.numel()) + 34 * n
     k = 200_000
     ak, Lk, tk = T.var_orders(k)
 
@@ -127,7 +131,7 @@ def row_var(steps, warmup):
         T.oracle_decode(o, oo_, T.DEC_PARSE, nthreads=CPU_THREADS)
 
     set_cpu(cpu_rate(cpu_rt, k), f"{k} variable-length records, oracle encode + parse_message, OpenMP {CPU_THREADS} threads")
-    line("config4_var_roundtrip", n, s, {"sbe_enc_pack<packed,wire>": (pk, arena.size + 28 * n + outb + 9 * n),
+    line("config4_var_roundtrip", n, s, {"sbe_enc_pack<packed,wire>": (pk, a.numel() + 28 * n + outb + 9 * n),
                                          "sbe_decode_kernel<parse_message>": (dk, outb + 8 * n + DESC * n)})
 
 
@@ -260,7 +264,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
     args = ap.parse_args()
+    global NO_CPU
+    NO_CPU = args.no_cpu
     sbecodec.require_device()
     for r in args.rows.split(","):
         if r == "mixed":

@@ -574,6 +574,13 @@ _TOPICS = [b"orders", b"order_request_topic", b"order_notification_topic"]
 _TYPES = [b"CREATE_ORDER", b"UPDATE_ORDER"]
 
 
+# printable filler byte for each random byte: (b % 94) + 32, with "_" → "-" (keeps
+# "_sequence_number" out of synthetic payloads) and "\\" → "/" (JSON order payloads carry no escapes)
+_FILL_LUT = (np.arange(256) % 94 + 32).astype(np.uint8)
+_FILL_LUT[_FILL_LUT == ord("_")] = ord("-")
+_FILL_LUT[_FILL_LUT == ord("\\")] = ord("/")
+
+
 def var_orders(n: int, seed: int = 0x5EED0004):
     """SURVEY §8(d) config 4 (variable length): topic ∈ 3 names, type ∈ 2, uuid 29 B, payload
     uniform [32,480] with a 3–10 B symbol, headers uniform [16,64].  Packed SoA."""
@@ -593,9 +600,7 @@ def var_orders(n: int, seed: int = 0x5EED0004):
     arena = np.empty(int(starts[-1]), np.uint8)
     # fill with printable filler derived from the random stream, then lay the fixed pieces
     fill = splitmix64(seed ^ 0xABCDEF, (arena.size + 7) // 8).view(np.uint8)[: arena.size]
-    arena[:] = (fill % 94) + 32
-    arena[arena == ord('_')] = ord('-')  # keep "_sequence_number" out of synthetic payloads
-    arena[arena == ord('\\')] = ord('/')  # and escapes (JSON order payloads carry none)
+    arena[:] = _FILL_LUT[fill]
     base = starts[:-1]
     for k, t in enumerate(_TOPICS):
         idx = base[ti == k]
@@ -612,6 +617,78 @@ def var_orders(n: int, seed: int = 0x5EED0004):
     pb = ub + 29
     arena[pb[:, None] + np.arange(10)] = np.frombuffer(b'{"symbol":', np.uint8)
     return arena, str_len, ts
+
+
+def _s64(c: int) -> int:
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _lsr(z, k: int):
+    """logical right shift of an int64 tensor holding uint64 bits"""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def _umod(z, m: int):
+    """uint64 value of int64 tensor z, mod m (m < 2^31)"""
+    return ((_lsr(z, 1) % m) * 2 + (z & 1)) % m
+
+
+def _splitmix64_t(seed: int, lo: int, count: int, device):
+    """splitmix64(seed, .)[lo:lo+count] as int64 tensors (two's-complement wrap == uint64 math)."""
+    import torch
+    z = torch.arange(lo + 1, lo + 1 + count, dtype=torch.int64, device=device)
+    z = z * _s64(0x9E3779B97F4A7C15) + _s64(seed & ((1 << 64) - 1))
+    z = (z ^ _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _lsr(z, 27)) * _s64(0x94D049BB133111EB)
+    return z ^ _lsr(z, 31)
+
+
+def var_orders_t(n: int, device, seed: int = 0x5EED0004, chunk: int = 1 << 22):
+    """var_orders(n, seed) generated with torch ops on `device` (chunked), byte-identical to the
+    numpy generator (the 16 M-record config-4 batch takes ~1.5 min on the host in numpy).  Returns
+    (arena uint8 [Σlen], str_len int32 [n,5], ts int64 [n])."""
+    import torch
+    r = _splitmix64_t(seed, 0, 6 * n, device).view(n, 6)
+    ti, yi = _umod(r[:, 0], 3), _umod(r[:, 1], 2)
+    plen, hlen = 32 + _umod(r[:, 2], 449), 16 + _umod(r[:, 3], 49)
+    tl = torch.tensor([len(t) for t in _TOPICS], dtype=torch.int64, device=device)[ti]
+    yl = torch.tensor([len(t) for t in _TYPES], dtype=torch.int64, device=device)[yi]
+    str_len = torch.stack([tl, yl, torch.full_like(tl, 29), plen, hlen], dim=1)
+    ts = torch.arange(n, dtype=torch.int64, device=device) + 1_760_000_000_000_000_000
+    base = torch.cumsum(str_len.sum(1), 0) - str_len.sum(1)
+    total = int(str_len.sum())
+    arena = torch.empty(total, dtype=torch.uint8, device=device)
+    lut = torch.from_numpy(_FILL_LUT).to(device)
+    words = (total + 7) // 8
+    for a in range(0, words, 8 * chunk):
+        b = min(words, a + 8 * chunk)
+        f = _splitmix64_t(seed ^ 0xABCDEF, a, b - a, device).view(torch.uint8)
+        e = min(total, 8 * b)
+        arena[8 * a:e] = lut[f[: e - 8 * a].to(torch.int64)]
+    del r
+    u8 = lambda bs: torch.tensor(list(bs), dtype=torch.uint8, device=device)  # noqa: E731
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        bb, tib, yib = base[a:b], ti[a:b], yi[a:b]
+        for k, t in enumerate(_TOPICS):
+            idx = bb[tib == k]
+            arena[(idx[:, None] + torch.arange(len(t), device=device)).reshape(-1)] = u8(t).repeat(idx.numel())
+        tb = bb + tl[a:b]
+        for k, t in enumerate(_TYPES):
+            idx = tb[yib == k]
+            arena[(idx[:, None] + torch.arange(len(t), device=device)).reshape(-1)] = u8(t).repeat(idx.numel())
+        ub = tb + yl[a:b]
+        m = b - a
+        uu = torch.empty((m, 29), dtype=torch.uint8, device=device)
+        uu[:, :4] = u8(b"msg_")
+        uu[:, 4:23] = _digits_t(ts[a:b], 19)
+        uu[:, 23] = ord("-")
+        r5 = _splitmix64_t(seed, 6 * a, 6 * m, device).view(m, 6)[:, 5]
+        uu[:, 24:29] = _digits_t(_umod(r5, 100_000), 5)
+        arena[(ub[:, None] + torch.arange(29, device=device)).reshape(-1)] = uu.reshape(-1)
+        pb = ub + 29
+        arena[(pb[:, None] + torch.arange(10, device=device)).reshape(-1)] = u8(b'{"symbol":').repeat(m)
+    return arena, str_len.to(torch.int32), ts
 
 
 def lite_records(n: int, template_id: int, seed: int = 0x5EED0301):

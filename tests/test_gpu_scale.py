@@ -78,10 +78,9 @@ def test_config3_mixed_decode_1m_bit_exact(codec, mode):
 @pytest.mark.timeout(900)
 def test_config4_roundtrip_16m_var(codec):
     n = 16 * 1024 * 1024
-    arena, L, ts = T.var_orders(n)
-    d_arena = _dev(arena, torch.uint8)
-    d_len = _dev(L, torch.int32)
-    d_ts = _dev(ts, torch.int64)
+    d_arena, d_len, d_ts = T.var_orders_t(n, DEV)  # T.var_orders(n), generated on the device
+    arena, L = d_arena.cpu().numpy(), d_len.cpu().numpy().view(np.uint32)
+    ts = d_ts.cpu().numpy().view(np.uint64)
     enc = codec.encode_topic_batch(d_arena, d_len, d_ts)
     dec = codec.decode_batch(enc.out, enc.out_off, mode=codec.DEC_PARSE_MESSAGE)
     torch.cuda.synchronize()
