@@ -1055,9 +1055,7 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
     RecEnt N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
-    int32_t base[kCpl];  // p - sh0: the staged-input position of zone 0 for this chunk
     int32_t u[kCpl];
-    uint32_t zm[kCpl];
     const int32_t lb = lane << lg;  // the lane's first byte
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
@@ -1070,27 +1068,60 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
                 N = rec_load(rt, r + 1 < kRpt ? r + 1 : r);
             } while (p >= E.rend && r + 1 < kRpt);
         }
-        base[k] = p - E.sh0;
-        u[k] = base[k] - 2 * zone_of(E, p - E.rw);
-        zm[k] = zone_marks(E, p - E.rw);
+        u[k] = p - E.sh0 - 2 * zone_of(E, p - E.rw);
     }
-    uint32_t d[kCpl][6];
+    uint32_t d[kCpl][5];
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
         int32_t i = u[k] >> 2;
-        i = i < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (i > imax ? imax : i);
-        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i - 1;
+        i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) d[k][j] = q[j];
+        for (int j = 0; j < 5; ++j) d[k][j] = q[j];
     }
     lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;  // padded rows never split a lane
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
-        // string starts inside the chunk (a few chunks per record): later zones overwrite the tail
-        const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, zm[k], inb, u[k], imax);
+        const u32x4 v = align4(d[k][0], d[k][1], d[k][2], d[k][3], d[k][4], (uint32_t)u[k] & 3u);
         if (lb + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
+    }
+}
+
+// Zone fix-up: the bulk passes compose every chunk from the zone (string) of its first byte; a
+// chunk with a string start on bytes 1..15 gets its tail from the later zone(s) here.  Work items
+// are the (record, string start) pairs of the record table, 4 per record (z1..z4), two per lane
+// per pass; the item of a chunk's first interior string start recomputes the whole chunk
+// (chunk_zones, all its string starts) and rewrites it, the others do nothing.  So the merges cost
+// two item passes per window instead of a merge step at every chunk position of every lane.
+// Records of the table outside the window, empty ones (rend <= rw) and not-staged ones
+// (chunk_pass_global composes those whole) have no items.
+__device__ __forceinline__ void zone_fixup(lds_u8* wout, lds_cu8* inb, lds_i32* rt, int32_t wlen, int32_t nb,
+                                           int lane) {
+    const int32_t imax = (nb + kInSlack) / 4 - 5;
+#pragma unroll
+    for (int i0 = 0; i0 < 4 * kRpt; i0 += kWave) {
+        const int i = i0 + lane, j = i >> 2, f = i & 3;  // string start z_{f+1} of record j
+        const RecEnt E = rec_load(rt, j);
+        const int32_t zf = f == 0 ? E.z1 : f == 1 ? E.z2 : f == 2 ? E.z3 : E.z4;
+        const int32_t zp = f == 0 ? 0 : f == 1 ? E.z1 : f == 2 ? E.z2 : E.z3;
+        const int32_t P = E.rw + zf;  // window position of the string start
+        const int32_t C = P >> 4;     // its chunk
+        const bool own = (P & 15) != 0 && P < E.rend && P >= 0 && 16 * C < wlen && !(E.z5 & kNotStaged) &&
+                         (f == 0 || E.rw + zp <= 16 * C);
+        if (own) {
+            const int32_t X = 16 * C - E.rw;  // record-relative chunk start (> 0: strings start >= 26 B in)
+            const int32_t u = 16 * C - E.sh0 - 2 * zone_of(E, X);
+            int32_t q = u >> 2;
+            q = q < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (q > imax ? imax : q);
+            lds_cu32* src = reinterpret_cast<lds_cu32*>(inb) + q - 1;
+            uint32_t d[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) d[k] = src[k];
+            const u32x4 v = chunk_zones(d, (uint32_t)u & 3u, zone_marks(E, X), inb, u, imax);
+            *reinterpret_cast<lds_u32x4*>(wout + wout_addr(16 * C)) = v;
+        }
     }
 }
 
@@ -1257,6 +1288,8 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
     chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
     if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, kk, lg, lane);
     wsync();
+    zone_fixup(wout, inb, rt, wlen, nb, lane);
+    wsync();
     literal_pass<LY>(ea, wout, rt, S, wlen, lane);
 }
 
@@ -1286,9 +1319,9 @@ __device__ __forceinline__ void put_lit(lds_u8* wout, int32_t x, const uint32_t*
 }
 
 template <class LY>
-__device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, const TileSt& S,
-                                                int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int lane,
-                                                int ra, int rb) {
+__device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, lds_i32* rt,
+                                                const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
+                                                int lane, int ra, int rb) {
     const int q = lane % kLpr, r = lane / kLpr;
     const bool live = S.rec_out != 0 && r >= ra && r < rb;
     const int32_t rw = (int32_t)S.rs - wrel;  // record start in the window
@@ -1322,39 +1355,47 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     // records of > 256 B make some lanes loop longer than the window's other lanes (the chunk-owner
     // passes of pack_window keep every lane at 8 chunks): those windows go there
     if (__ballot(n_mine > kCpl)) return false;
-    const int32_t xlast = rl - 1;
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
     for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
-        int32_t X[kG], u[kG];
-        uint32_t d[kG][6];
+        int32_t u[kG];
+        uint32_t d[kG][5];
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
-            X[k] = 16 * (cb + i0 + k) - rw;
-            const int32_t f = (X[k] >= z1) + (X[k] >= z2) + (X[k] >= z3) + (X[k] >= z4);
-            u[k] = src0 + X[k] - 2 * f;
+            const int32_t X = 16 * (cb + i0 + k) - rw;
+            const int32_t f = (X >= z1) + (X >= z2) + (X >= z3) + (X >= z4);
+            u[k] = src0 + X - 2 * f;
             int32_t i = u[k] >> 2;
-            i = i < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (i > imax ? imax : i);
-            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i - 1;
+            i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) d[k][j] = qd[j];
+            for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
-            // a string starting on bytes 1..15 of the chunk (inside the record): merge the tail
-            const int32_t lim = min(X[k] + 15, xlast);
-            uint32_t m = 0;
-            m |= (z1 > X[k] && z1 <= lim) ? (uint32_t)(z1 - X[k]) : 0u;
-            m |= (z2 > X[k] && z2 <= lim) ? (uint32_t)(z2 - X[k]) << 4 : 0u;
-            m |= (z3 > X[k] && z3 <= lim) ? (uint32_t)(z3 - X[k]) << 8 : 0u;
-            m |= (z4 > X[k] && z4 <= lim) ? (uint32_t)(z4 - X[k]) << 12 : 0u;
-            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, m, inb, u[k], imax);
+            // the zone of the chunk's first byte; string starts inside it: zone_fixup
+            const u32x4 v = align4(d[k][0], d[k][1], d[k][2], d[k][3], d[k][4], (uint32_t)u[k] & 3u);
             if (i0 + k < n_mine) {
                 const int32_t p = 16 * (cb + i0 + k);
                 *reinterpret_cast<lds_u32x4*>(wout + wout_addr(p)) = v;
             }
         }
     }
+    if (q == 0) {  // the record table entry zone_fixup reads (RecEnt; no record clipped here)
+        i32x4 ea4, eb4;
+        ea4.x = rw;
+        ea4.y = live ? rw + rl : rw;
+        ea4.z = rw - src0;
+        ea4.w = z1;
+        eb4.x = z2;
+        eb4.y = z3;
+        eb4.z = z4;
+        eb4.w = zs[4];
+        reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[0] = ea4;
+        reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = eb4;
+    }
+    wsync();
+    zone_fixup(wout, inb, rt, wlen, nb, lane);
     wsync();
     if (!live) return true;
     // literal bytes: q = 0 the header prefix (TopicMessage.h:221-238, :362-437), q = 1 the lengths
@@ -1475,7 +1516,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         // current window (fast) or the whole tile window by window
         if (fast) {
-            if (!compose_records<LY>(a, wout, win_in, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
+            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
             store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, S.T0 + (int64_t)(W.wrel + W.wlen),

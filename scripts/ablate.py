@@ -1,0 +1,57 @@
+"""Build ablation variants of the product library without touching its source: each variant is the
+product's csrc/sbe_codec.hip with a few text substitutions (a phase skipped), compiled to
+abl/<name>.so for scripts/ab.py (timing) or rocprofv3 PMC passes (instruction counts).  Timing-only:
+the variants produce wrong bytes.  Usage: python scripts/ablate.py name [name ...] | --list"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "aeron-cluster-client-cpp_amd", "csrc", "sbe_codec.hip")
+OUT = os.path.join(ROOT, "abl")
+
+# name -> list of (old, new) substitutions (each old string must occur exactly once)
+VARIANTS = {
+    "base": [],
+    # record-lane composition: skip the literal bytes / the zone merges / everything after the gate
+    "nolit": [("    wsync();\n    if (!live) return true;\n    // literal bytes: q = 0",
+               "    wsync();\n    return true;\n    // literal bytes: q = 0")],
+    "nomerge": [("            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, m, inb, u[k], imax);\n"
+                 "            if (i0 + k < n_mine) {",
+                 "            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, 0u, inb, u[k], imax);\n"
+                 "            if (i0 + k < n_mine) {")],
+    "nocompose": [("    if (__ballot(n_mine > kCpl)) return false;\n",
+                   "    if (__ballot(n_mine > kCpl)) return false;\n    return true;\n")],
+    # chunk-owner path (long records): skip chunk_pass / literal_pass
+    "nochunk": [("    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);\n", "")],
+    "nolitpass": [("    literal_pass<LY>(ea, wout, rt, S, wlen, lane);\n}", "}")],
+    # the fast path's window store
+    "nostore": [("            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, "
+                 "S.T0 + (int64_t)(W.wrel + W.wlen),\n                         lane);\n", "")],
+}
+
+
+def build(name):
+    s = open(SRC).read()
+    for old, new in VARIANTS[name]:
+        if s.count(old) != 1:
+            raise SystemExit(f"{name}: substitution target found {s.count(old)} times: {old[:60]!r}")
+        s = s.replace(old, new)
+    tmp = os.path.join(os.path.dirname(SRC), f"_abl_{name}.hip")
+    open(tmp, "w").write(s)
+    os.makedirs(OUT, exist_ok=True)
+    try:
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                               tmp, "-o", os.path.join(OUT, f"{name}.so"), "-L/opt/rocm/lib", "-lrccl",
+                               "-Wl,-rpath,/opt/rocm/lib"])
+    finally:
+        os.remove(tmp)
+
+
+if __name__ == "__main__":
+    if sys.argv[1:] == ["--list"]:
+        print(" ".join(VARIANTS))
+        sys.exit(0)
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(4) as ex:
+        list(ex.map(build, sys.argv[1:]))
