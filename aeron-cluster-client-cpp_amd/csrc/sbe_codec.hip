@@ -985,59 +985,25 @@ __device__ __forceinline__ uint32_t zone_marks(const RecEnt& E, int32_t X) {
     return m;
 }
 
-// bytes b0..15 of v replaced by w's (b0 in 1..15): one v_bfi per dword
+// bytes b0..15 of v replaced by w's (b0 in 1..16; 16: none): byte masks from two 64-bit shifts,
+// one v_bfi per dword
 __device__ __forceinline__ u32x4 merge_tail(u32x4 v, u32x4 w, int32_t b0) {
+    const uint32_t s = 8u * (uint32_t)b0;
+    const uint64_t m01 = s >= 64 ? 0ull : ~0ull << s;
+    const uint64_t m23 = s >= 128 ? 0ull : (s <= 64 ? ~0ull : ~0ull << (s - 64));
+    const uint32_t m[4] = {(uint32_t)m01, (uint32_t)(m01 >> 32), (uint32_t)m23, (uint32_t)(m23 >> 32)};
     u32x4 r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int32_t t = b0 - 4 * j;
-        const uint32_t m = t <= 0 ? 0xffffffffu : (t >= 4 ? 0u : (0xffffffffu << (8 * t)));
-        r[j] = (v[j] & ~m) | (w[j] & m);
-    }
+    for (int j = 0; j < 4; ++j) r[j] = (v[j] & ~m[j]) | (w[j] & m[j]);
     return r;
 }
 
-// A chunk at staged position u = 4 i + sh, from the six dwords d = i-1 .. i+4: its zone-f0 bytes
-// (u), and the string starts inside it (marks m, zone_marks' nibbles) merged over the tail.  The
-// first two later zones read 2 and 4 bytes further back (u - 2, u - 4), which the same six dwords
-// hold; a third one (strings shorter than 12 bytes) reads the LDS again.  A lane without a mark
-// merges at byte 16, i.e. not at all, so the common steps run without branches.
 __device__ __forceinline__ u32x4 align4(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, uint32_t e4, uint32_t s) {
     u32x4 v;
     v.x = __builtin_amdgcn_alignbyte(e1, e0, s);
     v.y = __builtin_amdgcn_alignbyte(e2, e1, s);
     v.z = __builtin_amdgcn_alignbyte(e3, e2, s);
     v.w = __builtin_amdgcn_alignbyte(e4, e3, s);
-    return v;
-}
-__device__ __forceinline__ u32x4 chunk_zones(const uint32_t (&d)[6], uint32_t sh, uint32_t m, lds_cu8* inb,
-                                             int32_t u, int32_t imax) {
-    u32x4 v = align4(d[1], d[2], d[3], d[4], d[5], sh);
-    if (__ballot(m != 0)) {
-        const int32_t n1 = m ? __builtin_ctz(m) >> 2 : 0;
-        const int32_t b1 = m ? (int32_t)((m >> (4 * n1)) & 15u) : 16;
-        m &= ~(15u << (4 * n1));
-        const bool hi = sh >= 2;  // u - 2 = 4 i + (sh - 2), or 4 (i - 1) + (sh + 2)
-        const uint32_t s1 = hi ? sh - 2 : sh + 2;
-        v = merge_tail(v, align4(hi ? d[1] : d[0], hi ? d[2] : d[1], hi ? d[3] : d[2], hi ? d[4] : d[3],
-                                 hi ? d[5] : d[4], s1), b1);
-        if (__ballot(m != 0)) {
-            const int32_t n2 = m ? __builtin_ctz(m) >> 2 : 0;
-            const int32_t b2 = m ? (int32_t)((m >> (4 * n2)) & 15u) : 16;
-            m &= ~(15u << (4 * n2));
-            v = merge_tail(v, align4(d[0], d[1], d[2], d[3], d[4], sh), b2);  // u - 4 = 4 (i - 1) + sh
-            int32_t j = 3;
-            while (__ballot(m != 0)) {  // zone f0 + j at u - 2 j
-                if (m) {
-                    const int32_t nib = __builtin_ctz(m) >> 2;
-                    const int32_t b0 = (int32_t)((m >> (4 * nib)) & 15u);
-                    m &= ~(15u << (4 * nib));
-                    v = merge_tail(v, chunk_lds(inb, u - 2 * j, imax), b0);
-                }
-                ++j;
-            }
-        }
-    }
     return v;
 }
 
@@ -1092,8 +1058,9 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
 // Zone fix-up: the bulk passes compose every chunk from the zone (string) of its first byte; a
 // chunk with a string start on bytes 1..15 gets its tail from the later zone(s) here.  Work items
 // are the (record, string start) pairs of the record table, 4 per record (z1..z4), two per lane
-// per pass; the item of a chunk's first interior string start recomputes the whole chunk
-// (chunk_zones, all its string starts) and rewrites it, the others do nothing.  So the merges cost
+// per pass; the item of a chunk's first interior string start recomputes the whole chunk (its
+// zone, then every later string start inside it merged over the tail) and rewrites it, the others
+// do nothing.  So the merges cost
 // two item passes per window instead of a merge step at every chunk position of every lane.
 // Records of the table outside the window, empty ones (rend <= rw) and not-staged ones
 // (chunk_pass_global composes those whole) have no items.
@@ -1111,15 +1078,34 @@ __device__ __forceinline__ void zone_fixup(lds_u8* wout, lds_cu8* inb, lds_i32* 
         const bool own = (P & 15) != 0 && P < E.rend && P >= 0 && 16 * C < wlen && !(E.z5 & kNotStaged) &&
                          (f == 0 || E.rw + zp <= 16 * C);
         if (own) {
-            const int32_t X = 16 * C - E.rw;  // record-relative chunk start (> 0: strings start >= 26 B in)
-            const int32_t u = 16 * C - E.sh0 - 2 * zone_of(E, X);
-            int32_t q = u >> 2;
+            // the chunk's first byte is in zone f (z_f <= its start < z_{f+1} = P): source u0; zone
+            // f+1 from byte P - 16 C on reads 2 bytes further back, zone f+2 (a string start at
+            // P2 in the same chunk: string f+1 shorter than 14 bytes) 4, later ones from the LDS
+            const int32_t u0 = 16 * C - E.sh0 - 2 * f;
+            int32_t q = u0 >> 2;
             q = q < 1 - kInSlack / 4 ? 1 - kInSlack / 4 : (q > imax ? imax : q);
             lds_cu32* src = reinterpret_cast<lds_cu32*>(inb) + q - 1;
             uint32_t d[6];
 #pragma unroll
             for (int k = 0; k < 6; ++k) d[k] = src[k];
-            const u32x4 v = chunk_zones(d, (uint32_t)u & 3u, zone_marks(E, X), inb, u, imax);
+            const uint32_t sh = (uint32_t)u0 & 3u;
+            u32x4 v = align4(d[1], d[2], d[3], d[4], d[5], sh);
+            const bool hi = sh >= 2;  // u0 - 2 = 4 q + (sh - 2), or 4 (q - 1) + (sh + 2)
+            v = merge_tail(v, align4(hi ? d[1] : d[0], hi ? d[2] : d[1], hi ? d[3] : d[2], hi ? d[4] : d[3],
+                                     hi ? d[5] : d[4], hi ? sh - 2 : sh + 2), P - 16 * C);
+            const int32_t cend = min(16 * C + 16, E.rend);
+            const int32_t P2 = E.rw + (f == 0 ? E.z2 : f == 1 ? E.z3 : E.z4);
+            const bool has2 = f < 3 && P2 < cend;
+            if (__ballot(has2)) {
+                v = merge_tail(v, align4(d[0], d[1], d[2], d[3], d[4], sh), has2 ? P2 - 16 * C : 16);
+                const int32_t P3 = E.rw + (f == 0 ? E.z3 : E.z4);
+                const bool has3 = f < 2 && P3 < cend;
+                if (__ballot(has3)) {
+                    v = merge_tail(v, chunk_lds(inb, u0 - 6, imax), has3 ? P3 - 16 * C : 16);
+                    const bool has4 = f == 0 && E.rw + E.z4 < cend;
+                    if (__ballot(has4)) v = merge_tail(v, chunk_lds(inb, u0 - 8, imax), has4 ? E.rw + E.z4 - 16 * C : 16);
+                }
+            }
             *reinterpret_cast<lds_u32x4*>(wout + wout_addr(16 * C)) = v;
         }
     }
