@@ -16,12 +16,13 @@ VARIANTS = {
     # record-lane composition: skip the literal bytes / the zone merges / everything after the gate
     "nolit": [("    wsync();\n    if (!live) return true;\n    // literal bytes: q = 0",
                "    wsync();\n    return true;\n    // literal bytes: q = 0")],
-    "nomerge": [("            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, m, inb, u[k], imax);\n"
-                 "            if (i0 + k < n_mine) {",
-                 "            const u32x4 v = chunk_zones(d[k], (uint32_t)u[k] & 3u, 0u, inb, u[k], imax);\n"
-                 "            if (i0 + k < n_mine) {")],
+    "nofix": [("    wsync();\n    zone_fixup(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    if (!live) return true;",
+               "    wsync();\n    if (!live) return true;")],
     "nocompose": [("    if (__ballot(n_mine > kCpl)) return false;\n",
                    "    if (__ballot(n_mine > kCpl)) return false;\n    return true;\n")],
+    # the fast loop's input staging (loads + LDS writes)
+    "nostage": [("        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);\n", ""),
+                ("        if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in\n", "")],
     # chunk-owner path (long records): skip chunk_pass / literal_pass
     "nochunk": [("    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);\n", "")],
     "nolitpass": [("    literal_pass<LY>(ea, wout, rt, S, wlen, lane);\n}", "}")],

@@ -9,7 +9,7 @@ for lib in new noscan; do
              "SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_IFETCH SQ_WAIT_INST_ANY SQ_INSTS_BRANCH" \
              "SQC_ICACHE_MISSES SQC_ICACHE_HITS"; do
     i=$((i+1))
-    timeout -s KILL 90 rocprofv3 --pmc $set --kernel-include-regex "sbe_decode_kernel" -d $O/${lib}_$i -o run --output-format csv -- python3 scripts/dec_run.py abl/$lib.so --var --k 3 > $O/${lib}_$i.log 2>&1 || { echo "pmc $lib $i failed"; tail -5 $O/${lib}_$i.log; exit 1; }
+    timeout -s KILL 90 rocprofv3 --pmc $set --kernel-include-regex "sbe_decode_kernel" -d $O/${lib}_$i -o run --output-format csv -- python3 scripts/k_run.py abl/$lib.so --var --k 3 > $O/${lib}_$i.log 2>&1 || { echo "pmc $lib $i failed"; tail -5 $O/${lib}_$i.log; exit 1; }
   done
 done
 python3 - <<'PY'
