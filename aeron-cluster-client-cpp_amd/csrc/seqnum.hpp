@@ -12,8 +12,10 @@
 // integer arithmetic (jnum_seq).
 //
 // One lane per flagged record: the work is serial byte parsing of rare records (payloads that
-// contain the key or a backslash, SBE_FL_SEQ_KEY / SBE_FL_SEQ_ESC), so it runs as its own small
-// launch instead of widening the decode kernel's register budget.
+// contain the key or a backslash, SBE_FL_SEQ_KEY / SBE_FL_SEQ_ESC).  The decode kernel calls it
+// out of line (json_seq_eval_call) after its descriptor stores, from the lanes that hold such a
+// record, so it does not widen the kernel's register budget; sbe_seqnum_kernel runs the same
+// reader as a standalone launch over finished descriptors (sbe_eval_sequence_numbers).
 
 enum : int { JT_OBEG, JT_OEND, JT_ABEG, JT_AEND, JT_STR, JT_NUM, JT_LIT, JT_COMMA, JT_COLON, JT_COMMENT,
              JT_EOS, JT_ERR };

@@ -26,6 +26,9 @@ VARIANTS = {
     # chunk-owner path (long records): skip chunk_pass / literal_pass
     "nochunk": [("    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);\n", "")],
     "nolitpass": [("    literal_pass<LY>(ea, wout, rt, S, wlen, lane);\n}", "}")],
+    "nofixw": [("    wsync();\n    zone_fixup(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    literal_pass", "    wsync();\n    literal_pass")],
+    "notables": [("    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);\n",
+                  "    const bool outside = false;\n")],
     # the fast path's window store
     "nostore": [("            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, "
                  "S.T0 + (int64_t)(W.wrel + W.wlen),\n                         lane);\n", "")],
