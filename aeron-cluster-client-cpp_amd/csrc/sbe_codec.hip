@@ -1338,9 +1338,9 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     const int32_t c0 = (rw + 15) >> 4, nc = live ? ((rw + rl + 15) >> 4) - c0 : 0;
     const int32_t h = (nc + 1) >> 1;
     const int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
-    // records of > 256 B make some lanes loop longer than the window's other lanes (the chunk-owner
-    // passes of pack_window keep every lane at 8 chunks): those windows go there
-    if (__ballot(n_mine > kCpl)) return false;
+    // records of > 768 B make some lanes loop much longer than the window's other lanes (the
+    // chunk-owner passes of pack_window keep every lane at 8 chunks): those windows go there
+    if (__ballot(n_mine > 3 * kCpl)) return false;
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
     for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
