@@ -20,6 +20,12 @@ VARIANTS = {
                "    wsync();\n    if (!live) return true;")],
     "nocompose": [("    if (__ballot(n_mine > kCpl)) return false;\n",
                    "    if (__ballot(n_mine > kCpl)) return false;\n    return true;\n")],
+    # decode window swizzle on 16-byte chunk slots only (no in-chunk dword permutation)
+    "swz28": [("__device__ __forceinline__ uint32_t swz(uint32_t i) { return i ^ ((i >> 6) & 31u); }",
+               "__device__ __forceinline__ uint32_t swz(uint32_t i) { return i ^ ((i >> 6) & 28u); }"),
+              ("    return permute4(v, x & 3u);\n}", "    return v;\n}"),
+              ("    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = permute4(v, x & 3u);",
+               "    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = v;")],
     # the fast loop's input staging (loads + LDS writes)
     "nostage": [("        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);\n", ""),
                 ("        if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in\n", "")],
