@@ -1385,7 +1385,27 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         uint32_t w[LY::kLit / 4];
 #pragma unroll
         for (int j = 0; j < LY::kLit / 4; ++j) w[j] = lit_word_v<LY>(I, j);
-        put_lit<LY::kLit>(wout, rw, w);
+        if ((rw & 15) == 0) {
+            // a 16-aligned record (fixed-size records of a 16-multiple): its whole literal chunks
+            // as ds_write_b128, the rest as one b64 / b32 (chunks never cross a padded row)
+#pragma unroll
+            for (int c = 0; c < LY::kLit / 16; ++c) {
+                i32x4 v4;
+                v4.x = (int32_t)w[4 * c];
+                v4.y = (int32_t)w[4 * c + 1];
+                v4.z = (int32_t)w[4 * c + 2];
+                v4.w = (int32_t)w[4 * c + 3];
+                *reinterpret_cast<lds_i32x4*>(wout + wout_addr(rw + 16 * c)) = v4;
+            }
+            constexpr int kT = (LY::kLit % 16) / 4, kB = LY::kLit / 16 * 4;  // tail dwords, first tail dword
+            lds_u8* const t = wout + wout_addr(rw + 4 * kB);
+            if (kT >= 2)
+                *reinterpret_cast<lds_u64*>(t) = (uint64_t)w[kB] | ((uint64_t)w[kB + 1 < LY::kLit / 4 ? kB + 1 : kB] << 32);
+            if (kT == 1 || kT == 3)
+                *reinterpret_cast<lds_u32*>(t + 4 * (kT - 1)) = w[kB + kT - 1 < LY::kLit / 4 ? kB + kT - 1 : 0];
+        } else {
+            put_lit<LY::kLit>(wout, rw, w);
+        }
     } else {
 #pragma unroll
         for (int f = 0; f < LY::kNF; ++f) {

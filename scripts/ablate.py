@@ -26,6 +26,16 @@ VARIANTS = {
               ("    return permute4(v, x & 3u);\n}", "    return v;\n}"),
               ("    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = permute4(v, x & 3u);",
                "    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = v;")],
+    # decode tiles of 48 / 32 records (lanes past the tile idle) in 12 / 8 KiB windows: more
+    # workgroups per CU (LDS-bound at 16 KiB) against idle parse lanes
+    "t48": [("constexpr int kTile = 64; ", "constexpr int kTile = 48; "),
+            ("constexpr uint32_t kWin = 16384; ", "constexpr uint32_t kWin = 12288; "),
+            ("    const uint64_t r = t0 + (uint64_t)lane;\n    const bool valid = r < a.n;",
+             "    const uint64_t r = t0 + (uint64_t)lane;\n    const bool valid = lane < kTile && r < a.n;")],
+    "t32": [("constexpr int kTile = 64; ", "constexpr int kTile = 32; "),
+            ("constexpr uint32_t kWin = 16384; ", "constexpr uint32_t kWin = 8192; "),
+            ("    const uint64_t r = t0 + (uint64_t)lane;\n    const bool valid = r < a.n;",
+             "    const uint64_t r = t0 + (uint64_t)lane;\n    const bool valid = lane < kTile && r < a.n;")],
     # the fast loop's input staging (loads + LDS writes)
     "nostage": [("        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);\n", ""),
                 ("        if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in\n", "")],
