@@ -1046,19 +1046,23 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
 
 // Zone fix-up: the bulk passes compose every chunk from the zone (string) of its first byte; a
 // chunk with a string start on bytes 1..15 gets its tail from the later zone(s) here.  Work items
-// are the (record, string start) pairs of the record table, 4 per record (z1..z4), two per lane
-// per pass; the item of a chunk's first interior string start recomputes the whole chunk (its
+// are the (record, string start) pairs of the record table, kNF - 1 per record (z1..z4 for a
+// TopicMessage: two item passes per window; one for the Lite layouts); the item of a chunk's first interior string start recomputes the whole chunk (its
 // zone, then every later string start inside it merged over the tail) and rewrites it, the others
 // do nothing.  So the merges cost
 // two item passes per window instead of a merge step at every chunk position of every lane.
 // Records of the table outside the window, empty ones (rend <= rw) and not-staged ones
 // (chunk_pass_global composes those whole) have no items.
+template <class LY>
 __device__ __forceinline__ void zone_fixup(lds_u8* wout, lds_cu8* inb, lds_i32* rt, int32_t wlen, int32_t nb,
                                            int lane) {
     const int32_t imax = (nb + kInSlack) / 4 - 5;
+    constexpr int kZ = LY::kNF - 1;  // interior string starts per record (z_1 .. z_{kNF-1})
+    static_assert(kZ >= 1 && kZ <= 4, "layouts have 2..5 strings");
 #pragma unroll
-    for (int i0 = 0; i0 < 4 * kRpt; i0 += kWave) {
-        const int i = i0 + lane, j = i >> 2, f = i & 3;  // string start z_{f+1} of record j
+    for (int i0 = 0; i0 < kZ * kRpt; i0 += kWave) {
+        const int i = i0 + lane, j = i / kZ, f = i % kZ;  // string start z_{f+1} of record j
+        if (j >= kRpt) break;
         const RecEnt E = rec_load(rt, j);
         const int32_t zf = f == 0 ? E.z1 : f == 1 ? E.z2 : f == 2 ? E.z3 : E.z4;
         const int32_t zp = f == 0 ? 0 : f == 1 ? E.z1 : f == 2 ? E.z2 : E.z3;
@@ -1263,7 +1267,7 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
     chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
     if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, kk, lg, lane);
     wsync();
-    zone_fixup(wout, inb, rt, wlen, nb, lane);
+    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);
     wsync();
     literal_pass<LY>(ea, wout, rt, S, wlen, lane);
 }
@@ -1370,7 +1374,7 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = eb4;
     }
     wsync();
-    zone_fixup(wout, inb, rt, wlen, nb, lane);
+    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);
     wsync();
     if (!live) return true;
     // literal bytes: q = 0 the header prefix (TopicMessage.h:221-238, :362-437), q = 1 the lengths
