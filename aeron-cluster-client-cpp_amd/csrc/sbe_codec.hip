@@ -2418,15 +2418,15 @@ void prof_commit(int which, hipEvent_t start) {
 
 // ------------------------------------------------------------------------------------------
 // Aeron fragment reassembly (LocalFragmentReassembler::onFragment, src/cluster_client.cpp:39-82)
-//   1. frag_classify: per fragment a scan element (delivery-point count, last BEGIN, last END,
-//      non-single bytes, singles); message sizes zeroed
-//   2. one device-wide inclusive scan of the elements (hipCUB / rocPRIM, tuple operator)
-//   3. frag_messages: every delivery point (a BEGIN|END single, or an END) sizes its message:
+//   1-3. the inclusive scan of one element per fragment (delivery-point count, last BEGIN, last
+//      END, non-single bytes, singles) in three launches (frag_reduce, frag_scan_blocks,
+//      frag_scan: the elements are classified on the fly, never stored); message sizes zeroed
+//   4. frag_messages: every delivery point (a BEGIN|END single, or an END) sizes its message:
 //      the END's group is the non-single fragments since the last BEGIN or END before it; the
 //      open group at the end of the batch is the carry
-//   4. exclusive scan of the sizes → msg_off
-//   5. frag_copy: one wave per message, realigning dword copy (fragment by fragment only when a
-//      single sits inside a group)
+//   5. exclusive scan of the sizes → msg_off (hipCUB)
+//   6. frag_copy: one wave per 64 messages, runs of back-to-back messages copied as one block
+//      (fragment by fragment only when a single sits inside a group)
 // ------------------------------------------------------------------------------------------
 struct FragScan {  // 24 bytes (batches of up to 2^31 fragments)
     uint32_t dp;   // delivery points (singles + ENDs) so far
@@ -2460,10 +2460,15 @@ __device__ __forceinline__ bool frag_single(uint8_t f) {
     return (f & (SBE_FRAG_BEGIN | SBE_FRAG_END)) == (SBE_FRAG_BEGIN | SBE_FRAG_END);
 }
 
-__global__ __launch_bounds__(256) void frag_classify(FragArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= a.n) a.msize[i] = 0;
-    if (i >= a.n) return;
+// The scan of the per-fragment elements in three launches of our own (it replaced a classify
+// kernel + a generic device scan over the 24-B tuple, which ran at 0.6 TB/s): frag_reduce classifies each
+// 1024-fragment block on the fly and writes the block's aggregate; frag_scan_blocks turns the
+// aggregates into exclusive block prefixes (one workgroup, 1024 at a time with a carry);
+// frag_scan re-classifies and writes the inclusive scan.  Elements are never materialised.
+constexpr int kFsPer = 4, kFsThreads = 256, kFsBlk = kFsPer * kFsThreads;
+__device__ __forceinline__ FragScan fs_identity() { return FragScan{0u, 0u, -1, -1, 0ull}; }
+__device__ __forceinline__ FragScan fs_elem(const FragArgs& a, uint64_t i) {
+    if (i >= a.n) return fs_identity();
     const uint8_t f = a.flags[i];
     const bool single = frag_single(f);
     const uint64_t len = a.frag_off[i + 1] - a.frag_off[i];
@@ -2473,7 +2478,95 @@ __global__ __launch_bounds__(256) void frag_classify(FragArgs a) {
     e.le = (!single && (f & SBE_FRAG_END)) ? (int32_t)i : -1;
     e.ns = single ? 0u : len;
     e.sg = single ? 1u : 0u;
-    a.el[i] = e;
+    return e;
+}
+__device__ __forceinline__ FragScan fs_shfl_up(const FragScan& v, int d) {
+    FragScan t;
+    t.dp = __shfl_up(v.dp, d, kWave);
+    t.sg = __shfl_up(v.sg, d, kWave);
+    t.lb = __shfl_up(v.lb, d, kWave);
+    t.le = __shfl_up(v.le, d, kWave);
+    t.ns = __shfl_up(v.ns, d, kWave);
+    return t;
+}
+// inclusive scan across the wave (Hillis-Steele on shuffles: this is a small share of the work)
+__device__ __forceinline__ FragScan fs_wave_scan(FragScan v, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const FragScan t = fs_shfl_up(v, d);
+        if (lane >= d) v = FragScanOp{}(t, v);
+    }
+    return v;
+}
+// the block's kFsBlk elements, kFsPer consecutive ones per thread, scanned: thread-inclusive values
+// in e[], the block total returned (LDS wt[] holds the wave totals)
+__device__ __forceinline__ FragScan fs_block(const FragArgs& a, uint64_t b, FragScan (&e)[kFsPer], FragScan* wt,
+                                             FragScan& before) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const uint64_t i0 = b * kFsBlk + (uint64_t)tid * kFsPer;
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k) e[k] = fs_elem(a, i0 + k);
+#pragma unroll
+    for (int k = 1; k < kFsPer; ++k) e[k] = FragScanOp{}(e[k - 1], e[k]);
+    const FragScan inc = fs_wave_scan(e[kFsPer - 1], lane);
+    const FragScan up = fs_shfl_up(inc, 1);
+    const FragScan ex = lane ? up : fs_identity();  // the thread's exclusive prefix inside the wave
+    if (lane == kWave - 1) wt[w] = inc;
+    __syncthreads();
+    FragScan wpre = fs_identity(), tot = fs_identity();
+#pragma unroll
+    for (int k = 0; k < kFsThreads / kWave; ++k) {
+        if (k < w) wpre = FragScanOp{}(wpre, wt[k]);
+        tot = FragScanOp{}(tot, wt[k]);
+    }
+    before = FragScanOp{}(wpre, ex);
+    return tot;
+}
+__global__ __launch_bounds__(kFsThreads) void frag_reduce(FragArgs a, FragScan* agg) {
+    __shared__ FragScan wt[kFsThreads / kWave];
+    const uint64_t b = blockIdx.x;
+    const uint64_t i0 = b * kFsBlk + (uint64_t)threadIdx.x * kFsPer;
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k)
+        if (i0 + k <= a.n) a.msize[i0 + k] = 0;  // (msize[n] too: the carry slot)
+    FragScan e[kFsPer], before;
+    const FragScan tot = fs_block(a, b, e, wt, before);
+    if (threadIdx.x == 0) agg[b] = tot;
+}
+// exclusive prefixes of the nb block aggregates, in place
+__global__ __launch_bounds__(kFsThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb) {
+    __shared__ FragScan wt[kFsThreads / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    FragScan carry = fs_identity();
+    for (uint64_t c0 = 0; c0 < nb; c0 += kFsThreads) {
+        const uint64_t j = c0 + (uint64_t)tid;
+        const FragScan v = j < nb ? agg[j] : fs_identity();
+        const FragScan inc = fs_wave_scan(v, lane);
+        const FragScan up = fs_shfl_up(inc, 1);
+        const FragScan ex = lane ? up : fs_identity();
+        __syncthreads();
+        if (lane == kWave - 1) wt[w] = inc;
+        __syncthreads();
+        FragScan wpre = fs_identity(), tot = fs_identity();
+#pragma unroll
+        for (int k = 0; k < kFsThreads / kWave; ++k) {
+            if (k < w) wpre = FragScanOp{}(wpre, wt[k]);
+            tot = FragScanOp{}(tot, wt[k]);
+        }
+        if (j < nb) agg[j] = FragScanOp{}(carry, FragScanOp{}(wpre, ex));
+        carry = FragScanOp{}(carry, tot);
+    }
+}
+__global__ __launch_bounds__(kFsThreads) void frag_scan(FragArgs a, const FragScan* pre) {
+    __shared__ FragScan wt[kFsThreads / kWave];
+    const uint64_t b = blockIdx.x;
+    FragScan e[kFsPer], before;
+    (void)fs_block(a, b, e, wt, before);
+    const FragScan base = FragScanOp{}(pre[b], before);
+    const uint64_t i0 = b * kFsBlk + (uint64_t)threadIdx.x * kFsPer;
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k)
+        if (i0 + k < a.n) a.sc[i0 + k] = FragScanOp{}(base, e[k]);
 }
 
 // group of non-single fragments ending at i (inclusive): from the later of the last BEGIN at or
@@ -2892,9 +2985,11 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
     FragArgs a{in, frag_off, flags, n, out, msg_off, counts, el, sc, msize, mfirst, mlast};
     const uint32_t blocks = (uint32_t)((n + 1 + 255) / 256);
-    hipLaunchKernelGGL(frag_classify, dim3(blocks), dim3(256), 0, s, a);
+    const uint64_t nb = (n + 1 + kFsBlk - 1) / kFsBlk;  // (n + 1: frag_reduce also zeroes msize[n])
+    hipLaunchKernelGGL(frag_reduce, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, el);
+    hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsThreads), 0, s, el, nb);
+    hipLaunchKernelGGL(frag_scan, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveScan(tmp, tmp_bytes, el, sc, FragScanOp{}, n, s);
     if (e != hipSuccess) return record_hip(e);
     hipLaunchKernelGGL(frag_messages, dim3(blocks), dim3(256), 0, s, a);
     e = hipGetLastError();

@@ -8,7 +8,7 @@ algorithmic bytes per launch (computed from the actual record sizes) and its fra
   lite301 / lite201      1 M CommitOffsetLite / OrderRequestLite records, encode + Lite decode
   order_json             1 M Orders → Order::to_json payload + publish_order headers JSON (two calls)
   reassemble             1 M Aeron fragments (90 % whole messages, the rest BEGIN..END groups),
-                         BEGIN/END reassembly (all five launches, torch events around the call)
+                         BEGIN/END reassembly (all its launches, torch events around the call)
 Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...]  (GPU only)
 """
 import argparse
@@ -221,7 +221,7 @@ def row_reassemble(steps, warmup):
     set_cpu(cpu_rate(lambda: T.oracle().orc_reassemble(P(dk_), P(ok_), P(fk_), k, P(ob_), P(mo_), P(cn_), P(ab_)), k),
             f"{k} fragments of the same stream, oracle LocalFragmentReassembler restatement, 1 thread (sequential by definition)",
             cores=1)
-    line("reassemble", n, ms * 1e-3, {"sbe_reassemble_fragments (5 launches)": (ms, nbytes)})
+    line("reassemble", n, ms * 1e-3, {"sbe_reassemble_fragments (all launches)": (ms, nbytes)})
 
 
 def row_order_json(steps, warmup):
