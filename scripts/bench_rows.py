@@ -196,7 +196,8 @@ def row_lite(t_id, steps, warmup):
 
 def row_reassemble(steps, warmup):
     n = 1_000_000
-    data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512)
+    # 90 % whole messages, 10 % BEGIN..END groups of 2-5 fragments, no strays
+    data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512, p_group=0.1)
     d, o, f = dev(data, torch.uint8), dev(off.view(np.int64), torch.int64), dev(flags, torch.uint8)
     out = torch.empty(max(data.size, 16), dtype=torch.uint8, device="cuda")
     mo = torch.empty(n + 1, dtype=torch.int64, device="cuda")

@@ -157,18 +157,21 @@ def oracle_reassemble(data, frag_off, flags):
     return msgs, carry
 
 
-def fragment_stream(n, seed, p_single=0.6, maxlen=300):
+def fragment_stream(n, seed, p_single=0.6, maxlen=300, p_group=None):
     """Random Aeron fragment stream: lengths 0..maxlen, flags drawn from whole messages
-    (BEGIN|END), BEGIN … END sequences, and stray middle / END / BEGIN fragments."""
+    (BEGIN|END, probability p_single), BEGIN … END sequences of 2-5 fragments (p_group, default
+    0.9 - p_single; a middle fragment is a whole message with probability 0.1), and stray middle /
+    END / BEGIN fragments (the rest)."""
     rng = np.random.default_rng(seed)
     flags = np.zeros(n, np.uint8)
+    p_grp_end = p_single + (0.9 - p_single if p_group is None else p_group)
     i = 0
     while i < n:
         r = rng.random()
         if r < p_single:
             flags[i] = 0xC0
             i += 1
-        elif r < 0.9:
+        elif r < p_grp_end:
             k = int(rng.integers(2, 6))
             for t in range(k):
                 if i >= n:
