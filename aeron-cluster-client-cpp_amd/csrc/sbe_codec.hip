@@ -2649,7 +2649,7 @@ __device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
 
 // wave copy of src[0, len) to dst with 16-byte stores once dst is aligned; each output chunk
 // joins the two aligned 16-byte source blocks it spans (never past the source's last block);
-// two chunks per lane in flight per step
+// four chunks per lane per step, all eight loads issued before the first join
 __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
     if (len == 0) return;
     uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
@@ -2660,13 +2660,20 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
     const uint32_t sh = (uint32_t)(p0 & 15u);
     const uintptr_t q0 = p0 & ~(uintptr_t)15;
     uint4* d16 = reinterpret_cast<uint4*>(dst + head);
-    for (uint64_t c = lane; c < nc; c += 2 * kWave) {
-        const uint64_t c2 = c + kWave;
-        const uintptr_t qa = q0 + 16 * c, qb = q0 + 16 * (c2 < nc ? c2 : c);
-        const uint4 a0 = gload128(qa), a1 = sh ? gload128(qa + 16) : a0;
-        const uint4 b0 = gload128(qb), b1 = sh ? gload128(qb + 16) : b0;
-        d16[c] = sh ? join16(a0, a1, sh) : a0;
-        if (c2 < nc) d16[c2] = sh ? join16(b0, b1, sh) : b0;
+    for (uint64_t c0 = 0; c0 < nc; c0 += 4 * kWave) {
+        uint4 x[4], y[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
+            const uintptr_t q = q0 + 16 * (c < nc ? c : nc - 1);
+            x[u] = gload128(q);
+            y[u] = gload128(q + (sh ? 16 : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
+            if (c < nc) d16[c] = sh ? join16(x[u], y[u], sh) : x[u];
+        }
     }
     const uint64_t t0 = head + 16 * nc;
     if ((uint64_t)lane < len - t0) dst[t0 + lane] = src[t0 + lane];

@@ -20,12 +20,6 @@ VARIANTS = {
                "    wsync();\n    if (!live) return true;")],
     "nocompose": [("    if (__ballot(n_mine > kCpl)) return false;\n",
                    "    if (__ballot(n_mine > kCpl)) return false;\n    return true;\n")],
-    # decode window swizzle on 16-byte chunk slots only (no in-chunk dword permutation)
-    "swz28": [("__device__ __forceinline__ uint32_t swz(uint32_t i) { return i ^ ((i >> 6) & 31u); }",
-               "__device__ __forceinline__ uint32_t swz(uint32_t i) { return i ^ ((i >> 6) & 28u); }"),
-              ("    return permute4(v, x & 3u);\n}", "    return v;\n}"),
-              ("    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = permute4(v, x & 3u);",
-               "    *reinterpret_cast<uint4*>(win + ((4u * c) ^ (x & 28u))) = v;")],
     # decode tiles of 48 / 32 records (lanes past the tile idle) in 12 / 8 KiB windows: more
     # workgroups per CU (LDS-bound at 16 KiB) against idle parse lanes
     "t48": [("constexpr int kTile = 64; ", "constexpr int kTile = 48; "),
