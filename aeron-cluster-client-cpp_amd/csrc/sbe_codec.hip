@@ -88,6 +88,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+// inclusive max over the 64 lanes of values >= 0 (0 is the identity DPP fills in)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, dpp0<0x111>(v));
+    v = max(v, dpp0<0x112>(v));
+    v = max(v, dpp0<0x114>(v));
+    v = max(v, dpp0<0x118>(v));
+    v = max(v, dpp0<0x142, 0xa>(v));
+    v = max(v, dpp0<0x143, 0xc>(v));
+    return v;
+}
+
 // the same on 64-bit values (lo / hi halves with the carries of the lo adds)
 template <int kCtrl, int kRowMask = 0xf>
 __device__ __forceinline__ uint64_t dpp_add64(uint64_t v) {
@@ -1330,10 +1341,47 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     // this lane's chunks: the first (q = 0) or second half of the record's own chunks
     const int32_t c0 = (rw + 15) >> 4, nc = live ? ((rw + rl + 15) >> 4) - c0 : 0;
     const int32_t h = (nc + 1) >> 1;
-    const int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
-    // records of > 768 B make some lanes loop much longer than the window's other lanes (the
-    // chunk-owner passes of pack_window keep every lane at 8 chunks): those windows go there
-    if (__ballot(n_mine > 3 * kCpl)) return false;
+    int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
+    // the record this lane composes chunks of (its own unless rebalanced)
+    int32_t brw = rw, bsrc0 = src0, bz1 = z1, bz2 = z2, bz3 = z3, bz4 = z4;
+    if (__ballot(n_mine > kCpl)) {
+        // records of unequal lengths (variable-length records, or one long record): two lanes per
+        // record would let the longest record set the wave's loop count.  Rebalance: T chunks per
+        // lane with T = ceil(C / (64 - records)), record j served by ceil(nc_j / T) consecutive
+        // lanes (at most 64 in all); a lane finds its record by a max-scan of the lanes where the
+        // records' runs start, then reads that record's registers from its lead lane.
+        const bool lead = q == 0 && nc > 0;
+        const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
+        const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
+        const uint32_t T = (C + (kWave - nrec) - 1) / (kWave - nrec);  // >= 1: C >= nrec >= 1
+        const uint32_t L = lead ? ((uint32_t)nc + T - 1) / T : 0u;
+        const uint32_t incL = wave_incl_scan(L, lane);
+        const uint32_t A = incL - L;  // first lane serving this lane's record (lead lanes)
+        const uint32_t used = lane_u32(incL, kWave - 1);
+        // lane A of every record learns the record's lead lane + 1 (0: no record starts there),
+        // through the record-table area (written again below)
+        rt[lane] = 0;
+        wsync();
+        if (lead) rt[A] = lane + 1;
+        wsync();
+        const uint32_t start = (uint32_t)rt[lane];
+        wsync();
+        const uint32_t owner1 = wave_incl_max(start);  // lead lane + 1 of the record this lane serves
+        const int owner = (int)owner1 - 1;
+        const bool serve = (uint32_t)lane < used && owner >= 0;
+        const int src = owner >= 0 ? owner : lane;
+        const int32_t oA = __shfl((int32_t)A, src, kWave), oc0 = __shfl(c0, src, kWave), onc = __shfl(nc, src, kWave);
+        brw = __shfl(rw, src, kWave);
+        bsrc0 = __shfl(src0, src, kWave);
+        bz1 = __shfl(z1, src, kWave);
+        bz2 = __shfl(z2, src, kWave);
+        bz3 = __shfl(z3, src, kWave);
+        bz4 = __shfl(z4, src, kWave);
+        const int32_t part = lane - oA;
+        cb = oc0 + part * (int32_t)T;
+        n_mine = serve ? min((int32_t)T, onc - part * (int32_t)T) : 0;
+        n_mine = n_mine > 0 ? n_mine : 0;
+    }
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
     for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
@@ -1341,9 +1389,9 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         uint32_t d[kG][5];
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
-            const int32_t X = 16 * (cb + i0 + k) - rw;
-            const int32_t f = (X >= z1) + (X >= z2) + (X >= z3) + (X >= z4);
-            u[k] = src0 + X - 2 * f;
+            const int32_t X = 16 * (cb + i0 + k) - brw;
+            const int32_t f = (X >= bz1) + (X >= bz2) + (X >= bz3) + (X >= bz4);
+            u[k] = bsrc0 + X - 2 * f;
             int32_t i = u[k] >> 2;
             i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
             lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
