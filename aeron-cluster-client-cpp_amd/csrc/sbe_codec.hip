@@ -1293,19 +1293,27 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
 // record's registers.
 static_assert(kLpr == 2, "record-lane composition splits a record between two lanes");
 
-// n literal bytes (dwords w) at window position x (padded rows: a run that reaches a row end
-// continues kRowPad bytes further)
+// N literal bytes (N / 4 dwords w) at window position x: the 0..3 bytes up to the first 4-aligned
+// position and the 0..3 after the last whole dword as byte stores, the rest as dword stores of the
+// realigned words (a 4-aligned dword never crosses a padded 256-byte row)
 template <int N>
 __device__ __forceinline__ void put_lit(lds_u8* wout, int32_t x, const uint32_t* w) {
-    lds_u8* const b = wout + wout_addr(x);
-    const int32_t split = 256 - (x & 255);
-    if (split >= N) {
+    static_assert(N % 4 == 0, "literal prefixes are whole dwords");
+    const uint32_t a = (uint32_t)(-x) & 3u;  // bytes before the first 4-aligned position
 #pragma unroll
-        for (int j = 0; j < N; ++j) b[j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
-    } else {
+    for (uint32_t j = 0; j < 3; ++j)
+        if (j < a) wout[wout_addr(x + (int32_t)j)] = (uint8_t)(w[0] >> (8 * j));
+    const int32_t xa = x + (int32_t)a;
 #pragma unroll
-        for (int j = 0; j < N; ++j) b[j + (j >= split ? kRowPad : 0)] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    for (int k = 0; k < N / 4; ++k) {
+        if (k == N / 4 - 1 && a != 0) break;
+        const uint32_t v = a ? __builtin_amdgcn_alignbyte(w[k + 1 < N / 4 ? k + 1 : k], w[k], a) : w[k];
+        *reinterpret_cast<lds_u32*>(wout + wout_addr(xa + 4 * k)) = v;
     }
+#pragma unroll
+    for (uint32_t t = 0; t < 3; ++t)  // bytes a + 4 (N/4 - 1) + t of the prefix, from its last dword
+        if (a != 0 && t < 4 - a)
+            wout[wout_addr(x + N - 4 + (int32_t)(a + t))] = (uint8_t)(w[N / 4 - 1] >> (8 * (a + t)));
 }
 
 template <class LY>

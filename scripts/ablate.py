@@ -16,10 +16,9 @@ VARIANTS = {
     # record-lane composition: skip the literal bytes / the zone merges / everything after the gate
     "nolit": [("    wsync();\n    if (!live) return true;\n    // literal bytes: q = 0",
                "    wsync();\n    return true;\n    // literal bytes: q = 0")],
-    "nofix": [("    wsync();\n    zone_fixup(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    if (!live) return true;",
+    "nofix": [("    wsync();\n    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    if (!live) return true;",
                "    wsync();\n    if (!live) return true;")],
-    "nocompose": [("    if (__ballot(n_mine > kCpl)) return false;\n",
-                   "    if (__ballot(n_mine > kCpl)) return false;\n    return true;\n")],
+    "nocompose": [("    if (__ballot(!ok)) return false;\n", "    if (__ballot(!ok)) return false;\n    return true;\n")],
     # decode tiles of 48 / 32 records (lanes past the tile idle) in 12 / 8 KiB windows: more
     # workgroups per CU (LDS-bound at 16 KiB) against idle parse lanes
     "t48": [("constexpr int kTile = 64; ", "constexpr int kTile = 48; "),
@@ -36,7 +35,7 @@ VARIANTS = {
     # chunk-owner path (long records): skip chunk_pass / literal_pass
     "nochunk": [("    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);\n", "")],
     "nolitpass": [("    literal_pass<LY>(ea, wout, rt, S, wlen, lane);\n}", "}")],
-    "nofixw": [("    wsync();\n    zone_fixup(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    literal_pass", "    wsync();\n    literal_pass")],
+    "nofixw": [("    wsync();\n    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    literal_pass", "    wsync();\n    literal_pass")],
     "notables": [("    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);\n",
                   "    const bool outside = false;\n")],
     # the fast path's window store
