@@ -73,6 +73,30 @@ def test_encode_var(codec, flags):
 
 
 @pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+@pytest.mark.parametrize("pattern", ["one_big", "alternating", "random"])
+def test_encode_unequal_records(codec, flags, pattern):
+    """Windows whose records differ wildly in length (the rebalanced record-lane bulk pass: a
+    record served by up to 63 lanes, lanes spanning 1-chunk records, records of 1..7000 B)."""
+    rng = np.random.default_rng({"one_big": 11, "alternating": 12, "random": 13}[pattern])
+    n = 3000
+    if pattern == "one_big":      # one ~7 KB record per 32-record tile, the rest tiny
+        big = (np.arange(n) % 32) == rng.integers(0, 32)
+    elif pattern == "alternating":
+        big = (np.arange(n) % 2) == 0
+    else:
+        big = rng.random(n) < 0.1
+    L = np.zeros((n, 5), np.uint32)
+    L[:, :3] = rng.integers(0, 4, (n, 3))
+    L[:, 3] = np.where(big, rng.integers(2000, 7000, n), rng.integers(0, 20, n))
+    L[:, 4] = rng.integers(0, 3, n)
+    if pattern == "alternating":
+        L[:, 3] = np.where(big, rng.integers(200, 900, n), L[:, 3])
+    arena = rng.integers(32, 127, int(L.sum()), dtype=np.uint8)
+    ts = rng.integers(1, 1 << 62, n, dtype=np.uint64)
+    check_encode(codec, arena, L, ts, flags=flags)
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
 def test_encode_gather_mode(codec, flags):
     # explicit per-field offsets into a shuffled arena, ragged alignment
     arena, L, ts = T.var_orders(5000, seed=99)
