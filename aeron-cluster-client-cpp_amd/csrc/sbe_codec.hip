@@ -2355,24 +2355,17 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
                       ((uint64_t)((uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16)) << 32));
         dst_store(a.ts + r, d.ts);
     }
-    // views [n][5]: transpose through LDS so each store instruction writes 256 contiguous bytes
-    wsync();
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        win[5 * lane + k] = d.off[k];
-        win[5 * kWave + 5 * lane + k] = d.len[k];
-    }
-    wsync();
-    const uint32_t nv = 5u * (uint32_t)(last - t0);
-    uint32_t* vo = a.view_off + 5 * t0;
-    uint32_t* vl = a.view_len + 5 * t0;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const uint32_t i = lane + kWave * k;
-        if (i < nv) {
-            dst_store(vo + i, win[i]);
-            dst_store(vl + i, win[5 * kWave + i]);
-        }
+    // views [n][5]: each lane stores its record's 20 contiguous bytes per array (a dwordx4 and a
+    // dword; the wave's stores cover 1280 contiguous bytes), no LDS transpose
+    if (valid) {
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        u32x4a4 o4, l4;
+        o4.x = d.off[0]; o4.y = d.off[1]; o4.z = d.off[2]; o4.w = d.off[3];
+        l4.x = d.len[0]; l4.y = d.len[1]; l4.z = d.len[2]; l4.w = d.len[3];
+        __builtin_nontemporal_store(o4, reinterpret_cast<u32x4a4*>(a.view_off + 5 * r));
+        __builtin_nontemporal_store(d.off[4], a.view_off + 5 * r + 4);
+        __builtin_nontemporal_store(l4, reinterpret_cast<u32x4a4*>(a.view_len + 5 * r));
+        __builtin_nontemporal_store(d.len[4], a.view_len + 5 * r + 4);
     }
     // ParseResult.sequence_number of flagged TopicMessages (rare: payloads with the key or a
     // backslash), evaluated from HBM by the lanes that hold one
