@@ -342,7 +342,10 @@ def main():
     if not args.no_config5:
         del arena, L, ts, out, dec, seq
         torch.cuda.empty_cache()
-        c5 = config5(args, world, rank, dev)
+        try:
+            c5 = config5(args, world, rank, dev)
+        except Exception as e:  # the headline line must still come out
+            c5 = {"workload": "config5_fixed256_sharded", "error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         def gbs(b, ms):
