@@ -290,19 +290,25 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
         uint64_t ib;
         uint8_t st;
         rec_sizes<LY, kLen>(a, r, ob, ib, st);
-        // per tile (kRpt consecutive lanes): sums via shuffles (input side in 64 bits: E109
-        // records may carry up to 5 x 4 GiB of strings)
-        uint32_t to = ob;
-        uint64_t ti = kPacked ? ib : 0u;
-#pragma unroll
-        for (int d = 1; d < kRpt; d <<= 1) {
-            to += __shfl_xor(to, d, kWave);
-            if (kPacked) ti += __shfl_xor(ti, d, kWave);
+        // per tile (kRpt = 32 consecutive lanes, two tiles per wave): one DPP scan over the wave,
+        // the tiles' sums read at lanes 31 and 63 (input side in 64 bits: E109 records may carry
+        // up to 5 x 4 GiB of strings)
+        static_assert(kRpt == 32, "two tiles per wave");
+        const int lane = tid & (kWave - 1);
+        const uint32_t so = wave_incl_scan(ob, lane);
+        const uint32_t o31 = lane_u32(so, 31), o63 = lane_u32(so, kWave - 1);
+        uint64_t i31 = 0, i63 = 0;
+        if (kPacked) {
+            const uint64_t si = wave_incl_scan64(ib, lane);
+            i31 = lane_u64(si, 31);
+            i63 = lane_u64(si, kWave - 1);
         }
-        if ((tid & (kRpt - 1)) == 0) {
-            const int tile = j * (kSbThreads / kRpt) + tid / kRpt;
-            tl[0][tile] = to;
-            tl[1][tile] = ti;
+        if (lane == 0) {
+            const int tile = j * (kSbThreads / kRpt) + 2 * (tid / kWave);
+            tl[0][tile] = o31;
+            tl[1][tile] = i31;
+            tl[0][tile + 1] = o63 - o31;
+            tl[1][tile + 1] = i63 - i31;
         }
     }
     __syncthreads();
