@@ -2210,12 +2210,9 @@ Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint32_t rl) {
 // (bit k: chunk lane + 64 k holds a key-slice dword or a backslash byte), classified from the
 // staging registers (tiles with records over kSeqLaneRec bytes: `wide`), so the "_sequence_number"
 // scan needs no LDS pass of its own.
-template <uint32_t kMode>
-__device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, bool wide,
-                                              int lane) {
+__device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane, uint4 (&I)[kDecRegs]) {
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
     const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
-    uint4 I[kDecRegs];
 #pragma unroll
     for (int k = 0; k < kDecRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -2225,6 +2222,12 @@ __device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, u
         I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
 #endif
     }
+}
+
+template <uint32_t kMode>
+__device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint64_t we, bool wide, int lane,
+                                               const uint4 (&I)[kDecRegs]) {
+    const uint32_t nch = (uint32_t)((we - wb) >> 4);
 #pragma unroll
     for (int k = 0; k < kDecRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -2240,6 +2243,14 @@ __device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, u
         }
     }
     return sm;
+}
+
+template <uint32_t kMode>
+__device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, bool wide,
+                                              int lane) {
+    uint4 I[kDecRegs];
+    dec_issue(a, wb, we, lane, I);
+    return dec_commit<kMode>(win, wb, we, wide, lane, I);
 }
 
 // One workgroup (one wave) per 64-record tile.  The tile's bytes are staged window by window:
@@ -2293,6 +2304,9 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
 #ifndef SBE_DEC_MINW
 #define SBE_DEC_MINW 3
 #endif
+#ifndef SBE_DEC_PIPE
+#define SBE_DEC_PIPE 1
+#endif
 template <uint32_t kMode>
 __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
     __shared__ uint32_t win[kWinDw];
@@ -2320,9 +2334,40 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     uint64_t wb = T0 & ~15ull;
     uint64_t we = wb + kWin < end ? wb + kWin : (end > wb ? end : wb);
     const bool wide = __ballot(valid && rl > kSeqLaneRec) != 0;
-    uint32_t sm = dec_stage<kMode>(a, win, wb, we, wide, lane);
+    uint4 I[kDecRegs];
+    dec_issue(a, wb, we, lane, I);
+    uint32_t sm = dec_commit<kMode>(win, wb, we, wide, lane, I);
+#if SBE_DEC_PIPE
+    // The second window starts at the first record the first one cannot hold, which the record
+    // offsets already tell: its loads go out before the first window is parsed (tiles of records
+    // over 256 B on average take two windows; each would otherwise wait one more HBM round trip).
+    bool pre = false;
+    uint64_t wb2 = 0, we2 = 0;
+    {
+        const uint64_t m = __ballot(!(done || (rs >= wb && rs + rl <= we)));
+        if (m) {
+            const int f = __builtin_ctzll(m);
+            const uint64_t rsf = uniform64(__shfl(rs, f, kWave));
+            const uint64_t rlf = uniform64(__shfl(rl, f, kWave));
+            if ((rsf & 15) + rlf <= kWin && rsf + rlf <= end && rsf >= (T0 & ~15ull)) {
+                wb2 = rsf & ~15ull;
+                we2 = wb2 + kWin < end ? wb2 + kWin : end;
+                pre = true;
+                dec_issue(a, wb2, we2, lane, I);
+            }
+        }
+    }
+#endif
     wsync();
     dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
+#if SBE_DEC_PIPE
+    if (pre) {
+        wsync();
+        sm = dec_commit<kMode>(win, wb2, we2, wide, lane, I);
+        wsync();
+        dec_window<kMode>(win, wb2, we2, rs, rl, wide, sm, done, d, lane);
+    }
+#endif
     if (__ballot(!done)) {
         // later windows start at the first record still to parse; records no window can hold are
         // parsed from HBM
