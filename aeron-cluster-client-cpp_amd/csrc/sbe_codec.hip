@@ -1853,7 +1853,10 @@ __device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
 // resolves the pending payloads from those bits: none set in the wave (the usual case) clears them
 // all; else the flagged chunks alone get the exact tests (window_exact) and each lane looks its
 // payload up in the hit list.
-constexpr uint32_t kSeqLaneRec = 256;
+#ifndef SBE_SEQ_LANE_REC
+#define SBE_SEQ_LANE_REC 320
+#endif
+constexpr uint32_t kSeqLaneRec = SBE_SEQ_LANE_REC;
 // _sequence_number flag of a payload: SBE_FL_SEQ_KEY or 0; staged payloads return kFlSeqPending
 constexpr uint32_t kFlSeqPending = 0x80u;
 template <typename R_t>
@@ -2235,11 +2238,16 @@ __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint6
     }
     uint32_t sm = 0;
     if (kMode == SBE_DEC_PARSE_MESSAGE && wide) {
+        // rows of chunks past the window are skipped (a tile's later window is often part full);
+        // zero chunks of the last row are never suspect
+        const uint32_t nrow = (nch + kWave - 1) / kWave;
 #pragma unroll
-        for (int k = 0; k < kDecRegs; ++k) {  // zero chunks (past the window) are never suspect
-            Suspect S;
-            S.add(I[k]);
-            sm |= S.any() ? 1u << k : 0u;
+        for (int k = 0; k < kDecRegs; ++k) {
+            if ((uint32_t)k < nrow) {
+                Suspect S;
+                S.add(I[k]);
+                sm |= S.any() ? 1u << k : 0u;
+            }
         }
     }
     return sm;

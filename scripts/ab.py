@@ -21,6 +21,7 @@ ap.add_argument("--records", type=int, default=1_000_000)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--var", action="store_true", help="variable-length workload (config 4) instead of fixed-256")
+ap.add_argument("--session", action="store_true", help="session-framed fixed-256 records (the session row)")
 ap.add_argument("--no-check", action="store_true", help="ablation builds: skip the same-output check")
 args = ap.parse_args()
 
@@ -35,7 +36,7 @@ else:
     a = torch.from_numpy(arena).to(dev)
     l = torch.from_numpy(L.view(np.int32)).to(dev)
     t = torch.from_numpy(ts.view(np.int64)).to(dev)
-cap = int(l.sum()) + 34 * n
+cap = int(l.sum()) + 66 * n
 out = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
 off = torch.empty(n + 1, dtype=torch.int64, device=dev)
 st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -48,7 +49,10 @@ for rnd in range(args.rounds):
         dec = sbecodec.alloc_decoded(n, dev)
 
         def step():
-            sbecodec.encode_topic_batch(a, l, t, out=out, out_off=off, status=st, workspace=ws)
+            if args.session:
+                sbecodec.encode_session_batch(a, l, t, 7, 8, out=out, out_off=off, status=st, workspace=ws)
+            else:
+                sbecodec.encode_topic_batch(a, l, t, out=out, out_off=off, status=st, workspace=ws)
             sbecodec.decode_batch(out, off, out=dec)
         for _ in range(3):
             step()

@@ -108,6 +108,21 @@ def test_seq_long_payloads(codec, lead):
     assert int((exp_seq != 0).sum()) > 200
 
 
+@pytest.mark.parametrize("lead", [0, 7])
+def test_seq_lane_scan_records_to_320(codec, lead):
+    """Tiles whose records are all at most 320 B (the per-lane scan's limit, e.g. 280-B session
+    frames) with payloads of 200-280 B: keys and escapes at every position of the lane scan."""
+    r = random.Random(17)
+    recs = []
+    for i, p in enumerate(q for q in seq_payloads(14, 800) if len(q) <= 240):
+        size = r.randint(max(160, len(p)), 260)
+        tm = T.tm_wire([b"orders", b"T", b"id", padded(r, p, size), b"{}"], i + 1)
+        recs.append(T.session_wrap(tm) if i % 3 == 0 and len(tm) + 32 <= 320 else tm)
+    assert max(len(x) for x in recs) <= 320
+    exp, exp_seq = run(codec, recs, lead)
+    assert int((exp_seq != 0).sum()) > 50
+
+
 def test_seq_wrapped_and_unflagged(codec):
     """Session-wrapped records are evaluated too; records of other kinds are never written."""
     r = random.Random(3)
