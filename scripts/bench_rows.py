@@ -266,7 +266,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
+    ap.add_argument("--lib", help="library build to measure (A/B of variants; default: the product's)")
     args = ap.parse_args()
+    if args.lib:
+        sbecodec.use_library(os.path.abspath(args.lib))
     global NO_CPU
     NO_CPU = args.no_cpu
     sbecodec.require_device()
