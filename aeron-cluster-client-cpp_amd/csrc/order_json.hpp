@@ -46,9 +46,16 @@ struct JsonArgs {
 };
 
 // ---- byte sinks: counting (sizing launch) and writing (8-byte buffered, byte-exact edges) ----
+__device__ inline uint32_t block_byte(const uint4& v, uint32_t o) {
+    const uint32_t w = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);
+    return (w >> (8 * (o & 3))) & 0xFF;
+}
+
+// put(b) appends one byte; run(v, o, m) appends bytes [o, o + m) of the loaded 16-byte block v
 struct CountSink {
     uint64_t n = 0;
     __device__ void put(uint8_t) { ++n; }
+    __device__ void run(const uint4&, uint32_t, uint32_t m) { n += m; }
 };
 
 // One byte store per put: into the wave's LDS window (ds_write_b8) or, for a record larger than
@@ -58,12 +65,18 @@ struct LdsSink {
     uint32_t n = 0;
     __device__ explicit LdsSink(lw8* q) : p(q) {}
     __device__ void put(uint8_t b) { p[n++] = b; }
+    __device__ void run(const uint4& v, uint32_t o, uint32_t m) {
+        for (uint32_t k = o; k < o + m; ++k) p[n++] = (uint8_t)block_byte(v, k);
+    }
 };
 struct HbmSink {
     gw8* p;
     uint64_t n = 0;
     __device__ explicit HbmSink(gw8* q) : p(q) {}
     __device__ void put(uint8_t b) { p[n++] = b; }
+    __device__ void run(const uint4& v, uint32_t o, uint32_t m) {
+        for (uint32_t k = o; k < o + m; ++k) p[n++] = (uint8_t)block_byte(v, k);
+    }
 };
 
 // A literal run: the length is a compile-time constant, so the copy unrolls into immediate
@@ -137,6 +150,20 @@ __device__ inline void hex4(S& s, uint32_t v) {
     s.put((uint8_t)hx[v & 15]);
 }
 
+// Bit k set iff byte k of the block needs more than a plain copy in valueToQuotedStringN: a
+// control byte (< 0x20), a byte >= 0x80, '"' or '\\' (SWAR, four bytes per dword, exact per byte).
+__device__ inline uint32_t zero_bytes(uint32_t x) {  // 0x80 in exactly the zero bytes of x
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+__device__ inline uint32_t special4(uint32_t w) {  // 4-bit mask of w's special bytes
+    const uint32_t ctl = ~((w & 0x7f7f7f7fu) + 0x60606060u) & 0x80808080u;  // low 7 bits < 0x20
+    const uint32_t m = (w & 0x80808080u) | ctl | zero_bytes(w ^ 0x22222222u) | zero_bytes(w ^ 0x5c5c5c5cu);
+    return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
+}
+__device__ inline uint32_t special16(const uint4& v) {
+    return special4(v.x) | (special4(v.y) << 4) | (special4(v.z) << 8) | (special4(v.w) << 12);
+}
+
 // jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
 // Out-of-line helpers take the sink by value and return it: a sink passed by reference lives in
 // scratch and every put would load and store its count.
@@ -146,21 +173,18 @@ __device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
     BlockReader rd;
     uint64_t i = 0;
     while (i < len) {
-        {  // the common case: a run of plain bytes inside the current 16-byte block (32-bit offsets)
+        {  // the common case: a run of plain bytes inside the current 16-byte block, found with
+           // one SWAR classification of the block (no per-byte tests)
             (void)rd.at(p + i);  // loads the block holding p + i
-            uint32_t o = (uint32_t)((uintptr_t)(p + i) & 15);
+            const uint32_t o = (uint32_t)((uintptr_t)(p + i) & 15);
             const uint64_t left = len - i;
             const uint32_t stop = left < 16 - o ? o + (uint32_t)left : 16;
-            const uint32_t o0 = o;
-            for (; o < stop; ++o) {
-                const uint32_t w = o < 8 ? (o < 4 ? rd.v.x : rd.v.y) : (o < 12 ? rd.v.z : rd.v.w);
-                const uint32_t b = (w >> (8 * (o & 3))) & 0xFF;
-                if (!(b >= 0x20 && b < 0x80 && b != '"' && b != '\\')) break;
-                s.put((uint8_t)b);
-            }
-            i += o - o0;
+            const uint32_t stops = special16(rd.v) | (0xffffffffu << stop);
+            const uint32_t m = (uint32_t)__builtin_ctz(stops >> o);  // plain bytes from o
+            s.run(rd.v, o, m);
+            i += m;
             if (i >= len) break;
-            if (o == 16) continue;  // the block was all plain: next block
+            if (o + m == 16) continue;  // the rest of the block was plain: next block
         }
         const uint8_t c = (uint8_t)rd.at(p + i);
         if (c >= 0x20 && c < 0x80 && c != '"' && c != '\\') {
@@ -621,20 +645,36 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
     a.sz[i] = c.n;
 }
 
-// Writing launch: one wave per 64 Orders.  Their texts are contiguous in `out`: the wave stages
-// them in an LDS window (one byte write per character), stores the window with 16-byte coalesced
-// stores and moves the window on to the first record not yet written, until every record is out.
-// Only a record larger than the window is written from its lane straight to HBM.  Records past
-// out_capacity are written by nobody.
+// Writing launch: one wave per kOpw Orders (WShape).  Their texts are contiguous in `out`: the
+// wave stages them in an LDS window (one byte write per character), stores the window with 16-byte
+// coalesced stores and moves the window on to the first record not yet written, until every record
+// is out.  Only a record larger than the window is written from its lane straight to HBM.  Records
+// past out_capacity are written by nobody.  The window is sized so that a wave's texts fit it in
+// one pass (a second pass would serialise the lanes it leaves over): payload texts (~560 B) 32 per
+// wave in 18 KiB, headers texts (~95 B) 64 per wave in 8 KiB; 8 waves per CU either way (the
+// payload writer's 207 VGPRs allow 2 per SIMD).  Measured (1 M orders, both texts): 64 payload
+// texts in a 24 KiB window (two passes) 1.54 ms, 32 in 18 KiB 1.29 ms, plus the 8 KiB headers
+// window 1.25 ms.
 constexpr uint32_t kWWave = 64;
 #ifndef SBE_OJ_WIN
-#define SBE_OJ_WIN 24576
+#define SBE_OJ_WIN 18432
 #endif
+#ifndef SBE_OJ_OPW
+#define SBE_OJ_OPW 32
+#endif
+#ifndef SBE_OJ_HDR_WIN
+#define SBE_OJ_HDR_WIN 8192
+#endif
+// Orders per wave (lanes past it idle) and LDS window bytes of the writing launch, per text kind
+template <uint32_t kWhat>
+struct WShape {
+    static constexpr uint32_t kOpw = kWhat == SBE_JSON_PUBLISH_HEADERS ? 64u : (uint32_t)SBE_OJ_OPW;
+    static constexpr uint32_t kWinB = kWhat == SBE_JSON_PUBLISH_HEADERS ? (uint32_t)SBE_OJ_HDR_WIN : (uint32_t)SBE_OJ_WIN;
+};
 #ifndef SBE_OJ_DIRECT
 #define SBE_OJ_DIRECT 0
 #endif
-constexpr uint32_t kWin = SBE_OJ_WIN;  // bytes of LDS window per wave
-static_assert(kWin >= 4096, "the window must hold a typical record");
+static_assert(SBE_OJ_WIN >= 4096 && SBE_OJ_HDR_WIN >= 4096, "the window must hold a typical record");
 constexpr bool kDirect = SBE_OJ_DIRECT != 0;  // A/B switch: every record straight to HBM
 
 __device__ inline uint64_t wave_max(uint64_t v) {
@@ -647,10 +687,11 @@ __device__ inline uint64_t wave_max(uint64_t v) {
 
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+    constexpr uint32_t kWin = WShape<kWhat>::kWinB;
     __shared__ __attribute__((aligned(16))) uint8_t win[kDirect ? 16 : kWin];
     const uint32_t lane = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * kWWave + lane;
-    const bool live = i < a.n;
+    const uint64_t i = (uint64_t)blockIdx.x * WShape<kWhat>::kOpw + lane;
+    const bool live = lane < WShape<kWhat>::kOpw && i < a.n;
     uint64_t o = 0, e = 0;
     bool done = true;
     gu8* f[kFields];

@@ -3157,11 +3157,15 @@ int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what
     e = hipGetLastError();
     if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sz, out_off, n + 1, s);
     if (e != hipSuccess) return record_hip(e);
-    const uint32_t wblocks = (uint32_t)((n + oj::kWWave - 1) / oj::kWWave);
-    if (what == SBE_JSON_PUBLISH_HEADERS)
-        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_PUBLISH_HEADERS>, dim3(wblocks), dim3(oj::kWWave), 0, s, a);
-    else
-        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_ORDER_PAYLOAD>, dim3(wblocks), dim3(oj::kWWave), 0, s, a);
+    if (what == SBE_JSON_PUBLISH_HEADERS) {
+        constexpr uint64_t w = oj::WShape<SBE_JSON_PUBLISH_HEADERS>::kOpw;
+        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_PUBLISH_HEADERS>, dim3((uint32_t)((n + w - 1) / w)),
+                           dim3(oj::kWWave), 0, s, a);
+    } else {
+        constexpr uint64_t w = oj::WShape<SBE_JSON_ORDER_PAYLOAD>::kOpw;
+        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_ORDER_PAYLOAD>, dim3((uint32_t)((n + w - 1) / w)),
+                           dim3(oj::kWWave), 0, s, a);
+    }
     return record_hip(hipGetLastError());
 }
 

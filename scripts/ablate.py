@@ -8,6 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "aeron-cluster-client-cpp_amd", "csrc", "sbe_codec.hip")
+OJ = os.path.join(ROOT, "aeron-cluster-client-cpp_amd", "csrc", "order_json.hpp")
 OUT = os.path.join(ROOT, "abl")
 
 # name -> list of (old, new) substitutions (each old string must occur exactly once)
@@ -39,6 +40,12 @@ VARIANTS = {
     "notables": [("    const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);\n",
                   "    const bool outside = false;\n")],
     # the fast path's window store
+    # Order JSON writer (substitutions in order_json.hpp, inlined into the variant): number
+    # formatting / string quoting / the window stores left out (measure and write agree on sizes)
+    "oj_nonum": [("OJ", "    s = fmt_g17(s, q);\n", "    s.put('1');\n"), ("OJ", "    s = fmt_fixed6(s, q);\n", "    s.put('1');\n")],
+    "oj_noquote": [("OJ", "__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {\n",
+                    "__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {\n    if (len < ~0ull) { s.put('\"'); s.put('\"'); return s; }\n")],
+    "oj_nostore": [("OJ", "        for (uint64_t c = lane; c < nch; c += kWWave) {", "        for (uint64_t c = nch + lane; c < nch; c += kWWave) {")],
     "nostore": [("            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, "
                  "S.T0 + (int64_t)(W.wrel + W.wlen),\n                         lane);\n", "")],
 }
@@ -46,10 +53,17 @@ VARIANTS = {
 
 def build(name):
     s = open(SRC).read()
-    for old, new in VARIANTS[name]:
-        if s.count(old) != 1:
-            raise SystemExit(f"{name}: substitution target found {s.count(old)} times: {old[:60]!r}")
-        s = s.replace(old, new)
+    oj = open(OJ).read()
+    for sub in VARIANTS[name]:
+        tgt, old, new = sub if len(sub) == 3 else ("SRC", *sub)
+        t = oj if tgt == "OJ" else s
+        if t.count(old) != 1:
+            raise SystemExit(f"{name}: substitution target found {t.count(old)} times: {old[:60]!r}")
+        if tgt == "OJ":
+            oj = oj.replace(old, new)
+        else:
+            s = s.replace(old, new)
+    s = s.replace('#include "order_json.hpp"', oj)
     tmp = os.path.join(os.path.dirname(SRC), f"_abl_{name}.hip")
     open(tmp, "w").write(s)
     os.makedirs(OUT, exist_ok=True)
