@@ -2725,24 +2725,6 @@ __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
     }
 }
 
-// copy src[0, len) to dst with dword stores where dst is aligned (lanes stride dwords); source
-// dwords are read aligned and joined with v_alignbyte (never past the source's last dword)
-__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
-    if (len == 0) return;
-    const uint64_t head = ((4u - ((uintptr_t)dst & 3u)) & 3u) < len ? ((4u - ((uintptr_t)dst & 3u)) & 3u) : len;
-    if ((uint64_t)lane < head) dst[lane] = src[lane];
-    const uint64_t nd = (len - head) >> 2;
-    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + head;
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-    for (uint64_t k = lane; k < nd; k += kWave) {
-        const uintptr_t p = s0 + 4 * k;
-        const uint32_t lo = gload32(p & ~(uintptr_t)3), hi = gload32((p + 3) & ~(uintptr_t)3);
-        d32[k] = (p & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(p & 3)) : lo;
-    }
-    const uint64_t tail0 = head + 4 * nd;
-    if ((uint64_t)lane < len - tail0) dst[tail0 + lane] = src[tail0 + lane];
-}
-
 // the 16 bytes at src + 16c + sh from the aligned blocks b0 (at 16c) and b1 (the next one)
 __device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
     const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
