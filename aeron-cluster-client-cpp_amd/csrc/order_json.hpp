@@ -671,11 +671,7 @@ struct WShape {
     static constexpr uint32_t kOpw = kWhat == SBE_JSON_PUBLISH_HEADERS ? 64u : (uint32_t)SBE_OJ_OPW;
     static constexpr uint32_t kWinB = kWhat == SBE_JSON_PUBLISH_HEADERS ? (uint32_t)SBE_OJ_HDR_WIN : (uint32_t)SBE_OJ_WIN;
 };
-#ifndef SBE_OJ_DIRECT
-#define SBE_OJ_DIRECT 0
-#endif
 static_assert(SBE_OJ_WIN >= 4096 && SBE_OJ_HDR_WIN >= 4096, "the window must hold a typical record");
-constexpr bool kDirect = SBE_OJ_DIRECT != 0;  // A/B switch: every record straight to HBM
 
 __device__ inline uint64_t wave_max(uint64_t v) {
     for (int d = 32; d >= 1; d >>= 1) {
@@ -688,7 +684,7 @@ __device__ inline uint64_t wave_max(uint64_t v) {
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
     constexpr uint32_t kWin = WShape<kWhat>::kWinB;
-    __shared__ __attribute__((aligned(16))) uint8_t win[kDirect ? 16 : kWin];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWin];
     const uint32_t lane = threadIdx.x;
     const uint64_t i = (uint64_t)blockIdx.x * WShape<kWhat>::kOpw + lane;
     const bool live = lane < WShape<kWhat>::kOpw && i < a.n;
@@ -704,7 +700,7 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         done = !fits;
         if (fits) {
             fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-            if (kDirect || e - o > kWin - 16) {  // larger than any window: straight to HBM
+            if (e - o > kWin - 16) {  // larger than any window: straight to HBM
                 HbmSink w((gw8*)(a.out + o));
                 order_text<kWhat>(w, a, i, f, l);
                 done = true;

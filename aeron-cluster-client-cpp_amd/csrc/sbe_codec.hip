@@ -153,22 +153,10 @@ __device__ __forceinline__ uint4 gload128_nt(uintptr_t addr) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(addr));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-#ifndef SBE_DEC_LD_NT
-#define SBE_DEC_LD_NT 1
-#endif
-#ifndef SBE_DEC_ST_NT
-#define SBE_DEC_ST_NT 1
-#endif
-#ifndef SBE_ENC_LD_NT
-#define SBE_ENC_LD_NT 0
-#endif
+// decode descriptor stores: written once, read by the host or the next kernel
 template <typename T>
 __device__ __forceinline__ void dst_store(T* p, T v) {
-#if SBE_DEC_ST_NT
     __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -235,14 +223,9 @@ struct EncArgs {
 };
 constexpr int kSinkBytes = 16 * 64;
 
-// Output store form of the pack kernel: buffer stores with cache-policy bits SBE_OUT_AUX
-// (0 default, 2 nt, 16 sc1 write-through) or plain global stores with a sink.
-#ifndef SBE_OUT_STORE_BUF
-#define SBE_OUT_STORE_BUF 1
-#endif
-#ifndef SBE_OUT_AUX
-#define SBE_OUT_AUX 2
-#endif
+// Cache policy of the pack kernel's output stores (buffer stores; 2 = nt: the stream is written
+// once and read by the next kernel or the host, not from this kernel's caches)
+constexpr int kOutAux = 2;
 
 // Record length modes of the TopicMessage encoders:
 //   kLenWire  the wire record, 34+Σlen (computeLength's E109 above 65534 B)
@@ -668,11 +651,7 @@ __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int l
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-#if SBE_ENC_LD_NT
-        const u32x4 v = __builtin_nontemporal_load(&base[ch < last ? ch : last]);
-#else
         const u32x4 v = base[ch < last ? ch : last];
-#endif
         I[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -790,9 +769,8 @@ __device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu
         const u32x4 a0 = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * ch + (ch >> 4) * kRowPad);
         v[k] = make_uint4(a0.x, a0.y, a0.z, a0.w);
     }
-#if SBE_OUT_STORE_BUF
     // kIt unconditional 16-byte buffer stores; chunks not wholly inside [lo, we) take an offset past
-    // the descriptor's range, which the hardware drops (cache policy SBE_OUT_AUX)
+    // the descriptor's range, which the hardware drops (cache policy kOutAux)
     (void)ob;
     (void)sink;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + wb, 0, (int)(16u * c_hi), 0x00020000);
@@ -802,18 +780,8 @@ __device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu
         const bool full = ch >= c_lo && ch < c_hi;
         u32x4 x;
         x.x = v[k].x; x.y = v[k].y; x.z = v[k].z; x.w = v[k].w;
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, full ? (int)(16u * ch) : 0x7ffffff0, 0, SBE_OUT_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, full ? (int)(16u * ch) : 0x7ffffff0, 0, kOutAux);
     }
-#else
-    // kIt unconditional 16-byte stores (chunks not wholly inside [lo, we) go to the sink)
-#pragma unroll
-    for (int k = 0; k < kIt; ++k) {
-        const uint32_t ch = lane + kWave * k;
-        const bool full = ch >= c_lo && ch < c_hi;
-        uint4* dst = full ? ob + ch : reinterpret_cast<uint4*>(sink) + lane;
-        *dst = v[k];
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
         const uint32_t ch = lane + kWave * k;
@@ -2192,16 +2160,8 @@ __device__ __forceinline__ void dec_record(const R_t& R, uint32_t len, Desc& d) 
 
 // a record parsed straight from HBM (rare: see sbe_decode_kernel); not inlined, so its register
 // needs stay out of the window loop's
-#ifndef SBE_DEC_GLB_INLINE
-#define SBE_DEC_GLB_INLINE 0
-#endif
 template <uint32_t kMode>
-#if SBE_DEC_GLB_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint32_t rl) {
+__device__ __noinline__ Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint32_t rl) {
     Desc d;
     d.clear();
     dec_record<kMode>(GlbRec{reinterpret_cast<uintptr_t>(in) + rs}, rl, d);
@@ -2219,11 +2179,7 @@ __device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_
 #pragma unroll
     for (int k = 0; k < kDecRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-#if SBE_DEC_LD_NT
         I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
-#else
-        I[k] = ch < nch ? gload128(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
-#endif
     }
 }
 
@@ -2312,9 +2268,6 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
 #ifndef SBE_DEC_MINW
 #define SBE_DEC_MINW 3
 #endif
-#ifndef SBE_DEC_PIPE
-#define SBE_DEC_PIPE 1
-#endif
 template <uint32_t kMode>
 __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
     __shared__ uint32_t win[kWinDw];
@@ -2345,7 +2298,6 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     uint4 I[kDecRegs];
     dec_issue(a, wb, we, lane, I);
     uint32_t sm = dec_commit<kMode>(win, wb, we, wide, lane, I);
-#if SBE_DEC_PIPE
     // The second window starts at the first record the first one cannot hold, which the record
     // offsets already tell: its loads go out before the first window is parsed (tiles of records
     // over 256 B on average take two windows; each would otherwise wait one more HBM round trip).
@@ -2365,17 +2317,14 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
             }
         }
     }
-#endif
     wsync();
     dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
-#if SBE_DEC_PIPE
     if (pre) {
         wsync();
         sm = dec_commit<kMode>(win, wb2, we2, wide, lane, I);
         wsync();
         dec_window<kMode>(win, wb2, we2, rs, rl, wide, sm, done, d, lane);
     }
-#endif
     if (__ballot(!done)) {
         // later windows start at the first record still to parse; records no window can hold are
         // parsed from HBM
@@ -2470,12 +2419,6 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
                 break;
             }
     }
-    // A/B override of the persistent grid (SBE_PACK_GRID=<workgroups>), read once
-    static const uint64_t g_env = [] {
-        const char* v = getenv("SBE_PACK_GRID");
-        return v ? (uint64_t)strtoull(v, nullptr, 10) : 0ull;
-    }();
-    if (g_env) g = g_env;
     // the pack kernel's tile_load adds at most one superblock total per lane per tile step:
     // G/128 + 1 <= 64
     if (g > (uint64_t)(kWave - 1) * kTilesPerSb) g = (uint64_t)(kWave - 1) * kTilesPerSb;
