@@ -195,6 +195,9 @@ struct Lay {
     static constexpr int32_t kS0 = kLit + 2;          // first string byte
     static constexpr int32_t kOvh = kLit + 2 * kNF;   // wire overhead
     static constexpr int32_t ovh(bool trunc) { return kOvh - (trunc ? 8 : 0); }
+    // window store rows issued unconditionally (store_window): CommitOffsetLite's 32-record tiles
+    // (~77-B records) are ~2.5 KiB, three of the eight 1-KiB rows
+    static constexpr int kStoreRows0 = kNF == 2 ? 3 : 8;
 };
 using LayTM = Lay<0, 16, 5, true>;
 using LayTMS = Lay<32, 16, 5, true>;
@@ -753,44 +756,59 @@ __device__ __forceinline__ void compose(const EncArgs& a, lds_u8* wout, lds_cu8*
     W.flush();
 }
 
-// window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte
-__device__ __forceinline__ void store_window(uint8_t* out, uint8_t* sink, lds_cu8* wout, uint64_t T0, uint64_t wb,
-                                             uint64_t we, int lane) {
-    constexpr int kIt = kEW / 16 / kWave;
-    const uint64_t lo = wb > T0 ? wb : T0;
-    const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
-    const uint32_t c_lo = (uint32_t)((lo - wb + 15) >> 4);  // chunks [c_lo, c_hi) lie inside [lo, we)
-    const uint32_t c_hi = (uint32_t)((we - wb) >> 4);
-    uint4* const ob = reinterpret_cast<uint4*>(out + wb);   // uniform base + 32-bit lane offsets
-    uint4 v[kIt];
+// window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte.
+// Rows of 64 chunks [0, kRows0) are stored unconditionally; the rows after them only when the
+// window reaches them (a uniform branch).  kRows0 = all rows for layouts whose windows are usually
+// full; layouts of small records whose 32-record tiles are a few KiB (CommitOffsetLite) skip the
+// empty rows: the join after the branch makes the compiler wait for the longer path's extra stores
+// before the next window's staging, but the short path, the one those tiles take, waits exactly.
+template <int kRows0>
+__device__ __forceinline__ void store_rows(uint8_t* out, lds_cu8* wout, uint64_t wb, uint64_t lo, uint64_t we,
+                                           uint32_t nch, uint32_t c_lo, uint32_t c_hi,
+                                           const __amdgpu_buffer_rsrc_t& rs, int lane, int k0) {
+    uint4 v[kRows0];
 #pragma unroll
-    for (int k = 0; k < kIt; ++k) {
-        const uint32_t ch = lane + kWave * k;
+    for (int k = 0; k < kRows0; ++k) {
+        const uint32_t ch = lane + kWave * (k0 + k);
         const u32x4 a0 = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * ch + (ch >> 4) * kRowPad);
         v[k] = make_uint4(a0.x, a0.y, a0.z, a0.w);
     }
-    // kIt unconditional 16-byte buffer stores; chunks not wholly inside [lo, we) take an offset past
+    // unconditional 16-byte buffer stores; chunks not wholly inside [lo, we) take an offset past
     // the descriptor's range, which the hardware drops (cache policy kOutAux)
-    (void)ob;
-    (void)sink;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + wb, 0, (int)(16u * c_hi), 0x00020000);
 #pragma unroll
-    for (int k = 0; k < kIt; ++k) {
-        const uint32_t ch = lane + kWave * k;
+    for (int k = 0; k < kRows0; ++k) {
+        const uint32_t ch = lane + kWave * (k0 + k);
         const bool full = ch >= c_lo && ch < c_hi;
         u32x4 x;
         x.x = v[k].x; x.y = v[k].y; x.z = v[k].z; x.w = v[k].w;
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, full ? (int)(16u * ch) : 0x7ffffff0, 0, kOutAux);
     }
 #pragma unroll
-    for (int k = 0; k < kIt; ++k) {
-        const uint32_t ch = lane + kWave * k;
+    for (int k = 0; k < kRows0; ++k) {
+        const uint32_t ch = lane + kWave * (k0 + k);
         if (ch >= nch || (ch >= c_lo && ch < c_hi)) continue;
         const uint64_t g = wb + 16ull * ch;
         const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j)
             if (g + j >= lo && g + j < we) out[g + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
+    }
+}
+
+constexpr int kStoreRows = kEW / 16 / kWave;  // rows of 64 chunks in a window
+template <int kRows0 = kStoreRows>
+__device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64_t T0, uint64_t wb, uint64_t we,
+                                             int lane) {
+    static_assert(kRows0 >= 1 && kRows0 <= kStoreRows, "store rows");
+    const uint64_t lo = wb > T0 ? wb : T0;
+    const uint32_t nch = (uint32_t)((we - wb + 15) >> 4);
+    const uint32_t c_lo = (uint32_t)((lo - wb + 15) >> 4);  // chunks [c_lo, c_hi) lie inside [lo, we)
+    const uint32_t c_hi = (uint32_t)((we - wb) >> 4);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out + wb, 0, (int)(16u * c_hi), 0x00020000);
+    store_rows<kRows0>(out, wout, wb, lo, we, nch, c_lo, c_hi, rs, lane, 0);
+    if constexpr (kRows0 < kStoreRows) {
+        if (nch > (uint32_t)(kWave * kRows0))
+            store_rows<kStoreRows - kRows0>(out, wout, wb, lo, we, nch, c_lo, c_hi, rs, lane, kRows0);
     }
 }
 
@@ -1326,16 +1344,24 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
     // the record this lane composes chunks of (its own unless rebalanced)
     int32_t brw = rw, bsrc0 = src0, bz1 = z1, bz2 = z2, bz3 = z3, bz4 = z4;
+    bool rebal = false;
+    uint32_t T = 0;
     if (__ballot(n_mine > kCpl)) {
+        const bool lead = q == 0 && nc > 0;
+        const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
+        const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
+        T = (C + (kWave - nrec) - 1) / (kWave - nrec);  // >= 1: C >= nrec >= 1
+        // only when it shortens the two-lane split's longest lane (records of equal lengths just
+        // over 2 kCpl chunks, e.g. 280-B session frames, are better off split in two)
+        rebal = T < lane_u32(wave_incl_max((uint32_t)(n_mine > 0 ? n_mine : 0)), kWave - 1);
+    }
+    if (rebal) {
         // records of unequal lengths (variable-length records, or one long record): two lanes per
         // record would let the longest record set the wave's loop count.  Rebalance: T chunks per
         // lane with T = ceil(C / (64 - records)), record j served by ceil(nc_j / T) consecutive
         // lanes (at most 64 in all); a lane finds its record by a max-scan of the lanes where the
         // records' runs start, then reads that record's registers from its lead lane.
         const bool lead = q == 0 && nc > 0;
-        const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
-        const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
-        const uint32_t T = (C + (kWave - nrec) - 1) / (kWave - nrec);  // >= 1: C >= nrec >= 1
         const uint32_t L = lead ? ((uint32_t)nc + T - 1) / T : 0u;
         const uint32_t incL = wave_incl_scan(L, lane);
         const uint32_t A = incL - L;  // first lane serving this lane's record (lead lanes)
@@ -1548,8 +1574,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
             if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
-            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, S.T0 + (int64_t)(W.wrel + W.wlen),
-                         lane);
+            store_window<LY::kStoreRows0>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,
+                                          S.T0 + (int64_t)(W.wrel + W.wlen), lane);
             wsync();
         } else {
             const int32_t wrel0 = -(int32_t)(S.T0 & 15);
@@ -1581,7 +1607,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                     compose<LY, false>(a, wout, win_in, S, wrel, we_rel, sw, nbw);
                 }
                 wsync();
-                store_window(a.out, a.sink, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
+                store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
                 wsync();
             }
         }
