@@ -46,6 +46,10 @@ VARIANTS = {
     "oj_noquote": [("OJ", "__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {\n",
                     "__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {\n    if (len < ~0ull) { s.put('\"'); s.put('\"'); return s; }\n")],
     "oj_nostore": [("OJ", "        for (uint64_t c = lane; c < nch; c += kWWave) {", "        for (uint64_t c = nch + lane; c < nch; c += kWWave) {")],
+    # decode: the Ack printable-run scan / the per-lane _sequence_number scan left out (config 3)
+    "noack": [("    // maximal runs of printable bytes over [16, len)", "    if (len) return;\n    // maximal runs of printable bytes over [16, len)")],
+    "noseqlane": [("__device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {\n    if (n < 16) return 0u;",
+                   "__device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {\n    if (n < ~0u) return 0u;")],
     "nostore": [("            store_window(a.out, a.sink, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel, "
                  "S.T0 + (int64_t)(W.wrel + W.wlen),\n                         lane);\n", "")],
 }
