@@ -63,10 +63,31 @@ struct CountSink {
 struct LdsSink {
     lw8* p;
     uint32_t n = 0;
-    __device__ explicit LdsSink(lw8* q) : p(q) {}
+    uint32_t lim;  // the text's length: bytes [0, lim) of p are this lane's
+    __device__ LdsSink(lw8* q, uint32_t len) : p(q), lim(len) {}
     __device__ void put(uint8_t b) { p[n++] = b; }
+    // a run of m plain bytes: one (unaligned) 16-byte LDS store of the block realigned to o; the
+    // bytes past the run are this lane's own later text, which overwrites them (near the end of
+    // the text, byte stores)
     __device__ void run(const uint4& v, uint32_t o, uint32_t m) {
-        for (uint32_t k = o; k < o + m; ++k) p[n++] = (uint8_t)block_byte(v, k);
+        if (n + 16 <= lim) {
+            typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+            typedef __attribute__((address_space(3))) u32x4u lw128u;
+            const uint32_t j = o >> 2, sh = o & 3u;
+            const uint32_t w0 = j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+            const uint32_t w1 = j == 0 ? v.y : j == 1 ? v.z : j == 2 ? v.w : 0u;
+            const uint32_t w2 = j == 0 ? v.z : j == 1 ? v.w : 0u;
+            const uint32_t w3 = j == 0 ? v.w : 0u;
+            u32x4u x;
+            x.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            x.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            x.w = __builtin_amdgcn_alignbyte(0u, w3, sh);
+            *reinterpret_cast<lw128u*>(p + n) = x;
+            n += m;
+        } else {
+            for (uint32_t k = o; k < o + m; ++k) p[n++] = (uint8_t)block_byte(v, k);
+        }
     }
 };
 struct HbmSink {
@@ -721,7 +742,7 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         const uint64_t wbase = start - (uint64_t)((uintptr_t)(a.out + start) & 15);  // win[0] ≡ out + wbase (mod 16)
         uint64_t my_end = 0;
         if (!done && e - wbase <= kWin) {
-            LdsSink w((lw8*)(win + (o - wbase)));
+            LdsSink w((lw8*)(win + (o - wbase)), (uint32_t)(e - o));
             order_text<kWhat>(w, a, i, f, l);
             done = true;
             my_end = e;
