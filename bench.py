@@ -57,7 +57,7 @@ DEC_BYTES_ALL = 256 + 8 + 2 + 8 + 8 + 40
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--records", type=int, default=1_000_000, help="records per GPU (headline)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0)")
@@ -69,7 +69,7 @@ def parse_args():
     p.add_argument("--separate-seq", action="store_true",
                    help="sequence_number evaluation as its own launch (sbe_eval_sequence_numbers)")
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
-    p.add_argument("--settle-ms", type=float, default=60.0,
+    p.add_argument("--settle-ms", type=float, default=500.0,
                    help="untimed round trips before the warmup steps, until the GPU has run this long")
     p.add_argument("--event-every", type=int, default=10,
                    help="HIP events on the pack / decode dispatches of every k-th timed step (0: none, "
@@ -300,7 +300,7 @@ def main():
     # up over the first tens of milliseconds of sustained load; a 5-step warmup is ~1 ms), then the
     # W warmup steps, then the timed K steps, with no host gap in between
     settle_steps, t_set = 0, time.perf_counter()
-    while args.settle_ms > 0 and settle_steps < 1000:
+    while args.settle_ms > 0 and settle_steps < 10000:
         for _ in range(10):
             step()
         settle_steps += 10
