@@ -1344,11 +1344,11 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
     // the record this lane composes chunks of (its own unless rebalanced)
     int32_t brw = rw, bsrc0 = src0, bz1 = z1, bz2 = z2, bz3 = z3, bz4 = z4;
-    // Session frames: rebalance only when it shortens the two-lane split's longest lane (records
-    // of equal lengths just over 2 kCpl chunks, 280-B frames, are better off split in two).  The
-    // TopicMessage layout keeps the plain test: its windows never gain from the check, and the
-    // extra code measured +0.6 % on the fixed-256 pack.
-    constexpr bool kGuard = LY::kPre > 0;
+    // Session frames and Lite records: rebalance only when it shortens the two-lane split's longest
+    // lane (records of equal lengths just over 2 kCpl chunks, e.g. 280-B frames, are better off
+    // split in two).  The plain TopicMessage layout keeps the unconditional rebalance: its windows
+    // never gain from the check, and the extra code measured +0.6 % on the fixed-256 pack.
+    constexpr bool kGuard = !(LY::kTM && LY::kPre == 0);
     bool rebal = false;
     uint32_t T = 0;
     if (__ballot(n_mine > kCpl)) {
