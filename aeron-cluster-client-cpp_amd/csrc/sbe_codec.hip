@@ -1960,6 +1960,31 @@ __device__ __forceinline__ uint64_t printable_mask64(const R_t& R, uint32_t p, u
     return nbytes >= 64 ? m : m & ((1ull << nbytes) - 1);
 }
 
+// The same for a staged record: the (up to) five 16-byte chunks holding [p, p + nbytes) as
+// ds_read_b128 (a chunk stays whole in its LDS slot), classified on 80 bytes and shifted into place
+// (5 LDS reads instead of 17 swizzled dword reads)
+__device__ __forceinline__ uint32_t printable4(uint32_t w) {  // bit k: byte k of w is printable
+    const uint32_t lo7 = w & 0x7f7f7f7fu;
+    const uint32_t pr = (lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u;
+    return (((pr >> 7) * 0x00204081u) >> 21) & 0xfu;
+}
+template <>
+__device__ __forceinline__ uint64_t printable_mask64<LdsRec>(const LdsRec& R, uint32_t p, uint32_t nbytes) {
+    const uint32_t A = R.base + p;  // window offset of byte p
+    const uint32_t c0 = A >> 4, s = A & 15u, clast = (A + nbytes - 1) >> 4;
+    uint64_t lo = 0;
+    uint32_t hi = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 5; ++j) {
+        const uint4 v = lds_read_chunk_raw(R.win, c0 + j < clast ? c0 + j : clast);
+        const uint32_t m16 = printable4(v.x) | (printable4(v.y) << 4) | (printable4(v.z) << 8) | (printable4(v.w) << 12);
+        if (j < 4) lo |= (uint64_t)m16 << (16 * j);
+        else hi = m16;
+    }
+    const uint64_t m = s ? (lo >> s) | ((uint64_t)hi << (64 - s)) : lo;
+    return nbytes >= 64 ? m : m & ((1ull << nbytes) - 1);
+}
+
 // decode_acknowledgment_with_sbe (src/sbe_encoder.cpp:833-954)
 template <typename R_t>
 __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
