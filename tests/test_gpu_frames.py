@@ -106,6 +106,25 @@ def test_lite_encode_gather_and_edges(codec, t):
                        *T.oracle_encode_lite(t, shifted, L, tid, seq, off))
 
 
+@pytest.mark.parametrize("lo,hi", [(60, 260), (0, 900)])
+def test_lite301_windows_past_three_rows(codec, lo, hi):
+    """CommitOffsetLite windows of 3-8 KiB (the store rows past the first three, which the
+    ~77-B records of the usual batch never reach), packed and gather input."""
+    rng = np.random.default_rng(lo + hi)
+    L = rng.integers(lo, hi, (3000, 2)).astype(np.uint32)
+    L[rng.random(3000) < 0.3] = rng.integers(0, 20, 2)  # small records in between
+    arena = rng.integers(0, 256, int(L.sum(dtype=np.int64)), dtype=np.uint8)
+    tid = rng.integers(0, 2**32, len(L), dtype=np.uint64).astype(np.uint32)
+    seq = rng.integers(0, 2**64 - 1, len(L), dtype=np.uint64)
+    assert_same_stream(*lite_gpu(codec, 301, arena, L, tid, seq), *T.oracle_encode_lite(301, arena, L, tid, seq))
+    starts = np.zeros(L.size + 1, np.int64)
+    starts[1:] = np.cumsum(L.reshape(-1).astype(np.int64))
+    off = (starts[:-1] + 5).astype(np.uint32)
+    shifted = np.concatenate([np.zeros(5, np.uint8), arena])
+    assert_same_stream(*lite_gpu(codec, 301, shifted, L, tid, seq, off),
+                       *T.oracle_encode_lite(301, shifted, L, tid, seq, off))
+
+
 def lite_decode_records():
     """Every Lite decode fixture record, plus TopicMessages and junk, at every start alignment."""
     import json
