@@ -2524,25 +2524,40 @@ void prof_commit(int which, hipEvent_t start) {
 // ------------------------------------------------------------------------------------------
 // Aeron fragment reassembly (LocalFragmentReassembler::onFragment, src/cluster_client.cpp:39-82)
 //   1-3. the inclusive scan of one element per fragment (delivery-point count, last BEGIN, last
-//      END, non-single bytes, singles) in three launches (frag_reduce, frag_scan_blocks,
-//      frag_scan: the elements are classified on the fly, never stored); message sizes zeroed
-//   4. frag_messages: every delivery point (a BEGIN|END single, or an END) sizes its message:
-//      the END's group is the non-single fragments since the last BEGIN or END before it; the
-//      open group at the end of the batch is the carry
-//   5. exclusive scan of the sizes → msg_off (hipCUB)
-//   6. frag_copy: one wave per 64 messages, runs of back-to-back messages copied as one block
+//      END, singles, the accumulator as an affine map) in three launches (frag_reduce,
+//      frag_scan_blocks, frag_scan: the elements are classified on the fly, never stored)
+//   4. frag_messages: every delivery point (a BEGIN|END single, or an END) writes its message's
+//      offset and size from the accumulator map, and the first / last fragment of its group (the
+//      non-single fragments since the last BEGIN or END before it); the open group at the end of
+//      the batch is the carry
+//   5. frag_copy: one wave per 64 messages, runs of back-to-back messages copied as one block
 //      (fragment by fragment only when a single sits inside a group)
 // ------------------------------------------------------------------------------------------
-struct FragScan {  // 24 bytes (batches of up to 2^31 fragments)
-    uint32_t dp;   // delivery points (singles + ENDs) so far
-    uint32_t sg;   // singles so far
+// The accumulator of onFragment as an affine map on (p = pending bytes, d = delivered bytes):
+// (p, d) -> (A p + B, d + C p + E), A, C in {0, 1}:
+//   single (BEGIN|END) A = 1, E = len;  BEGIN  A = 0, B = len;  middle  A = 1, B = len;
+//   END    A = 0, C = 1, E = len.
+// Maps compose associatively (g after f: A = Ag Af, B = Ag Bf + Bg, C = Cf + Cg Af, E = Ef + Cg Bf
+// + Eg; C stays 0 or 1: Cf = 1 implies Af = 0), so the inclusive scan gives, from (0, 0), the
+// pending and delivered bytes after every fragment: a message delivered at fragment i starts at
+// E(i - 1) in the output and has E(i) - E(i - 1) bytes, and the carry is B(n - 1).
+struct FragScan {  // 32 bytes (batches of up to 2^31 fragments, so bit 31 of dp / sg is free)
+    uint32_t dp;   // delivery points (singles + ENDs) so far; bit 31: C
+    uint32_t sg;   // singles so far; bit 31: A
     int32_t lb;    // last BEGIN (non-single) index so far, -1 none
     int32_t le;    // last END (non-single) index so far, -1 none
-    uint64_t ns;   // bytes of non-single fragments so far
+    uint64_t B, E; // the accumulator map (above)
 };
-struct FragScanOp {
+constexpr uint32_t kFsCount = 0x7fffffffu;
+__host__ __device__ __forceinline__ uint32_t fs_dp(const FragScan& e) { return e.dp & kFsCount; }
+__host__ __device__ __forceinline__ uint32_t fs_sg(const FragScan& e) { return e.sg & kFsCount; }
+struct FragScanOp {  // a before b
     __host__ __device__ FragScan operator()(const FragScan& a, const FragScan& b) const {
-        return FragScan{a.dp + b.dp, a.sg + b.sg, a.lb > b.lb ? a.lb : b.lb, a.le > b.le ? a.le : b.le, a.ns + b.ns};
+        const bool Aa = (a.sg >> 31) != 0, Ab = (b.sg >> 31) != 0, Ca = (a.dp >> 31) != 0, Cb = (b.dp >> 31) != 0;
+        const uint32_t C = (Ca || (Cb && Aa)) ? 0x80000000u : 0u, A = (Aa && Ab) ? 0x80000000u : 0u;
+        return FragScan{((fs_dp(a) + fs_dp(b)) & kFsCount) | C, ((fs_sg(a) + fs_sg(b)) & kFsCount) | A,
+                        a.lb > b.lb ? a.lb : b.lb, a.le > b.le ? a.le : b.le,
+                        (Ab ? a.B : 0ull) + b.B, a.E + (Cb ? a.B : 0ull) + b.E};
     }
 };
 
@@ -2571,18 +2586,20 @@ __device__ __forceinline__ bool frag_single(uint8_t f) {
 // aggregates into exclusive block prefixes (one workgroup, 1024 at a time with a carry);
 // frag_scan re-classifies and writes the inclusive scan.  Elements are never materialised.
 constexpr int kFsPer = 4, kFsThreads = 256, kFsBlk = kFsPer * kFsThreads;
-__device__ __forceinline__ FragScan fs_identity() { return FragScan{0u, 0u, -1, -1, 0ull}; }
+__device__ __forceinline__ FragScan fs_identity() { return FragScan{0u, 0x80000000u, -1, -1, 0ull, 0ull}; }
 __device__ __forceinline__ FragScan fs_elem(const FragArgs& a, uint64_t i) {
     if (i >= a.n) return fs_identity();
     const uint8_t f = a.flags[i];
     const bool single = frag_single(f);
+    const bool begin = (f & SBE_FRAG_BEGIN) != 0, endf = (f & SBE_FRAG_END) != 0;
     const uint64_t len = a.frag_off[i + 1] - a.frag_off[i];
     FragScan e;
-    e.dp = (single || (f & SBE_FRAG_END)) ? 1u : 0u;
-    e.lb = (!single && (f & SBE_FRAG_BEGIN)) ? (int32_t)i : -1;
-    e.le = (!single && (f & SBE_FRAG_END)) ? (int32_t)i : -1;
-    e.ns = single ? 0u : len;
-    e.sg = single ? 1u : 0u;
+    e.dp = ((single || endf) ? 1u : 0u) | ((!single && endf) ? 0x80000000u : 0u);      // C: END
+    e.sg = (single ? 1u : 0u) | ((single || (!begin && !endf)) ? 0x80000000u : 0u);  // A: single / middle
+    e.lb = (!single && begin) ? (int32_t)i : -1;
+    e.le = (!single && endf) ? (int32_t)i : -1;
+    e.B = (!single && !endf) ? len : 0ull;  // BEGIN / middle
+    e.E = (single || endf) ? len : 0ull;    // single / END
     return e;
 }
 __device__ __forceinline__ FragScan fs_shfl_up(const FragScan& v, int d) {
@@ -2591,7 +2608,8 @@ __device__ __forceinline__ FragScan fs_shfl_up(const FragScan& v, int d) {
     t.sg = __shfl_up(v.sg, d, kWave);
     t.lb = __shfl_up(v.lb, d, kWave);
     t.le = __shfl_up(v.le, d, kWave);
-    t.ns = __shfl_up(v.ns, d, kWave);
+    t.B = __shfl_up(v.B, d, kWave);
+    t.E = __shfl_up(v.E, d, kWave);
     return t;
 }
 // inclusive scan across the wave (Hillis-Steele on shuffles: this is a small share of the work)
@@ -2630,20 +2648,17 @@ __device__ __forceinline__ FragScan fs_block(const FragArgs& a, uint64_t b, Frag
 __global__ __launch_bounds__(kFsThreads) void frag_reduce(FragArgs a, FragScan* agg) {
     __shared__ FragScan wt[kFsThreads / kWave];
     const uint64_t b = blockIdx.x;
-    const uint64_t i0 = b * kFsBlk + (uint64_t)threadIdx.x * kFsPer;
-#pragma unroll
-    for (int k = 0; k < kFsPer; ++k)
-        if (i0 + k <= a.n) a.msize[i0 + k] = 0;  // (msize[n] too: the carry slot)
     FragScan e[kFsPer], before;
     const FragScan tot = fs_block(a, b, e, wt, before);
     if (threadIdx.x == 0) agg[b] = tot;
 }
 // exclusive prefixes of the nb block aggregates, in place
-__global__ __launch_bounds__(kFsThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb) {
-    __shared__ FragScan wt[kFsThreads / kWave];
+constexpr int kFsbThreads = 1024;  // one workgroup: a million fragments' 977 aggregates in one pass
+__global__ __launch_bounds__(kFsbThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb) {
+    __shared__ FragScan wt[kFsbThreads / kWave];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     FragScan carry = fs_identity();
-    for (uint64_t c0 = 0; c0 < nb; c0 += kFsThreads) {
+    for (uint64_t c0 = 0; c0 < nb; c0 += kFsbThreads) {
         const uint64_t j = c0 + (uint64_t)tid;
         const FragScan v = j < nb ? agg[j] : fs_identity();
         const FragScan inc = fs_wave_scan(v, lane);
@@ -2654,7 +2669,7 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_blocks(FragScan* agg, ui
         __syncthreads();
         FragScan wpre = fs_identity(), tot = fs_identity();
 #pragma unroll
-        for (int k = 0; k < kFsThreads / kWave; ++k) {
+        for (int k = 0; k < kFsbThreads / kWave; ++k) {
             if (k < w) wpre = FragScanOp{}(wpre, wt[k]);
             tot = FragScanOp{}(tot, wt[k]);
         }
@@ -2676,15 +2691,14 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan(FragArgs a, const FragSc
 
 // group of non-single fragments ending at i (inclusive): from the later of the last BEGIN at or
 // before i and the fragment after the last END before i
-__device__ __forceinline__ void frag_group(const FragArgs& a, uint64_t i, int64_t le_before, uint64_t& s,
-                                          uint64_t& bytes, bool& gap) {
+// (its bytes come from the accumulator map: FragScan)
+__device__ __forceinline__ void frag_group(const FragArgs& a, uint64_t i, int64_t le_before, uint64_t& s, bool& gap) {
     const FragScan& e = a.sc[i];
     int64_t st = (int64_t)e.lb > le_before + 1 ? (int64_t)e.lb : le_before + 1;
     if (st < 0) st = 0;
     s = (uint64_t)st;
-    const uint64_t ns0 = s ? a.sc[s - 1].ns : 0u, sg0 = s ? a.sc[s - 1].sg : 0u;
-    bytes = e.ns - ns0;
-    gap = e.sg != sg0;
+    const uint32_t sg0 = s ? fs_sg(a.sc[s - 1]) : 0u;
+    gap = fs_sg(e) != sg0;
 }
 
 __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
@@ -2692,29 +2706,33 @@ __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
     if (i >= a.n) return;
     const uint8_t f = a.flags[i];
     const FragScan e = a.sc[i];
+    const uint64_t E0 = i ? a.sc[i - 1].E : 0ull;  // delivered bytes before fragment i
     const bool single = frag_single(f);
-    if ((single || (f & SBE_FRAG_END)) && e.dp >= 1 && e.dp <= a.n) {
-        const uint64_t j = e.dp - 1;
+    const uint32_t dp = fs_dp(e);
+    if ((single || (f & SBE_FRAG_END)) && dp >= 1 && dp <= a.n) {
+        const uint64_t j = dp - 1;
+        a.msize[j] = e.E - E0;
+        a.msg_off[j] = E0;
         if (single) {
-            a.msize[j] = a.frag_off[i + 1] - a.frag_off[i];
             a.mfirst[j] = i;
             a.mlast[j] = i;
         } else {
-            uint64_t s, bytes;
+            uint64_t s;
             bool gap;
-            frag_group(a, i, i ? a.sc[i - 1].le : -1, s, bytes, gap);
-            a.msize[j] = bytes;
+            frag_group(a, i, i ? a.sc[i - 1].le : -1, s, gap);
             a.mfirst[j] = s;
             a.mlast[j] = i | (gap ? (1ull << 63) : 0ull);
         }
     }
     if (i == a.n - 1) {  // the open accumulator after the last fragment: the carry
-        const uint64_t m = e.dp <= a.n ? e.dp : a.n;
-        uint64_t s, bytes;
+        const uint64_t m = dp <= a.n ? dp : a.n;
+        uint64_t s;
         bool gap;
-        frag_group(a, i, e.le, s, bytes, gap);
+        frag_group(a, i, e.le, s, gap);
+        const uint64_t bytes = e.B;  // pending bytes after the last fragment
         const bool open = (int64_t)s <= (int64_t)i && bytes > 0;
         a.msize[m] = open ? bytes : 0u;
+        a.msg_off[m] = e.E;
         a.mfirst[m] = s;
         a.mlast[m] = i | (gap ? (1ull << 63) : 0ull);
         a.counts[0] = m;
@@ -2844,12 +2862,6 @@ __global__ __launch_bounds__(256) void offsets_rebase(uint64_t* dst, const uint6
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) dst[i] = src[i] + base;
 }
 
-size_t frag_scan_temp(uint64_t n, hipStream_t s) {
-    size_t t1 = 0, t2 = 0;
-    (void)hipcub::DeviceScan::InclusiveScan(nullptr, t1, (FragScan*)nullptr, (FragScan*)nullptr, FragScanOp{}, n, s);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (uint64_t*)nullptr, (uint64_t*)nullptr, n + 1, s);
-    return (t1 > t2 ? t1 : t2) + 256;
-}
 
 // One encode request, whatever the layout (the C entry points fill it).
 struct EncReq {
@@ -3046,8 +3058,8 @@ int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64
 }
 
 size_t sbe_reassemble_workspace_size(uint64_t n) {
-    // scan elements, sizes, first / last fragment per message, scan temporary storage
-    return (size_t)(2 * n * sizeof(FragScan) + 3 * 8 * (n + 1) + 5 * 16) + frag_scan_temp(n ? n : 1, nullptr);
+    // block aggregates / scan elements, sizes, first / last fragment per message
+    return (size_t)(2 * n * sizeof(FragScan) + 3 * 8 * (n + 1) + 5 * 16);
 }
 
 int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const uint8_t* flags, uint64_t n,
@@ -3074,20 +3086,16 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     uint64_t* mfirst = reinterpret_cast<uint64_t*>(w);
     w = al(w + 8 * (n + 1));
     uint64_t* mlast = reinterpret_cast<uint64_t*>(w);
-    w = al(w + 8 * (n + 1));
-    void* tmp = reinterpret_cast<void*>(w);
-    size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
     FragArgs a{in, frag_off, flags, n, out, msg_off, counts, el, sc, msize, mfirst, mlast};
     const uint32_t blocks = (uint32_t)((n + 1 + 255) / 256);
-    const uint64_t nb = (n + 1 + kFsBlk - 1) / kFsBlk;  // (n + 1: frag_reduce also zeroes msize[n])
+    const uint64_t nb = (n + kFsBlk - 1) / kFsBlk;
     hipLaunchKernelGGL(frag_reduce, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, el);
-    hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsThreads), 0, s, el, nb);
+    hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsbThreads), 0, s, el, nb);
     hipLaunchKernelGGL(frag_scan, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return record_hip(e);
     hipLaunchKernelGGL(frag_messages, dim3(blocks), dim3(256), 0, s, a);
     e = hipGetLastError();
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, msize, msg_off, n + 1, s);
     if (e != hipSuccess) return record_hip(e);
     const uint64_t cb = (n + 1 + 4 * kFragGroup - 1) / (4 * kFragGroup);  // four waves per block
     hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < 4096 ? cb : 4096)), dim3(256), 0, s, a);
