@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
 }
 
 // Writing launch: one wave per kOpw Orders (WShape).  Their texts are contiguous in `out`: the
-// wave stages them in an LDS window (one byte write per character), stores the window with 16-byte
+// wave stages them in an LDS window (byte writes; a plain string run as one 16-byte store), stores the window with 16-byte
 // coalesced stores and moves the window on to the first record not yet written, until every record
 // is out.  Only a record larger than the window is written from its lane straight to HBM.  Records
 // past out_capacity are written by nobody.  The window is sized so that a wave's texts fit it in
