@@ -21,7 +21,11 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_scan.hpp>
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: the library is dlopen-ed (rccl_api)
+
+#include <mutex>
+#include <type_traits>
 
 #include <cstdint>
 #include <cstdio>
@@ -2493,15 +2497,18 @@ thread_local ProfRing g_prof[2];
 
 // The ring slot's (start, stop) events for this launch of `which`, or nulls when it is not
 // sampled.  They are handed to hipExtLaunchKernel, which timestamps the kernel's own dispatch.
-// The ring's events, created once (by sbe_profile_enable, outside any timed region).
-bool prof_ready(ProfRing& R) {
+// The ring's events, created once (by sbe_profile_enable, outside any timed region); the error of
+// the failing creation otherwise.
+hipError_t prof_ready(ProfRing& R) {
     if (!R.ready) {
         for (int i = 0; i < ProfRing::kCap; ++i)
-            for (int j = 0; j < 2; ++j)
-                if (hipEventCreate(&R.ev[i][j]) != hipSuccess) return false;
+            for (int j = 0; j < 2; ++j) {
+                const hipError_t e = hipEventCreate(&R.ev[i][j]);
+                if (e != hipSuccess) return e;
+            }
         R.ready = true;
     }
-    return true;
+    return hipSuccess;
 }
 
 void prof_slot(int which, hipEvent_t* start, hipEvent_t* stop) {
@@ -2509,7 +2516,7 @@ void prof_slot(int which, hipEvent_t* start, hipEvent_t* stop) {
     if (g_prof_every <= 0) return;
     ProfRing& R = g_prof[which];
     if (R.launches++ % (uint64_t)g_prof_every != 0) return;
-    if (!prof_ready(R)) return;
+    if (!R.ready) return;  // sbe_profile_enable creates the events; never inside a launch
     *start = R.ev[R.head][0];
     *stop = R.ev[R.head][1];
 }
@@ -2844,12 +2851,12 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
 // one ncclAllGather, then the shards move in one group of ncclSend / ncclRecv at the prefix
 // offsets, and the root rebases each received offset array by its shard's byte prefix.
 // ------------------------------------------------------------------------------------------
-__global__ void shard_size_put(uint64_t* dst, const uint64_t* out_off, uint64_t n, uint64_t cap) {
+__global__ void shard_size_put(uint64_t* dst, const uint64_t* out_off, uint64_t n, uint64_t cap, uint64_t off_cap) {
     if (threadIdx.x == 0) {
         dst[0] = out_off[n];
         dst[1] = n;
-        dst[2] = cap;  // the root's receive capacity (0 elsewhere)
-        dst[3] = 0;
+        dst[2] = cap;      // the root's receive capacity in bytes (0 elsewhere)
+        dst[3] = off_cap;  // the root's dst_off entries (0 elsewhere)
     }
 }
 
@@ -3156,25 +3163,117 @@ int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what
     return record_hip(hipGetLastError());
 }
 
+// RCCL is loaded on the first communicator call (dlopen), so the codec itself needs no RCCL to
+// load.  In a process that already holds an RCCL (torch's), that same library is used.
+struct RcclApi {
+    bool loaded = false;
+    char err[160] = "";
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+static RcclApi& rccl_api() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);  // the process's own RCCL first
+        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            std::snprintf(api.err, sizeof(api.err), "RCCL not loadable: %s", dlerror());
+            return;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            ok = ok && fn != nullptr;
+        };
+        sym(api.GetUniqueId, "ncclGetUniqueId");
+        sym(api.CommInitRank, "ncclCommInitRank");
+        sym(api.CommDestroy, "ncclCommDestroy");
+        sym(api.AllGather, "ncclAllGather");
+        sym(api.Send, "ncclSend");
+        sym(api.Recv, "ncclRecv");
+        sym(api.GroupStart, "ncclGroupStart");
+        sym(api.GroupEnd, "ncclGroupEnd");
+        sym(api.GetErrorString, "ncclGetErrorString");
+        if (!ok) std::snprintf(api.err, sizeof(api.err), "RCCL lacks a required symbol");
+        api.loaded = ok;
+    });
+    return api;
+}
+
+static int rccl_ready() {
+    RcclApi& r = rccl_api();
+    if (r.loaded) return SBE_OK;
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s", r.err);
+    return SBE_ECOMM;
+}
+
 struct sbe_comm {
     ncclComm_t nc = nullptr;
     int world = 0, rank = 0;
-    uint64_t* d_mine = nullptr;   // {bytes, n, root capacity, 0} of this rank (device, 32 B)
+    uint64_t* d_mine = nullptr;   // {bytes, n, root byte capacity, root offset capacity} (device, 32 B)
     uint64_t* d_all = nullptr;    // the same of every rank (device, 32 B per rank)
     uint64_t* h_all = nullptr;    // pinned host copy of d_all
+    uint64_t* byte_base = nullptr;  // host [world + 1]: the gather plan
+    uint64_t* rec_base = nullptr;
 };
 
 static int record_nccl(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return SBE_OK;
-    std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, ncclGetErrorString(r));
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, rccl_api().GetErrorString(r));
     return SBE_ECOMM;
+}
+
+int sbe_gather_plan(const uint64_t* ranks, int world, int root, uint64_t* byte_base, uint64_t* rec_base,
+                    uint64_t* totals) {
+    if (!ranks || world < 1 || root < 0 || root >= world || !byte_base || !rec_base) return SBE_EINVAL;
+    uint64_t b = 0, m = 0;
+    for (int r = 0; r < world; ++r) {
+        byte_base[r] = b;
+        rec_base[r] = m;
+        b += ranks[4 * r];
+        m += ranks[4 * r + 1];
+    }
+    byte_base[world] = b;
+    rec_base[world] = m;
+    if (totals) {
+        totals[0] = b;
+        totals[1] = m;
+    }
+    // every rank decides from the root's capacities: a short root buffer stops all of them before
+    // any transfer is posted
+    const uint64_t cap = ranks[4 * root + 2], off_cap = ranks[4 * root + 3];
+    if (b > cap) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "gather: root buffer holds %llu of %llu bytes",
+                      (unsigned long long)cap, (unsigned long long)b);
+        return SBE_ENOSPC;
+    }
+    if (m + 1 > off_cap) {
+        std::snprintf(g_last_error, sizeof(g_last_error), "gather: root offsets hold %llu of %llu entries",
+                      (unsigned long long)off_cap, (unsigned long long)(m + 1));
+        return SBE_ENOSPC;
+    }
+    return SBE_OK;
 }
 
 int sbe_comm_unique_id(uint8_t id[SBE_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == SBE_COMM_ID_BYTES, "RCCL unique id size");
     if (!id) return SBE_EINVAL;
+    int rc = rccl_ready();
+    if (rc != SBE_OK) return rc;
     ncclUniqueId u;
-    const int rc = record_nccl(ncclGetUniqueId(&u), "ncclGetUniqueId");
+    rc = record_nccl(rccl_api().GetUniqueId(&u), "ncclGetUniqueId");
     if (rc == SBE_OK) std::memcpy(id, &u, sizeof(u));
     return rc;
 }
@@ -3182,16 +3281,20 @@ int sbe_comm_unique_id(uint8_t id[SBE_COMM_ID_BYTES]) {
 int sbe_comm_init(sbe_comm** comm, int world, int rank, const uint8_t id[SBE_COMM_ID_BYTES]) {
     if (!comm || !id || world < 1 || rank < 0 || rank >= world) return SBE_EINVAL;
     *comm = nullptr;
+    int rc = rccl_ready();
+    if (rc != SBE_OK) return rc;
     sbe_comm* c = new sbe_comm;
     c->world = world;
     c->rank = rank;
-    int rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_mine), 32));
+    c->byte_base = new uint64_t[world + 1];
+    c->rec_base = new uint64_t[world + 1];
+    rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_mine), 32));
     if (rc == SBE_OK) rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_all), 32 * (size_t)world));
     if (rc == SBE_OK) rc = record_hip(hipHostMalloc(reinterpret_cast<void**>(&c->h_all), 32 * (size_t)world, 0));
     if (rc == SBE_OK) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        rc = record_nccl(ncclCommInitRank(&c->nc, world, u, rank), "ncclCommInitRank");
+        rc = record_nccl(rccl_api().CommInitRank(&c->nc, world, u, rank), "ncclCommInitRank");
     }
     if (rc != SBE_OK) {
         sbe_comm_destroy(c);
@@ -3204,93 +3307,91 @@ int sbe_comm_init(sbe_comm** comm, int world, int rank, const uint8_t id[SBE_COM
 int sbe_comm_destroy(sbe_comm* c) {
     if (!c) return SBE_OK;
     int rc = SBE_OK;
-    if (c->nc) rc = record_nccl(ncclCommDestroy(c->nc), "ncclCommDestroy");
+    if (c->nc) rc = record_nccl(rccl_api().CommDestroy(c->nc), "ncclCommDestroy");
     if (c->d_mine) (void)hipFree(c->d_mine);
     if (c->d_all) (void)hipFree(c->d_all);
     if (c->h_all) (void)hipHostFree(c->h_all);
+    delete[] c->byte_base;
+    delete[] c->rec_base;
     delete c;
     return rc;
 }
 
 int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t* out_off, uint64_t n,
-                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t* totals, void* stream) {
+                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t dst_off_capacity,
+                       uint64_t* totals, void* stream) {
     if (!c || !out_off || root < 0 || root >= c->world) return SBE_EINVAL;
     const bool am_root = c->rank == root;
     if (am_root && !dst_off) return SBE_EINVAL;
+    const RcclApi& R = rccl_api();
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // 1. every rank's {bytes, n} and the root's capacity
+    // 1. every rank's {bytes, n} and the root's capacities
     hipLaunchKernelGGL(shard_size_put, dim3(1), dim3(64), 0, s, c->d_mine, out_off, n,
-                       am_root && dst ? dst_capacity : 0ull);
+                       am_root && dst ? dst_capacity : 0ull, am_root ? dst_off_capacity : 0ull);
     int rc = record_hip(hipGetLastError());
     if (rc != SBE_OK) return rc;
-    rc = record_nccl(ncclAllGather(c->d_mine, c->d_all, 4, ncclUint64, c->nc, s), "ncclAllGather");
+    rc = record_nccl(R.AllGather(c->d_mine, c->d_all, 4, ncclUint64, c->nc, s), "ncclAllGather");
     if (rc != SBE_OK) return rc;
     rc = record_hip(hipMemcpyAsync(c->h_all, c->d_all, 32 * (size_t)c->world, hipMemcpyDeviceToHost, s));
     if (rc == SBE_OK) rc = record_hip(hipStreamSynchronize(s));
     if (rc != SBE_OK) return rc;
-    uint64_t total_b = 0, total_n = 0;
-    for (int r = 0; r < c->world; ++r) {
-        total_b += c->h_all[4 * r];
-        total_n += c->h_all[4 * r + 1];
-    }
+    uint64_t tot[2];
+    rc = sbe_gather_plan(c->h_all, c->world, root, c->byte_base, c->rec_base, tot);
     if (totals) {
-        totals[0] = total_b;
-        totals[1] = total_n;
+        totals[0] = tot[0];
+        totals[1] = tot[1];
     }
-    // every rank sees the root's capacity: a short root buffer stops all of them before any send
-    const uint64_t root_cap = c->h_all[4 * root + 2];
-    if (total_b > root_cap) {
-        std::snprintf(g_last_error, sizeof(g_last_error), "gather: root buffer holds %llu of %llu bytes",
-                      (unsigned long long)root_cap, (unsigned long long)total_b);
-        return SBE_ENOSPC;
-    }
-    // 2. the shards and their offsets, in one group
-    rc = record_nccl(ncclGroupStart(), "ncclGroupStart");
     if (rc != SBE_OK) return rc;
-    uint64_t base = 0, rbase = 0;
+    // 2. the shards and their offsets, in one group
+    rc = record_nccl(R.GroupStart(), "ncclGroupStart");
+    if (rc != SBE_OK) return rc;
     for (int r = 0; r < c->world && rc == SBE_OK; ++r) {
         const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
         if (r == c->rank && !am_root) {
-            if (b) rc = record_nccl(ncclSend(out, b, ncclUint8, root, c->nc, s), "ncclSend");
-            if (m && rc == SBE_OK) rc = record_nccl(ncclSend(out_off, m, ncclUint64, root, c->nc, s), "ncclSend");
+            if (b) rc = record_nccl(R.Send(out, b, ncclUint8, root, c->nc, s), "ncclSend");
+            if (m && rc == SBE_OK) rc = record_nccl(R.Send(out_off, m, ncclUint64, root, c->nc, s), "ncclSend");
         } else if (am_root && r != root) {
-            if (b) rc = record_nccl(ncclRecv(dst + base, b, ncclUint8, r, c->nc, s), "ncclRecv");
-            if (m && rc == SBE_OK) rc = record_nccl(ncclRecv(dst_off + rbase, m, ncclUint64, r, c->nc, s), "ncclRecv");
+            if (b) rc = record_nccl(R.Recv(dst + c->byte_base[r], b, ncclUint8, r, c->nc, s), "ncclRecv");
+            if (m && rc == SBE_OK)
+                rc = record_nccl(R.Recv(dst_off + c->rec_base[r], m, ncclUint64, r, c->nc, s), "ncclRecv");
         }
-        base += b;
-        rbase += m;
     }
-    const int rc_end = record_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    const int rc_end = record_nccl(R.GroupEnd(), "ncclGroupEnd");
     if (rc != SBE_OK) return rc;
     if (rc_end != SBE_OK) return rc_end;
     if (!am_root) return SBE_OK;
     // 3. root: its own shard, the offset rebase, the closing offset
-    base = rbase = 0;
     for (int r = 0; r < c->world; ++r) {
         const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
-        if (r == root && b) rc = record_hip(hipMemcpyAsync(dst + base, out, b, hipMemcpyDeviceToDevice, s));
+        if (r == root && b)
+            rc = record_hip(hipMemcpyAsync(dst + c->byte_base[r], out, b, hipMemcpyDeviceToDevice, s));
         if (rc != SBE_OK) return rc;
         if (m) {
             const uint64_t blocks = (m + 255) / 256;
-            hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s,
-                               dst_off + rbase, r == root ? out_off : dst_off + rbase, m, base);
+            uint64_t* d = dst_off + c->rec_base[r];
+            hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d,
+                               r == root ? out_off : d, m, c->byte_base[r]);
             rc = record_hip(hipGetLastError());
             if (rc != SBE_OK) return rc;
         }
-        base += b;
-        rbase += m;
     }
-    hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + total_n, total_b);
+    hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + tot[1], tot[0]);
     return record_hip(hipGetLastError());
 }
 
 int sbe_profile_enable(int every) {
     if (every < 0) return SBE_EINVAL;
+    // both rings' events first: profiling turns on only once they exist
+    if (every > 0)
+        for (auto& R : g_prof) {
+            const hipError_t e = prof_ready(R);
+            if (e != hipSuccess) {
+                g_prof_every = 0;
+                return record_hip(e);
+            }
+        }
     g_prof_every = every;
-    for (auto& R : g_prof) {
-        R.head = R.count = 0, R.launches = 0;
-        if (every > 0 && !prof_ready(R)) return record_hip(hipGetLastError());
-    }
+    for (auto& R : g_prof) R.head = R.count = 0, R.launches = 0;
     return SBE_OK;
 }
 

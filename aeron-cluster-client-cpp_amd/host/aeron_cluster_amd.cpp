@@ -1,22 +1,39 @@
 // aeron_cluster_amd.cpp — host side of the reference codec surface over the C ABI.
-// Host memory in, host memory out (the reference's API contract): each call stages its batch in
-// pinned buffers, copies it to HBM on a private stream, launches the HIP kernels through
-// include/sbecodec.h and copies the results back.  Results are materialised on the host from the
-// device descriptors (views into the caller's own bytes), never recomputed here.
+// Host memory in, host memory out (the reference's API contract).  Every batch call runs a
+// two-slot pipeline: the batch is cut into chunks of a few MiB; while chunk k is copied to HBM,
+// coded by the HIP kernels of include/sbecodec.h and copied back on stream k%2, the host threads
+// stage chunk k+1 in page-locked memory, so host staging, H2D, kernels and D2H overlap.  Encoded
+// bytes land by DMA directly in a recycled page-locked block the caller receives (HostBytes);
+// decode descriptors land in one the same way, and ParseResults are built from them on the host
+// threads.  Results are materialised from the device descriptors (views into the caller's own
+// bytes), never recomputed here.
 #include "aeron_cluster_amd.hpp"
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <ctime>
+#include <iomanip>
 #include <iostream>
+#include <map>
 #include <mutex>
+#include <sstream>
 #include <stdexcept>
+#include <thread>
 
 #include "sbecodec.h"
 
 namespace aeron_cluster {
+
+// ======================================================================================
+// host runtime: worker threads, page-locked block pool
+// ======================================================================================
 namespace {
 
 [[noreturn]] void fail(const char* what) {
@@ -27,7 +44,149 @@ void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("sbecodec: ") + what + ": " + hipGetErrorString(e));
 }
 
-// Growable device / pinned host buffer.
+// A fixed set of worker threads (AERON_AMD_HOST_THREADS, default min(16, cores)) that run the
+// tasks of one parallel_for at a time; the calling thread takes tasks too.  A second caller
+// arriving while a loop runs executes its own loop inline (the mirror's entry points are
+// reentrant across threads, like the reference's static codec functions).
+class Workers {
+public:
+    static Workers& get() {
+        static Workers* w = new Workers();  // never destroyed: the threads outlive static teardown
+        return *w;
+    }
+    unsigned size() const { return (unsigned)threads_.size() + 1; }
+
+    template <class F>
+    void parallel_for(size_t ntasks, F&& fn) {
+        if (ntasks == 0) return;
+        std::unique_lock<std::mutex> call(call_m_, std::try_to_lock);
+        if (ntasks == 1 || threads_.empty() || !call.owns_lock()) {
+            for (size_t t = 0; t < ntasks; ++t) fn(t);
+            return;
+        }
+        std::function<void(size_t)> job(std::forward<F>(fn));
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            ntasks_ = ntasks;
+            next_.store(0);
+            busy_ = (unsigned)threads_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        run_tasks(job, ntasks);
+        std::unique_lock<std::mutex> g(m_);
+        done_cv_.wait(g, [&] { return busy_ == 0; });
+        job_ = nullptr;
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);
+        }
+    }
+
+private:
+    Workers() {
+        unsigned n = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = std::getenv("AERON_AMD_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(e));
+        for (unsigned i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
+        for (auto& t : threads_) t.detach();
+    }
+    void run_tasks(const std::function<void(size_t)>& job, size_t ntasks) {
+        for (size_t t; (t = next_.fetch_add(1)) < ntasks;) {
+            try {
+                job(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(m_);
+                if (!err_) err_ = std::current_exception();
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t)>* job;
+            size_t ntasks;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                job = job_;
+                ntasks = ntasks_;
+            }
+            run_tasks(*job, ntasks);
+            std::lock_guard<std::mutex> g(m_);
+            if (--busy_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> threads_;
+    std::mutex call_m_, m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)>* job_ = nullptr;
+    size_t ntasks_ = 0;
+    std::atomic<size_t> next_{0};
+    unsigned busy_ = 0;
+    uint64_t gen_ = 0;
+    std::exception_ptr err_;
+};
+
+// parallel_for over [0, n) in contiguous ranges of at least `grain` items: fn(lo, hi).
+template <class F>
+void for_ranges(size_t n, size_t grain, F&& fn) {
+    Workers& w = Workers::get();
+    const size_t maxt = (size_t)w.size() * 4;
+    size_t ntasks = std::min(maxt, std::max<size_t>(1, n / std::max<size_t>(grain, 1)));
+    if (ntasks <= 1) {
+        if (n) fn(size_t(0), n);
+        return;
+    }
+    w.parallel_for(ntasks, [&](size_t t) { fn(n * t / ntasks, n * (t + 1) / ntasks); });
+}
+
+// Page-locked host blocks recycled by size class (powers of two from 64 KiB); hipHostMalloc costs
+// milliseconds per call for large blocks, so a block is allocated once and reused.
+class PinnedPool {
+public:
+    static PinnedPool& get() {
+        static PinnedPool* p = new PinnedPool();  // never destroyed (blocks may outlive statics)
+        return *p;
+    }
+    std::shared_ptr<void> take(size_t bytes) {
+        size_t cls = size_t(1) << 16;
+        while (cls < bytes) cls <<= 1;
+        void* p = nullptr;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            auto& fl = free_[cls];
+            if (!fl.empty()) {
+                p = fl.back();
+                fl.pop_back();
+                cached_ -= cls;
+            }
+        }
+        if (!p) hip_check(hipHostMalloc(&p, cls, hipHostMallocDefault), "hipHostMalloc");
+        return std::shared_ptr<void>(p, [this, cls](void* q) { give(q, cls); });
+    }
+
+private:
+    void give(void* p, size_t cls) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            if (cached_ + cls <= kMaxCached) {
+                free_[cls].push_back(p);
+                cached_ += cls;
+                return;
+            }
+        }
+        (void)hipHostFree(p);
+    }
+    static constexpr size_t kMaxCached = size_t(4) << 30;
+    std::mutex m_;
+    std::map<size_t, std::vector<void*>> free_;
+    size_t cached_ = 0;
+};
+
+// Growable device / page-locked buffer owned by one thread's context.
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -40,6 +199,7 @@ struct DevBuf {
         hip_check(hipMalloc(&p, c), "hipMalloc");
         cap = c;
     }
+    uint8_t* b() const { return static_cast<uint8_t*>(p); }
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
@@ -56,22 +216,46 @@ struct HostBuf {
         hip_check(hipHostMalloc(&p, c, hipHostMallocDefault), "hipHostMalloc");
         cap = c;
     }
+    uint8_t* b() const { return static_cast<uint8_t*>(p); }
     ~HostBuf() {
         if (p) (void)hipHostFree(p);
     }
 };
 
+// One pipeline slot: a stream, its staging buffers, and an event marking its input copy done.
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t in_done = nullptr;
+    bool pending = false;  // in_done recorded and not yet waited for
+    HostBuf pin_in;
+    DevBuf d_in, d_out;
+    void wait_input_free() {
+        if (pending) hip_check(hipEventSynchronize(in_done), "hipEventSynchronize");
+        pending = false;
+    }
+};
+
 // Per-thread device context (the reference's codec functions are reentrant statics).
 struct Ctx {
-    hipStream_t stream = nullptr;
-    DevBuf d_arena, d_len, d_ts, d_out, d_off, d_st, d_ws, d_in, d_roff, d_dec;
-    HostBuf h_arena, h_len, h_ts, h_out, h_off, h_st, h_in, h_roff, h_dec;
+    Slot slot[2];
+    DevBuf d_aux;   // reassembly / Order JSON
+    HostBuf h_aux;
     Ctx() {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");
-        hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (Slot& s : slot) {
+            hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+            hip_check(hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming), "hipEventCreate");
+        }
     }
     ~Ctx() {
-        if (stream) (void)hipStreamDestroy(stream);
+        for (Slot& s : slot) {
+            if (s.in_done) (void)hipEventDestroy(s.in_done);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+        }
+    }
+    void sync_all() {
+        for (Slot& s : slot) hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
+        for (Slot& s : slot) s.pending = false;
     }
 };
 
@@ -80,81 +264,341 @@ Ctx& ctx() {
     return c;
 }
 
+inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// AERON_AMD_TRACE=1: one line per batch call on stderr with its phase times (diagnosis only)
+struct Trace {
+    using clk = std::chrono::steady_clock;
+    bool on;
+    const char* what;
+    clk::time_point t0, last;
+    double plan = 0, stage = 0, wait = 0, enqueue = 0, sync = 0, finish = 0;
+    explicit Trace(const char* w) : on(enabled()), what(w) {
+        if (on) t0 = last = clk::now();
+    }
+    static bool enabled() {
+        static const bool e = [] {
+            const char* v = std::getenv("AERON_AMD_TRACE");
+            return v && v[0] == '1';
+        }();
+        return e;
+    }
+    void lap(double& acc) {
+        if (!on) return;
+        const clk::time_point t = clk::now();
+        acc += std::chrono::duration<double, std::micro>(t - last).count();
+        last = t;
+    }
+    void done(size_t n, size_t chunks) {
+        if (!on) return;
+        std::fprintf(stderr,
+                     "[trace] %s n=%zu chunks=%zu threads=%u total=%.1fus plan=%.1f stage=%.1f wait=%.1f enqueue=%.1f sync=%.1f "
+                     "finish=%.1f\n",
+                     what, n, chunks, Workers::get().size(), std::chrono::duration<double, std::micro>(clk::now() - t0).count(), plan, stage,
+                     wait, enqueue, sync, finish);
+    }
+};
+
+// Bytes of staged work per pipeline chunk (AERON_AMD_CHUNK_BYTES, default 8 MiB).
+size_t chunk_target_bytes() {
+    static const size_t v = [] {
+        const char* e = std::getenv("AERON_AMD_CHUNK_BYTES");
+        const long long x = e ? std::atoll(e) : 0;
+        return x > 0 ? (size_t)x : (size_t(8) << 20);
+    }();
+    return v;
+}
+// Records per chunk: a power of two so that a chunk holds about chunk_target_bytes().
+size_t chunk_records(size_t n, size_t total_bytes) {
+    const size_t avg = std::max<size_t>(1, total_bytes / std::max<size_t>(n, 1));
+    size_t c = 1;
+    while (c < n && c < 65536 && (c * 2) * avg <= chunk_target_bytes()) c *= 2;
+    return c;
+}
+
+// Exclusive prefix sums of per-item values produced by val(i), in parallel ranges: out[0..n].
+template <class V>
+void prefix(size_t n, std::vector<uint64_t>& out, V&& val) {
+    out.resize(n + 1);
+    Workers& w = Workers::get();
+    const size_t ntasks = n < 65536 ? 1 : std::min<size_t>(w.size() * 2, n / 16384);
+    std::vector<uint64_t> part(ntasks + 1, 0);
+    auto lo = [&](size_t t) { return n * t / ntasks; };
+    w.parallel_for(ntasks, [&](size_t t) {
+        uint64_t s = 0;
+        for (size_t i = lo(t); i < lo(t + 1); ++i) {
+            out[i] = s;
+            s += val(i);
+        }
+        part[t + 1] = s;
+    });
+    for (size_t t = 0; t < ntasks; ++t) part[t + 1] += part[t];
+    w.parallel_for(ntasks, [&](size_t t) {
+        if (part[t])
+            for (size_t i = lo(t); i < lo(t + 1); ++i) out[i] += part[t];
+    });
+    out[n] = part[ntasks];
+}
+
+}  // namespace
+
+namespace detail {
+struct HostBytesAccess {
+    static HostBytes make(size_t n) {
+        HostBytes h;
+        if (n) {
+            h.block_ = PinnedPool::get().take(n);
+            h.p_ = static_cast<uint8_t*>(h.block_.get());
+        }
+        h.n_ = n;
+        return h;
+    }
+    static HostBytes from(const uint8_t* p, size_t n) {
+        HostBytes h = make(n);
+        if (n) std::memcpy(h.p_, p, n);
+        return h;
+    }
+};
+
+// Host copy of the decode descriptors, chunk-major: chunk c (records [c*C, c*C + C)) is the
+// device's struct of arrays for C records, copied back as one block.
+struct Descriptors {
+    std::shared_ptr<void> block;
+    size_t n = 0;
+    unsigned shift = 0;  // C = 1 << shift
+    size_t chunk_bytes = 0;
+    size_t o_fl = 0, o_hdr = 0, o_ts = 0, o_off = 0, o_len = 0, o_seq = 0;
+    bool has_seq = false;
+
+    void layout(size_t C, bool seq) {
+        shift = 0;
+        while ((size_t(1) << shift) < C) ++shift;
+        o_fl = al16(C);
+        o_hdr = o_fl + al16(C);
+        o_ts = o_hdr + al16(8 * C);
+        o_off = o_ts + al16(8 * C);
+        o_len = o_off + al16(20 * C);
+        o_seq = o_len + al16(20 * C);
+        chunk_bytes = o_seq + (seq ? al16(8 * C) : 0);
+        has_seq = seq;
+    }
+    const uint8_t* base(size_t i) const {
+        return static_cast<const uint8_t*>(block.get()) + (i >> shift) * chunk_bytes;
+    }
+    size_t j(size_t i) const { return i & ((size_t(1) << shift) - 1); }
+    uint8_t status(size_t i) const { return base(i)[j(i)]; }
+    uint8_t flags(size_t i) const { return base(i)[o_fl + j(i)]; }
+    const uint16_t* hdr(size_t i) const { return reinterpret_cast<const uint16_t*>(base(i) + o_hdr) + 4 * j(i); }
+    uint64_t ts(size_t i) const { return reinterpret_cast<const uint64_t*>(base(i) + o_ts)[j(i)]; }
+    const uint32_t* off(size_t i) const { return reinterpret_cast<const uint32_t*>(base(i) + o_off) + 5 * j(i); }
+    const uint32_t* len(size_t i) const { return reinterpret_cast<const uint32_t*>(base(i) + o_len) + 5 * j(i); }
+    // ParseResult.sequence_number: the device evaluates it for flagged TopicMessages only
+    // (include/sbecodec.h, sbe_decoded.seq); every other record's is 0
+    uint64_t seq(size_t i) const {
+        if (!has_seq || status(i) != SBE_ST_TM || !(flags(i) & (SBE_FL_SEQ_KEY | SBE_FL_SEQ_ESC))) return 0;
+        return reinterpret_cast<const uint64_t*>(base(i) + o_seq)[j(i)];
+    }
+};
+}  // namespace detail
+
+using detail::Descriptors;
+using detail::HostBytesAccess;
+
+namespace {
+
+// Decode n records data[rec_off[i], rec_off[i+1]) with `mode` through the two-slot pipeline.
+std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
+    auto d = std::make_shared<Descriptors>();
+    d->n = n;
+    if (n == 0) return d;
+    Trace tr("decode");
+    Ctx& c = ctx();
+    const uint64_t base = rec_off[0], total = rec_off[n] - base;
+    const size_t C = chunk_records(n, (size_t)total);
+    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
+    d->layout(C, parse);
+    const size_t K = (n + C - 1) / C;
+    d->block = PinnedPool::get().take(K * d->chunk_bytes);
+    uint8_t* hblk = static_cast<uint8_t*>(d->block.get());
+    tr.lap(tr.plan);
+    for (size_t k = 0; k < K; ++k) {
+        Slot& s = c.slot[k & 1];
+        const size_t a = k * C, m = std::min(n, a + C) - a;
+        const uint64_t lo = rec_off[a], bytes = rec_off[a + m] - lo;
+        const size_t o_data = al16((m + 1) * 8), in_bytes = o_data + bytes;
+        s.wait_input_free();
+        tr.lap(tr.wait);
+        s.pin_in.need(in_bytes + 16);
+        uint8_t* pin = s.pin_in.b();
+        uint64_t* ro = reinterpret_cast<uint64_t*>(pin);
+        // stage: the chunk's offsets rebased to 0 and its bytes (16-B aligned on the device)
+        for_ranges(m + 1, 8192, [&](size_t x, size_t y) {
+            for (size_t i = x; i < y; ++i) ro[i] = rec_off[a + i] - lo;
+        });
+        for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) {
+            std::memcpy(pin + o_data + x, data + lo + x, y - x);
+        });
+        tr.lap(tr.stage);
+        s.d_in.need(in_bytes + 16);
+        s.d_out.need(d->chunk_bytes);
+        hip_check(hipMemcpyAsync(s.d_in.p, pin, in_bytes, hipMemcpyHostToDevice, s.stream), "H2D");
+        hip_check(hipEventRecord(s.in_done, s.stream), "hipEventRecord");
+        s.pending = true;
+        uint8_t* db = s.d_out.b();
+        sbe_decoded out{db,
+                        db + d->o_fl,
+                        reinterpret_cast<uint16_t*>(db + d->o_hdr),
+                        reinterpret_cast<uint64_t*>(db + d->o_ts),
+                        reinterpret_cast<uint32_t*>(db + d->o_off),
+                        reinterpret_cast<uint32_t*>(db + d->o_len),
+                        parse ? reinterpret_cast<uint64_t*>(db + d->o_seq) : nullptr};
+        if (sbe_decode_batch(s.d_in.b() + o_data, reinterpret_cast<const uint64_t*>(s.d_in.p), m, mode, &out, s.stream) !=
+            SBE_OK)
+            fail("sbe_decode_batch");
+        hip_check(hipMemcpyAsync(hblk + k * d->chunk_bytes, db, d->chunk_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+        tr.lap(tr.enqueue);
+    }
+    c.sync_all();
+    tr.lap(tr.sync);
+    tr.done(n, K);
+    return d;
+}
+
+// Per-record output size of an encode (the plan the chunks are placed by; the device offsets are
+// checked against it): overhead + Σ field lengths (PUBLISH_TOPIC: each mod 65536); a record with
+// a field above 65534 B is an E109 and emits nothing.
+struct EncodePlan {
+    uint32_t overhead = 0;
+    bool e109 = true;
+    bool wrap16 = false;
+};
+
+// Encode n records (nf strings, a u64 and a u32 each) through the two-slot pipeline.  launch(...)
+// issues one sbe_encode_*_batch call for a chunk.
+template <class Field, class U64, class U32, class Launch>
+EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, EncodePlan plan, Launch&& launch) {
+    EncodedBatch b;
+    b.offsets.assign(n + 1, 0);
+    b.status.assign(n, 0);
+    if (n == 0) return b;
+    Trace tr("encode");
+    Ctx& c = ctx();
+    std::vector<uint64_t> pin, pout;  // per-record input (string) bytes / output bytes, prefixed
+    prefix(n, pin, [&](size_t i) {
+        uint64_t s = 0;
+        for (int k = 0; k < nf; ++k) s += field(i, k).size();
+        return s;
+    });
+    prefix(n, pout, [&](size_t i) -> uint64_t {
+        uint64_t s = plan.overhead;
+        for (int k = 0; k < nf; ++k) {
+            const size_t L = field(i, k).size();
+            if (plan.e109 && L > SBE_VAR_MAX_LEN) return 0;
+            s += plan.wrap16 ? (L & 0xFFFF) : L;
+        }
+        return s;
+    });
+    const size_t C = chunk_records(n, (size_t)(pin[n] + pout[n]) / 2);
+    const size_t K = (n + C - 1) / C;
+    b.bytes = HostBytesAccess::make((size_t)pout[n]);
+    // per-chunk device offsets (C + 1) and status (C), copied back beside each other
+    const size_t meta_stride = al16((C + 1) * 8 + C);
+    std::shared_ptr<void> meta = PinnedPool::get().take(K * meta_stride);
+    uint8_t* hmeta = static_cast<uint8_t*>(meta.get());
+    const size_t ws_bytes = sbe_encode_workspace_size(C);
+    tr.lap(tr.plan);
+    for (size_t k = 0; k < K; ++k) {
+        Slot& s = c.slot[k & 1];
+        const size_t a = k * C, m = std::min(n, a + C) - a;
+        const uint64_t in_lo = pin[a], in_bytes = pin[a + m] - in_lo;
+        const uint64_t out_lo = pout[a], out_bytes = pout[a + m] - out_lo;
+        // staging layout: arena | u32 lengths [m][nf] | u64 [m] | u32 [m]
+        const size_t o_len = al16((size_t)in_bytes), o_u64 = o_len + al16((size_t)m * 4 * nf),
+                     o_u32 = o_u64 + al16(m * 8), stage = o_u32 + al16(m * 4);
+        s.wait_input_free();
+        tr.lap(tr.wait);
+        s.pin_in.need(stage);
+        uint8_t* p = s.pin_in.b();
+        uint32_t* lp = reinterpret_cast<uint32_t*>(p + o_len);
+        uint64_t* up = reinterpret_cast<uint64_t*>(p + o_u64);
+        uint32_t* wp = reinterpret_cast<uint32_t*>(p + o_u32);
+        for_ranges(m, 2048, [&](size_t x, size_t y) {
+            for (size_t r = x; r < y; ++r) {
+                const size_t i = a + r;
+                uint8_t* at = p + (pin[i] - in_lo);
+                for (int k2 = 0; k2 < nf; ++k2) {
+                    const std::string_view f = field(i, k2);
+                    if (!f.empty()) std::memcpy(at, f.data(), f.size());
+                    at += f.size();
+                    lp[(size_t)nf * r + k2] = (uint32_t)f.size();
+                }
+                up[r] = u64(i);
+                wp[r] = u32(i);
+            }
+        });
+        tr.lap(tr.stage);
+        // device: out bytes | out_off [m+1] | status [m] | workspace
+        const size_t d_off = al16((size_t)out_bytes), d_ws = d_off + meta_stride;
+        s.d_in.need(stage);
+        s.d_out.need(d_ws + ws_bytes);
+        hip_check(hipMemcpyAsync(s.d_in.p, p, stage, hipMemcpyHostToDevice, s.stream), "H2D");
+        hip_check(hipEventRecord(s.in_done, s.stream), "hipEventRecord");
+        s.pending = true;
+        const uint8_t* di = s.d_in.b();
+        uint8_t* dout = s.d_out.b();
+        launch(di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
+               reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
+               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, s.stream);
+        if (out_bytes)
+            hip_check(hipMemcpyAsync(b.bytes.data() + out_lo, dout, out_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+        hip_check(hipMemcpyAsync(hmeta + k * meta_stride, dout + d_off, (m + 1) * 8 + m, hipMemcpyDeviceToHost, s.stream),
+                  "D2H");
+        tr.lap(tr.enqueue);
+    }
+    c.sync_all();
+    tr.lap(tr.sync);
+    for (size_t k = 0; k < K; ++k) {
+        const size_t a = k * C, m = std::min(n, a + C) - a;
+        const uint64_t* off = reinterpret_cast<const uint64_t*>(hmeta + k * meta_stride);
+        if (off[m] != pout[a + m] - pout[a])
+            throw std::logic_error("sbecodec: encoded chunk size differs from its plan");
+    }
+    for_ranges(n, 16384, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i) {
+            const size_t k = i / C, j = i - k * C, m = std::min(n, k * C + C) - k * C;
+            const uint8_t* mk = hmeta + k * meta_stride;
+            b.offsets[i] = pout[k * C] + reinterpret_cast<const uint64_t*>(mk)[j];
+            b.status[i] = mk[(m + 1) * 8 + j];
+        }
+    });
+    b.offsets[n] = pout[n];
+    tr.lap(tr.finish);
+    tr.done(n, K);
+    return b;
+}
+
 inline int64_t rdi64(const uint8_t* p) {
     uint64_t v = 0;
     for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
     return (int64_t)v;
 }
 inline int32_t rdi32(const uint8_t* p) { return (int32_t)((uint32_t)p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)); }
+inline uint16_t rdu16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
-// device descriptors of n records, in one allocation
-struct Desc {
-    std::vector<uint8_t> status, flags;
-    std::vector<uint16_t> hdr;
-    std::vector<uint64_t> ts;
-    std::vector<uint32_t> off, len;
-    std::vector<uint64_t> seq;  // parse mode: ParseResult.sequence_number (sbe_eval_sequence_numbers)
-};
-
-Desc run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
-    Ctx& c = ctx();
-    Desc d;
-    if (n == 0) return d;
-    const uint64_t base = rec_off[0], total = rec_off[n] - base;
-    // records rebased to 0 so the device stream starts 16-B aligned
-    c.h_in.need(total + 16);
-    std::memcpy(c.h_in.p, data + base, total);
-    c.h_roff.need((n + 1) * 8);
-    uint64_t* ro = static_cast<uint64_t*>(c.h_roff.p);
-    for (size_t i = 0; i <= n; ++i) ro[i] = rec_off[i] - base;
-    c.d_in.need(total + 16);
-    c.d_roff.need((n + 1) * 8);
-    // descriptor SoA: status n, flags n, hdr 8n, ts 8n, off 20n, len 20n, seq 8n (each 16-B aligned)
-    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
-    const size_t o_st = 0, o_fl = al(n), o_hdr = o_fl + al(n), o_ts = o_hdr + al(8 * n), o_off = o_ts + al(8 * n),
-                 o_len = o_off + al(20 * n), o_seq = o_len + al(20 * n), dbytes = o_seq + (parse ? al(8 * n) : 0);
-    c.d_dec.need(dbytes);
-    c.h_dec.need(dbytes);
-    hip_check(hipMemcpyAsync(c.d_in.p, c.h_in.p, total, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_roff.p, c.h_roff.p, (n + 1) * 8, hipMemcpyHostToDevice, c.stream), "H2D");
-    uint8_t* db = static_cast<uint8_t*>(c.d_dec.p);
-    sbe_decoded out{db + o_st, db + o_fl, reinterpret_cast<uint16_t*>(db + o_hdr), reinterpret_cast<uint64_t*>(db + o_ts),
-                    reinterpret_cast<uint32_t*>(db + o_off), reinterpret_cast<uint32_t*>(db + o_len), nullptr};
-    if (parse) {  // sequence_number of the flagged TopicMessages, in the decode launch; 0 elsewhere
-        out.seq = reinterpret_cast<uint64_t*>(db + o_seq);
-        hip_check(hipMemsetAsync(out.seq, 0, 8 * n, c.stream), "memset");
-    }
-    if (sbe_decode_batch(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p), n, mode, &out, c.stream) != SBE_OK)
-        fail("sbe_decode_batch");
-    hip_check(hipMemcpyAsync(c.h_dec.p, c.d_dec.p, dbytes, hipMemcpyDeviceToHost, c.stream), "D2H");
-    hip_check(hipStreamSynchronize(c.stream), "sync");
-    const uint8_t* hb = static_cast<const uint8_t*>(c.h_dec.p);
-    d.status.assign(hb + o_st, hb + o_st + n);
-    d.flags.assign(hb + o_fl, hb + o_fl + n);
-    d.hdr.assign(reinterpret_cast<const uint16_t*>(hb + o_hdr), reinterpret_cast<const uint16_t*>(hb + o_hdr) + 4 * n);
-    d.ts.assign(reinterpret_cast<const uint64_t*>(hb + o_ts), reinterpret_cast<const uint64_t*>(hb + o_ts) + n);
-    d.off.assign(reinterpret_cast<const uint32_t*>(hb + o_off), reinterpret_cast<const uint32_t*>(hb + o_off) + 5 * n);
-    d.len.assign(reinterpret_cast<const uint32_t*>(hb + o_len), reinterpret_cast<const uint32_t*>(hb + o_len) + 5 * n);
-    if (parse)
-        d.seq.assign(reinterpret_cast<const uint64_t*>(hb + o_seq), reinterpret_cast<const uint64_t*>(hb + o_seq) + n);
-    return d;
-}
-
-ParseResult materialize(const uint8_t* rec, const Desc& d, size_t i) {
+ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
     ParseResult r;
-    const uint8_t st = d.status[i], fl = d.flags[i];
-    const uint16_t* h = &d.hdr[4 * i];
-    auto view = [&](int k) {
-        return std::string(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]);
-    };
+    const uint8_t st = d.status(i), fl = d.flags(i);
+    const uint16_t* h = d.hdr(i);
+    const uint32_t* off = d.off(i);
+    const uint32_t* len = d.len(i);
+    auto view = [&](int k) { return std::string(reinterpret_cast<const char*>(rec) + off[k], len[k]); };
     auto take_hdr = [&] {
         r.block_length = h[0];
         r.template_id = h[1];
         r.schema_id = h[2];
         r.version = h[3];
     };
-    const uint32_t param = d.off[5 * i];
+    const uint32_t param = off[0];
     switch (st) {
         case SBE_ST_TM:  // src/sbe_encoder.cpp:1021-1135
             r.success = true;
@@ -162,16 +606,16 @@ ParseResult materialize(const uint8_t* rec, const Desc& d, size_t i) {
             r.message_id = view(2);
             r.payload = view(3);
             r.headers = view(4);
-            r.timestamp = (int64_t)d.ts[i];
+            r.timestamp = (int64_t)d.ts(i);
             r.sequence_key_present = (fl & SBE_FL_SEQ_KEY) != 0;
-            r.sequence_number = d.seq.empty() ? 0 : d.seq[i];  // src/sbe_encoder.cpp:1031-1125
+            r.sequence_number = d.seq(i);  // src/sbe_encoder.cpp:1031-1125
             take_hdr();
             break;
         case SBE_ST_ACK:  // src/sbe_encoder.cpp:916-941
             r.success = true;
             r.message_type = "Acknowledgment";
-            r.timestamp = (int64_t)d.ts[i];
-            r.message_id = (fl & SBE_FL_ID_DEFAULT) ? "ack_" + std::to_string(d.ts[i]) : view(0);
+            r.timestamp = (int64_t)d.ts(i);
+            r.message_id = (fl & SBE_FL_ID_DEFAULT) ? "ack_" + std::to_string(d.ts(i)) : view(0);
             r.payload = (fl & SBE_FL_PAYLOAD_DEFAULT) ? std::string("SUCCESS") : view(1);
             r.headers = view(2);
             take_hdr();
@@ -221,80 +665,6 @@ const char* kE109[5] = {"topicLength too long for length type [E109]", "messageT
                         "uuidLength too long for length type [E109]", "payloadLength too long for length type [E109]",
                         "headersLength too long for length type [E109]"};
 
-}  // namespace
-
-bool ParseResult::is_topic_message() const {
-    if (template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID && schema_id == SBEConstants::TOPIC_SCHEMA_ID) return true;
-    if (schema_id == SBEConstants::CLUSTER_SCHEMA_ID && template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID) return true;
-    if (schema_id == SBEConstants::TOPIC_SCHEMA_ID && template_id == SBEConstants::SESSION_EVENT_TEMPLATE_ID) return true;
-    if (!message_type.empty() &&
-        (message_type.find("ORDER") != std::string::npos || message_type.find("TopicMessage") != std::string::npos ||
-         message_type.find("CREATE_ORDER") != std::string::npos || message_type.find("UPDATE_ORDER") != std::string::npos))
-        return true;
-    return false;
-}
-
-bool gpu_codec_available() { return sbe_device_ready() == 1; }
-
-namespace {
-// Stage a batch of records (nf strings, a u64 and a u32 each) in pinned memory, copy it to HBM,
-// run `launch` (one sbe_encode_*_batch call) and copy the encoded stream back.
-template <class Launch>
-EncodedBatch run_encode(size_t n, int nf, const std::function<std::string_view(size_t, int)>& field,
-                        const std::function<uint64_t(size_t)>& u64, const std::function<uint32_t(size_t)>& u32,
-                        uint64_t bound_per_record, Launch launch) {
-    Ctx& c = ctx();
-    EncodedBatch b;
-    b.offsets.assign(n + 1, 0);
-    b.status.assign(n, 0);
-    if (n == 0) return b;
-    size_t arena = 0;
-    for (size_t i = 0; i < n; ++i)
-        for (int k = 0; k < nf; ++k) arena += field(i, k).size();
-    c.h_arena.need(arena + 16);
-    c.h_len.need(n * 4 * nf);
-    c.h_ts.need(n * 12);
-    uint8_t* ap = static_cast<uint8_t*>(c.h_arena.p);
-    uint32_t* lp = static_cast<uint32_t*>(c.h_len.p);
-    uint64_t* tp = static_cast<uint64_t*>(c.h_ts.p);
-    uint32_t* ip = reinterpret_cast<uint32_t*>(tp + n);
-    size_t at = 0;
-    for (size_t i = 0; i < n; ++i) {
-        for (int k = 0; k < nf; ++k) {
-            const std::string_view f = field(i, k);
-            std::memcpy(ap + at, f.data(), f.size());
-            at += f.size();
-            lp[(size_t)nf * i + k] = (uint32_t)f.size();
-        }
-        tp[i] = u64(i);
-        ip[i] = u32(i);
-    }
-    const uint64_t cap = arena + bound_per_record * n + 16;
-    c.d_arena.need(arena + 16);
-    c.d_len.need(n * 4 * nf);
-    c.d_ts.need(n * 12);
-    c.d_out.need(cap);
-    c.d_off.need((n + 1) * 8);
-    c.d_st.need(n);
-    c.d_ws.need(sbe_encode_workspace_size(n));
-    hip_check(hipMemcpyAsync(c.d_arena.p, ap, arena, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_len.p, lp, n * 4 * nf, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_ts.p, tp, n * 12, hipMemcpyHostToDevice, c.stream), "H2D");
-    const uint64_t* d_u64 = static_cast<const uint64_t*>(c.d_ts.p);
-    launch(static_cast<const uint8_t*>(c.d_arena.p), static_cast<const uint32_t*>(c.d_len.p), d_u64,
-           reinterpret_cast<const uint32_t*>(d_u64 + n), static_cast<uint8_t*>(c.d_out.p), cap,
-           static_cast<uint64_t*>(c.d_off.p), static_cast<uint8_t*>(c.d_st.p), c.d_ws.p, c.d_ws.cap, c.stream);
-    hip_check(hipMemcpyAsync(b.offsets.data(), c.d_off.p, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
-    hip_check(hipMemcpyAsync(b.status.data(), c.d_st.p, n, hipMemcpyDeviceToHost, c.stream), "D2H");
-    hip_check(hipStreamSynchronize(c.stream), "sync");
-    b.bytes.resize(b.offsets[n]);
-    if (b.offsets[n]) {
-        hip_check(hipMemcpyAsync(b.bytes.data(), c.d_out.p, b.offsets[n], hipMemcpyDeviceToHost, c.stream), "D2H");
-        hip_check(hipStreamSynchronize(c.stream), "sync");
-    }
-    return b;
-}
-
 std::string_view tm_field(const TopicMessageFields& m, int k) {
     switch (k) {
         case 0: return m.topic;
@@ -315,31 +685,199 @@ uint64_t clock_ns() {
                std::chrono::high_resolution_clock::now().time_since_epoch())
         .count();
 }
+uint64_t now_nanos_sys() {  // include/aeron_cluster/protocol.hpp:31-34
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
 
 EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength length, bool session, int64_t term,
                        int64_t sess, uint64_t ts_default) {
     const uint32_t flags = length == EncodeLength::Reference ? SBE_ENC_REF_TRUNCATE8
                          : length == EncodeLength::Publish   ? SBE_ENC_PUBLISH_TOPIC
                                                              : 0u;
+    EncodePlan plan;
+    plan.overhead = (length == EncodeLength::Reference ? SBE_TM_REF_OVERHEAD : SBE_TM_WIRE_OVERHEAD) +
+                    (session ? SBE_SESSION_HDR_LEN : 0u);
+    plan.e109 = length != EncodeLength::Publish;
+    plan.wrap16 = length == EncodeLength::Publish;
     return run_encode(
         msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
-        [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; },
-        SBE_TM_WIRE_OVERHEAD + SBE_SESSION_HDR_LEN,
-        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, uint8_t* out, uint64_t cap,
-            uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+        [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; }, plan,
+        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, size_t m, uint8_t* out,
+            uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
             sbe_tm_batch in{arena, nullptr, len, ts};
-            const int rc = session ? sbe_encode_session_batch(&in, msgs.size(), ts_default, flags, term, sess, out, cap,
-                                                              off, st, ws, wsb, s)
-                                   : sbe_encode_topic_batch(&in, msgs.size(), ts_default, flags, out, cap, off, st, ws,
-                                                            wsb, s);
+            const int rc = session ? sbe_encode_session_batch(&in, m, ts_default, flags, term, sess, out, cap, off, st,
+                                                              ws, wsb, s)
+                                   : sbe_encode_topic_batch(&in, m, ts_default, flags, out, cap, off, st, ws, wsb, s);
             if (rc != SBE_OK) fail(session ? "sbe_encode_session_batch" : "sbe_encode_topic_batch");
         });
 }
+
+// DEBUG_LOG of the reference (include/aeron_cluster/debug_utils.hpp:11-28, 71): on stdout when
+// AERON_CLUSTER_DEBUG=1
+bool debug_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("AERON_CLUSTER_DEBUG");
+        return e && std::string(e) == "1";
+    }();
+    return on;
+}
+template <class... A>
+void debug_log(const A&... a) {
+    if (!debug_enabled()) return;
+    std::cout << "[DEBUG] ";
+    (std::cout << ... << a);
+    std::cout << std::endl;
+}
+
 }  // namespace
 
+// ======================================================================================
+// SBEUtils (src/sbe_encoder.cpp:328-485) and ParseResult (sbe_messages.hpp:340-411)
+// ======================================================================================
+namespace SBEUtils {
+
+void print_hex_dump(const std::uint8_t* data, std::size_t length, const std::string& prefix, std::size_t max_bytes) {
+    if (!data || length == 0) return;
+    const size_t shown = max_bytes > 0 ? std::min(length, max_bytes) : length;
+    for (size_t row = 0; row < shown; row += 16) {
+        std::cout << prefix << std::setfill('0') << std::setw(4) << std::hex << row << ": ";
+        for (size_t j = 0; j < 16; ++j) {
+            if (row + j < shown)
+                std::cout << std::setfill('0') << std::setw(2) << std::hex << static_cast<unsigned>(data[row + j]) << " ";
+            else
+                std::cout << "   ";
+            if (j == 7) std::cout << " ";
+        }
+        std::cout << " |";
+        for (size_t j = 0; j < 16 && row + j < shown; ++j) {
+            const char ch = static_cast<char>(data[row + j]);
+            std::cout << ((ch >= 32 && ch <= 126) ? ch : '.');
+        }
+        std::cout << "|" << std::dec << std::endl;
+    }
+    if (max_bytes > 0 && length > max_bytes) std::cout << prefix << "... (" << (length - max_bytes) << " more bytes)" << std::endl;
+}
+
+std::string get_session_event_code_string(std::int32_t code) {
+    switch (code) {
+        case SBEConstants::SESSION_EVENT_OK: return "OK";
+        case SBEConstants::SESSION_EVENT_ERROR: return "ERROR";
+        case SBEConstants::SESSION_EVENT_AUTHENTICATION_REJECTED: return "AUTHENTICATION_REJECTED";
+        case SBEConstants::SESSION_EVENT_REDIRECT: return "REDIRECT";
+        case SBEConstants::SESSION_EVENT_CLOSED: return "CLOSED";
+        default: return "UNKNOWN(" + std::to_string(code) + ")";
+    }
+}
+
+std::string get_message_type_name(std::uint16_t template_id, std::uint16_t schema_id) {
+    if (schema_id == SBEConstants::CLUSTER_SCHEMA_ID) {
+        if (template_id == SBEConstants::SESSION_CONNECT_TEMPLATE_ID) return "SessionConnectRequest";
+        if (template_id == SBEConstants::SESSION_EVENT_TEMPLATE_ID) return "SessionEvent";
+        return "UnknownClusterMessage(" + std::to_string(template_id) + ")";
+    }
+    if (schema_id == SBEConstants::TOPIC_SCHEMA_ID) {
+        if (template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID) return "TopicMessage";
+        if (template_id == SBEConstants::ACKNOWLEDGMENT_TEMPLATE_ID) return "Acknowledgment";
+        return "UnknownTopicMessage(" + std::to_string(template_id) + ")";
+    }
+    return "UnknownSchema(" + std::to_string(schema_id) + "," + std::to_string(template_id) + ")";
+}
+
+bool is_valid_correlation_id(std::int64_t correlation_id) { return correlation_id > 0; }
+
+std::int64_t generate_correlation_id() {
+    return (std::int64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count() & 0x7FFFFFFFFFFFFFFFLL;
+}
+
+std::string format_timestamp(std::int64_t timestamp) {
+    const std::time_t secs = std::chrono::system_clock::to_time_t(
+        std::chrono::time_point<std::chrono::system_clock>(std::chrono::nanoseconds(timestamp)));
+    std::stringstream ss;
+    ss << std::put_time(std::gmtime(&secs), "%Y-%m-%d %H:%M:%S UTC");
+    ss << "." << std::setfill('0') << std::setw(9) << (timestamp % 1000000000);
+    return ss.str();
+}
+
+bool is_valid_sbe_message(const std::uint8_t* data, std::size_t length) {
+    if (!data || length < SBEConstants::SBE_HEADER_LENGTH) return false;
+    const uint16_t blk = rdu16(data), schema = rdu16(data + 4);
+    if (blk == 0 || blk > 10000) return false;
+    if (length < SBEConstants::SBE_HEADER_LENGTH + blk) return false;
+    return schema == SBEConstants::CLUSTER_SCHEMA_ID || schema == SBEConstants::TOPIC_SCHEMA_ID;
+}
+
+std::vector<std::string> extract_readable_strings(const std::uint8_t* data, std::size_t length, std::size_t min_length) {
+    std::vector<std::string> out;
+    if (!data || length == 0) return out;
+    size_t start = 0;
+    for (size_t i = 0; i <= length; ++i) {
+        const bool printable = i < length && data[i] >= 32 && data[i] <= 126;
+        if (printable) continue;
+        if (i - start >= min_length) out.emplace_back(reinterpret_cast<const char*>(data) + start, i - start);
+        start = i + 1;
+    }
+    return out;
+}
+
+}  // namespace SBEUtils
+
+bool ParseResult::is_topic_message() const {
+    if (template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID && schema_id == SBEConstants::TOPIC_SCHEMA_ID) return true;
+    if (schema_id == SBEConstants::CLUSTER_SCHEMA_ID && template_id == SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID) return true;
+    if (schema_id == SBEConstants::TOPIC_SCHEMA_ID && template_id == SBEConstants::SESSION_EVENT_TEMPLATE_ID) return true;
+    if (!message_type.empty() &&
+        (message_type.find("ORDER") != std::string::npos || message_type.find("TopicMessage") != std::string::npos ||
+         message_type.find("CREATE_ORDER") != std::string::npos || message_type.find("UPDATE_ORDER") != std::string::npos))
+        return true;
+    return false;
+}
+
+bool ParseResult::is_order_message() const {
+    if (!is_topic_message()) return false;
+    // every keyword of the reference's type list contains "ORDER" (sbe_messages.hpp:386-391)
+    if (!message_type.empty() && message_type.find("ORDER") != std::string::npos) return true;
+    if (payload.empty()) return false;
+    for (const char* k : {"order_details", "token_pair", "quantity", "side", "client_order_id"})
+        if (payload.find(k) != std::string::npos) return true;
+    return false;
+}
+
+std::string ParseResult::get_description() const {
+    std::stringstream ss;
+    if (success) {
+        ss << SBEUtils::get_message_type_name(template_id, schema_id);
+        if (is_session_event())
+            ss << " (code: " << SBEUtils::get_session_event_code_string(event_code) << ")";
+        else if (!message_type.empty())
+            ss << " (type: " << message_type << ")";
+        if (!message_id.empty()) ss << " [ID: " << message_id.substr(0, 8) << "...]";
+    } else {
+        ss << "Parse Error: " << error_message;
+    }
+    return ss.str();
+}
+
+bool gpu_codec_available() { return sbe_device_ready() == 1; }
+
+// ======================================================================================
+// encode
+// ======================================================================================
 EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) {
     // timestamp 0 → the clock the reference reads (src/sbe_encoder.cpp:134-138)
     return encode_tm(msgs, length, false, 0, 0, clock_ms());
+}
+
+std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
+                                                           const std::string& uuid, const std::string& payload,
+                                                           const std::string& headers, std::int64_t timestamp) {
+    TopicMessageFields f{topic, message_type, uuid, payload, headers, timestamp};
+    EncodedBatch b = encode_topic_batch({f}, EncodeLength::Reference);
+    const uint8_t st = b.status[0];
+    if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
+    if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
+    return b.bytes.to_vector();
 }
 
 EncodedBatch SessionFrameEncoder::encode_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) const {
@@ -357,13 +895,7 @@ std::vector<std::uint8_t> SessionFrameEncoder::create_combined_message(const std
     const uint8_t st = b.status[0];
     if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
     if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
-    return b.bytes;
-}
-
-static uint64_t now_nanos_sys() {  // include/aeron_cluster/protocol.hpp:31-34
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::system_clock::now().time_since_epoch())
-        .count();
+    return b.bytes.to_vector();
 }
 
 std::vector<std::string> TopicPublisher::publish_topic_batch(const std::vector<TopicMessageFields>& msgs) {
@@ -403,16 +935,16 @@ EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOf
             throw std::runtime_error("sbecodec: commit offset for unknown topic '" + offsets[i].topic +
                                      "' needs the jsoncpp TopicMessage fallback (not built)");
     }
+    EncodePlan plan;
+    plan.overhead = SBE_LITE_OVERHEAD(2);
     return run_encode(
         offsets.size(), 2,
         [&](size_t i, int k) { return std::string_view(k == 0 ? offsets[i].message_id : offsets[i].message_identifier); },
-        [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; },
-        SBE_LITE_OVERHEAD(2),
-        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid, uint8_t* out,
+        [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; }, plan,
+        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid, size_t m, uint8_t* out,
             uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
             sbe_lite_batch in{arena, nullptr, len, tid, seq};
-            if (sbe_encode_lite_batch(&in, offsets.size(), SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
-                                      wsb, s) != SBE_OK)
+            if (sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws, wsb, s) != SBE_OK)
                 fail("sbe_encode_lite_batch");
         });
 }
@@ -428,7 +960,7 @@ std::vector<std::uint8_t> CommitManager::build_commit_offset_message(const std::
     const uint8_t st = b.status[0];
     if (st == 1 || st == 2) throw std::runtime_error(kLiteE109[st - 1]);
     if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
-    return b.bytes;
+    return b.bytes.to_vector();
 }
 
 OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vector<std::string>& message_ids) {
@@ -454,68 +986,70 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
         }
     };
     Ctx& c = ctx();
-    size_t arena = 0;
-    for (size_t i = 0; i < n; ++i)
-        for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) arena += field(i, k).size();
-    const size_t nlen = n * 4 * SBE_ORDER_FIELDS, nnum = n * 24;
-    c.h_arena.need(arena + 16);
-    c.h_len.need(nlen + nnum);
-    uint8_t* ap = static_cast<uint8_t*>(c.h_arena.p);
-    uint32_t* lp = static_cast<uint32_t*>(c.h_len.p);
-    int64_t* cid = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(c.h_len.p) + ((nlen + 7) & ~(size_t)7));
+    Slot& s = c.slot[0];
+    std::vector<uint64_t> pin;
+    prefix(n, pin, [&](size_t i) {
+        uint64_t t = 0;
+        for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) t += field(i, k).size();
+        return t;
+    });
+    const size_t arena = (size_t)pin[n];
+    const size_t o_len = al16(arena), nlen = n * 4 * SBE_ORDER_FIELDS, o_num = o_len + al16(nlen), stage = o_num + n * 24;
+    s.wait_input_free();
+    s.pin_in.need(stage);
+    uint8_t* ap = s.pin_in.b();
+    uint32_t* lp = reinterpret_cast<uint32_t*>(ap + o_len);
+    int64_t* cid = reinterpret_cast<int64_t*>(ap + o_num);
     int64_t* ts = cid + n;
     double* q = reinterpret_cast<double*>(ts + n);
-    size_t at = 0;
-    for (size_t i = 0; i < n; ++i) {
-        for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) {
-            const std::string_view f = field(i, k);
-            std::memcpy(ap + at, f.data(), f.size());
-            at += f.size();
-            lp[SBE_ORDER_FIELDS * i + k] = (uint32_t)f.size();
+    for_ranges(n, 2048, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i) {
+            uint8_t* at = ap + pin[i];
+            for (int k = 0; k < (int)SBE_ORDER_FIELDS; ++k) {
+                const std::string_view f = field(i, k);
+                if (!f.empty()) std::memcpy(at, f.data(), f.size());
+                at += f.size();
+                lp[SBE_ORDER_FIELDS * i + k] = (uint32_t)f.size();
+            }
+            cid[i] = orders[i].customer_id;
+            ts[i] = orders[i].timestamp;
+            q[i] = orders[i].quantity;
         }
-        cid[i] = orders[i].customer_id;
-        ts[i] = orders[i].timestamp;
-        q[i] = orders[i].quantity;
-    }
-    const size_t small = ((nlen + 7) & ~(size_t)7) + nnum;
+    });
     // a record is at most ~800 B besides its strings (428 fixed, 316 for "%f" of a quantity near
     // DBL_MAX, 24 for "%.17g", 34 for two integers); strings escape to <= 6x and appear <= twice.
     // out_off always holds the full sizes, so a record past the capacity is redone below.
     uint64_t cap = 12 * (uint64_t)arena + 900 * (uint64_t)n + 16;
-    c.d_arena.need(arena + 16);
-    c.d_len.need(small);
-    c.d_off.need(2 * (n + 1) * 8);
-    c.d_st.need(2 * n);
-    c.d_ws.need(sbe_order_json_workspace_size(n));
-    hip_check(hipMemcpyAsync(c.d_arena.p, ap, arena, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_len.p, c.h_len.p, small, hipMemcpyHostToDevice, c.stream), "H2D");
-    const uint8_t* dl = static_cast<const uint8_t*>(c.d_len.p);
-    const int64_t* d_cid = reinterpret_cast<const int64_t*>(dl + ((nlen + 7) & ~(size_t)7));
-    sbe_order_batch in{static_cast<const uint8_t*>(c.d_arena.p), nullptr, reinterpret_cast<const uint32_t*>(dl),
-                       d_cid, d_cid + n, reinterpret_cast<const double*>(d_cid + 2 * n)};
+    s.d_in.need(stage);
+    const size_t o_off = 0, o_st = al16(2 * (n + 1) * 8), o_ws = o_st + al16(2 * n);
+    const size_t wsb = sbe_order_json_workspace_size(n);
+    c.d_aux.need(o_ws + wsb);
+    hip_check(hipMemcpyAsync(s.d_in.p, ap, stage, hipMemcpyHostToDevice, s.stream), "H2D");
+    const uint8_t* di = s.d_in.b();
+    const int64_t* d_cid = reinterpret_cast<const int64_t*>(di + o_num);
+    sbe_order_batch in{di, nullptr, reinterpret_cast<const uint32_t*>(di + o_len), d_cid, d_cid + n,
+                       reinterpret_cast<const double*>(d_cid + 2 * n)};
     for (int w = 0; w < 2; ++w) {
         EncodedBatch& b = w ? r.headers : r.payload;
-        uint64_t* off = static_cast<uint64_t*>(c.d_off.p) + w * (n + 1);
-        uint8_t* st = static_cast<uint8_t*>(c.d_st.p) + w * n;
+        uint64_t* off = reinterpret_cast<uint64_t*>(c.d_aux.b() + o_off) + w * (n + 1);
+        uint8_t* st = c.d_aux.b() + o_st + w * n;
         for (int attempt = 0;; ++attempt) {
-            c.d_out.need(2 * cap);
-            uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
-            if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, out, cap, off,
-                                        st, c.d_ws.p, c.d_ws.cap, c.stream) != SBE_OK)
+            s.d_out.need(cap);
+            if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, s.d_out.b(), cap,
+                                        off, st, c.d_aux.b() + o_ws, wsb, s.stream) != SBE_OK)
                 fail("sbe_order_to_json_batch");
-            hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
-            hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, c.stream), "D2H");
-            hip_check(hipStreamSynchronize(c.stream), "sync");
+            hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+            hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, s.stream), "D2H");
+            hip_check(hipStreamSynchronize(s.stream), "sync");
             if (b.offsets[n] <= cap || attempt > 0) break;
             cap = b.offsets[n];  // the measured size: one rerun
         }
         for (size_t i = 0; i < n; ++i)
             if (b.status[i] != SBE_JSON_OK) throw std::runtime_error("sbecodec: order JSON record did not fit");
-        uint8_t* out = static_cast<uint8_t*>(c.d_out.p) + w * cap;
-        b.bytes.resize(b.offsets[n]);
+        b.bytes = HostBytesAccess::make((size_t)b.offsets[n]);
         if (b.offsets[n]) {
-            hip_check(hipMemcpyAsync(b.bytes.data(), out, b.offsets[n], hipMemcpyDeviceToHost, c.stream), "D2H");
-            hip_check(hipStreamSynchronize(c.stream), "sync");
+            hip_check(hipMemcpyAsync(b.bytes.data(), s.d_out.p, b.offsets[n], hipMemcpyDeviceToHost, s.stream), "D2H");
+            hip_check(hipStreamSynchronize(s.stream), "sync");
         }
     }
     return r;
@@ -526,17 +1060,9 @@ std::string Order::to_json() const {
     return std::string(b.payload.bytes.begin(), b.payload.bytes.end());
 }
 
-std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
-                                                           const std::string& uuid, const std::string& payload,
-                                                           const std::string& headers, std::int64_t timestamp) {
-    TopicMessageFields f{topic, message_type, uuid, payload, headers, timestamp};
-    EncodedBatch b = encode_topic_batch({f}, EncodeLength::Reference);
-    const uint8_t st = b.status[0];
-    if (st >= SBE_ENC_E109_TOPIC && st <= SBE_ENC_E109_HEADERS) throw std::runtime_error(kE109[st - 1]);
-    if (st != SBE_ENC_OK) throw std::runtime_error("sbecodec: encode failed");
-    return b.bytes;
-}
-
+// ======================================================================================
+// decode
+// ======================================================================================
 ParseResult MessageParser::parse_message(const std::uint8_t* data, std::size_t length) {
     if (!data || length == 0) {  // src/sbe_encoder.cpp:516-519 (no device round trip needed)
         ParseResult r;
@@ -544,27 +1070,147 @@ ParseResult MessageParser::parse_message(const std::uint8_t* data, std::size_t l
         return r;
     }
     const uint64_t off[2] = {0, length};
-    Desc d = run_decode(data, off, 1, SBE_DEC_PARSE_MESSAGE);
-    return materialize(data, d, 0);
+    auto d = run_decode(data, off, 1, SBE_DEC_PARSE_MESSAGE);
+    return materialize(data, *d, 0);
+}
+
+ParseResult MessageParser::decode_topic_message_with_sbe(const std::uint8_t* data, std::size_t length) {
+    ParseResult r;
+    if (!data || length < SBEConstants::SBE_HEADER_LENGTH) {  // MessageHeader::wrap (MessageHeader.h:165-168)
+        r.error_message = "SBE TopicMessage decoding failed: buffer too short for flyweight [E107]";
+        return r;
+    }
+    const uint16_t tmpl = rdu16(data + 2), schema = rdu16(data + 4);
+    if (tmpl != SBEConstants::TOPIC_MESSAGE_TEMPLATE_ID || schema != SBEConstants::TOPIC_SCHEMA_ID) {  // :976-983
+        r.error_message = "Not a TopicMessage (got template_id=" + std::to_string(tmpl) +
+                          ", schema_id=" + std::to_string(schema) + ")";
+        return r;
+    }
+    // template 1 / schema 1: parse_message dispatches straight to this function (:539-541, :812-816)
+    return parse_message(data, length);
+}
+
+ParseResult MessageParser::decode_acknowledgment_with_sbe(const std::uint8_t* data, std::size_t length) {
+    ParseResult r;
+    if (!data || length < SBEConstants::SBE_HEADER_LENGTH) {  // :842-845
+        r.error_message = "Buffer too short for SBE header";
+        return r;
+    }
+    const uint16_t tmpl = rdu16(data + 2), schema = rdu16(data + 4);
+    if (tmpl != SBEConstants::ACKNOWLEDGMENT_TEMPLATE_ID || schema != SBEConstants::TOPIC_SCHEMA_ID) {  // :859-865
+        r.error_message = "Message is not an Acknowledgment. Expected: template_id=2, schema_id=1. Got: template_id=" +
+                          std::to_string(tmpl) + ", schema_id=" + std::to_string(schema);
+        return r;
+    }
+    // template 2 / schema 1: is_topic_message()'s third clause sends parse_message here (:539-541, :817-819)
+    return parse_message(data, length);
+}
+
+ParseResult MessageParser::parse_message_debug(const std::uint8_t* data, std::size_t length, const std::string& debug_prefix) {
+    debug_log(debug_prefix, "📋 Parsing message (", length, " bytes)");
+    if (length > 0 && length <= 200) {
+        debug_log(debug_prefix, "📋 Hex dump:");
+        SBEUtils::print_hex_dump(data, length, debug_prefix + "  ", 64);
+    }
+    ParseResult result = parse_message(data, length);
+    debug_log(debug_prefix, "📋 Parse result: ", (result.success ? "SUCCESS" : "FAILED"));
+    debug_log(debug_prefix, "📋 Description: ", result.get_description());
+    if (!result.success) {
+        debug_log(debug_prefix, "📋 Error: ", result.error_message);
+        const auto strings = SBEUtils::extract_readable_strings(data, length, 3);
+        if (!strings.empty()) {
+            debug_log(debug_prefix, "📋 Readable strings found:");
+            for (const auto& str : strings) debug_log(debug_prefix, "  \"", str, "\"");
+        }
+    }
+    return result;
+}
+
+std::string MessageParser::get_message_type(const std::uint8_t* data, std::size_t length) {
+    if (!data || length < SBEConstants::SBE_HEADER_LENGTH) return "INVALID";
+    return SBEUtils::get_message_type_name(rdu16(data + 2), rdu16(data + 4));
+}
+
+std::int64_t MessageParser::extract_correlation_id(const std::uint8_t* data, std::size_t length) {
+    if (!data || length < SBEConstants::SBE_HEADER_LENGTH + 8) return 0;
+    if (rdu16(data + 4) != SBEConstants::CLUSTER_SCHEMA_ID) return 0;
+    return rdi64(data + 8);
+}
+
+bool MessageParser::is_acknowledgment_for(const std::uint8_t* data, std::size_t length, const std::string& message_id) {
+    const ParseResult r = parse_message(data, length);
+    if (!r.success || !r.is_acknowledgment()) return false;
+    return r.message_id == message_id || r.payload.find(message_id) != std::string::npos ||
+           r.headers.find(message_id) != std::string::npos;
 }
 
 std::vector<ParseResult> MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
-    Desc d = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
-    std::vector<ParseResult> out;
-    out.reserve(n);
-    for (size_t i = 0; i < n; ++i) out.push_back(materialize(data + rec_off[i], d, i));
+    std::vector<ParseResult> out(n);
+    if (n == 0) return out;
+    auto d = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
+    for_ranges(n, 2048, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i) out[i] = materialize(data + rec_off[i], *d, i);
+    });
     return out;
 }
 
+ParsedBatch MessageParser::decode_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
+    ParsedBatch b;
+    b.desc_ = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
+    b.data_ = data;
+    b.rec_off_ = rec_off;
+    b.n_ = n;
+    return b;
+}
+
+ParseResult ParsedBatch::result(std::size_t i) const { return materialize(data_ + rec_off_[i], *desc_, i); }
+bool ParsedBatch::success(std::size_t i) const { return desc_->status(i) < SBE_ST_ERR_NULL_EMPTY; }
+std::uint8_t ParsedBatch::status(std::size_t i) const { return desc_->status(i); }
+std::uint16_t ParsedBatch::template_id(std::size_t i) const {
+    const uint8_t st = desc_->status(i);
+    return (st < SBE_ST_ERR_NULL_EMPTY || st == SBE_ST_ERR_UNKNOWN_TYPE) ? desc_->hdr(i)[1] : 0;
+}
+std::uint16_t ParsedBatch::schema_id(std::size_t i) const {
+    const uint8_t st = desc_->status(i);
+    return (st < SBE_ST_ERR_NULL_EMPTY || st == SBE_ST_ERR_UNKNOWN_TYPE) ? desc_->hdr(i)[2] : 0;
+}
+std::int64_t ParsedBatch::timestamp(std::size_t i) const {
+    const uint8_t st = desc_->status(i);
+    return (st == SBE_ST_TM || st == SBE_ST_ACK) ? (int64_t)desc_->ts(i) : 0;
+}
+std::uint64_t ParsedBatch::sequence_number(std::size_t i) const { return desc_->seq(i); }
+std::string_view ParsedBatch::view(std::size_t i, int field) const {
+    if (field < 0 || field > 4 || desc_->status(i) >= SBE_ST_ERR_NULL_EMPTY) return {};
+    return {reinterpret_cast<const char*>(data_ + rec_off_[i]) + desc_->off(i)[field], desc_->len(i)[field]};
+}
+void ParsedBatch::for_each(const std::function<void(std::size_t, const ParseResult&)>& fn) const {
+    const size_t block = 4096;
+    std::vector<ParseResult> buf[1];
+    auto build = [&](size_t k, std::vector<ParseResult>& v) {
+        const size_t a = k * block, m = std::min(n_, a + block) - a;
+        v.resize(m);
+        for_ranges(m, 256, [&](size_t x, size_t y) {
+            for (size_t r = x; r < y; ++r) v[r] = result(a + r);
+        });
+    };
+    const size_t K = (n_ + block - 1) / block;
+    for (size_t k = 0; k < K; ++k) {  // a block's ParseResults on the workers, then fn in order
+        build(k, buf[0]);
+        for (size_t r = 0; r < buf[0].size(); ++r) fn(k * block + r, buf[0][r]);
+    }
+}
+
 namespace {
-std::optional<AckInfo> ack_from(const uint8_t* rec, const Desc& d, size_t i) {
-    const uint8_t st = d.status[i];
+std::optional<AckInfo> ack_from(const uint8_t* rec, const Descriptors& d, size_t i) {
+    const uint8_t st = d.status(i);
     if (st != SBE_ST_EG_ACK_SIMPLE && st != SBE_ST_EG_ACK) return std::nullopt;
     AckInfo a;
-    a.timestamp_nanos = d.ts[i];
+    a.timestamp_nanos = d.ts(i);
     a.simple_control_ack = st == SBE_ST_EG_ACK_SIMPLE;
     if (st == SBE_ST_EG_ACK) {
-        auto v = [&](int k) { return std::string(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]); };
+        const uint32_t* off = d.off(i);
+        const uint32_t* len = d.len(i);
+        auto v = [&](int k) { return std::string(reinterpret_cast<const char*>(rec) + off[k], len[k]); };
         a.message_id = v(0);
         a.topic = v(1);
         a.correlation_id = v(2);
@@ -576,27 +1222,28 @@ std::optional<AckInfo> ack_from(const uint8_t* rec, const Desc& d, size_t i) {
 std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len) {
     if (!data || len < 8) return std::nullopt;  // src/ack_decoder.cpp:30
     const uint64_t off[2] = {0, len};
-    Desc d = run_decode(data, off, 1, SBE_DEC_ON_EGRESS);
-    return ack_from(data, d, 0);
+    auto d = run_decode(data, off, 1, SBE_DEC_ON_EGRESS);
+    return ack_from(data, *d, 0);
 }
 
 std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len) {
     if (!data || len < 8) return std::nullopt;
     const uint64_t off[2] = {0, len};
-    Desc d = run_decode(data, off, 1, SBE_DEC_LITE);
-    if (d.status[0] != SBE_ST_LITE) return std::nullopt;
+    auto d = run_decode(data, off, 1, SBE_DEC_LITE);
+    if (d->status(0) != SBE_ST_LITE) return std::nullopt;
     LiteRecord r;
-    r.template_id = d.hdr[1];
-    r.topic_id = d.off[4];
-    r.sequence = d.ts[0];
+    r.template_id = d->hdr(0)[1];
+    r.topic_id = d->off(0)[4];
+    r.sequence = d->ts(0);
     const int nf = (int)sbe_lite_fields(r.template_id);
-    for (int k = 0; k < nf; ++k) r.fields.emplace_back(reinterpret_cast<const char*>(data) + d.off[k], d.len[k]);
+    for (int k = 0; k < nf; ++k) r.fields.emplace_back(reinterpret_cast<const char*>(data) + d->off(0)[k], d->len(0)[k]);
     return r;
 }
 
 EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const std::uint64_t* frag_off,
                                                const std::uint8_t* flags, std::size_t n) {
     Ctx& c = ctx();
+    Slot& s = c.slot[0];
     EncodedBatch b;
     // the accumulator so far goes first as a middle fragment (flags 0): it is appended to exactly
     // as the reference's acc_ would be, or cleared by a BEGIN
@@ -606,13 +1253,14 @@ EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const s
         return b;
     }
     const uint64_t base = n ? frag_off[0] : 0, body = n ? frag_off[n] - base : 0, total = acc_.size() + body;
-    c.h_in.need(total + 16);
-    uint8_t* hi = static_cast<uint8_t*>(c.h_in.p);
-    std::memcpy(hi, acc_.data(), acc_.size());
-    if (body) std::memcpy(hi + acc_.size(), data + base, body);
-    c.h_roff.need((nf + 1) * 8 + nf);
-    uint64_t* ho = static_cast<uint64_t*>(c.h_roff.p);
-    uint8_t* hf = reinterpret_cast<uint8_t*>(ho + nf + 1);
+    const size_t o_fl = (nf + 1) * 8, o_data = al16(o_fl + nf), stage = o_data + total;
+    s.wait_input_free();
+    s.pin_in.need(stage + 16);
+    uint8_t* hp = s.pin_in.b();
+    uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
+    uint8_t* hf = hp + o_fl;
+    std::memcpy(hp + o_data, acc_.data(), acc_.size());
+    if (body) std::memcpy(hp + o_data + acc_.size(), data + base, body);
     ho[0] = 0;
     if (pre) {
         ho[1] = acc_.size();
@@ -622,38 +1270,32 @@ EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const s
         ho[pre + i + 1] = acc_.size() + (frag_off[i + 1] - base);
         hf[pre + i] = flags[i];
     }
-    c.d_in.need(total + 16);
-    c.d_roff.need((nf + 1) * 8 + nf);
-    c.d_out.need(total + 16);
-    c.d_off.need((nf + 1) * 8 + 16);
+    s.d_in.need(stage + 16);
+    const size_t d_off = al16(total), d_cnt = d_off + (nf + 1) * 8, d_ws = al16(d_cnt + 16);
     const size_t wsb = sbe_reassemble_workspace_size(nf);
-    c.d_ws.need(wsb);
-    hip_check(hipMemcpyAsync(c.d_in.p, hi, total, hipMemcpyHostToDevice, c.stream), "H2D");
-    hip_check(hipMemcpyAsync(c.d_roff.p, ho, (nf + 1) * 8 + nf, hipMemcpyHostToDevice, c.stream), "H2D");
-    uint64_t* d_off = static_cast<uint64_t*>(c.d_off.p);
-    uint64_t* d_counts = d_off + nf + 1;
-    if (sbe_reassemble_fragments(static_cast<uint8_t*>(c.d_in.p), static_cast<uint64_t*>(c.d_roff.p),
-                                 reinterpret_cast<uint8_t*>(static_cast<uint64_t*>(c.d_roff.p) + nf + 1), nf,
-                                 static_cast<uint8_t*>(c.d_out.p), d_off, d_counts, c.d_ws.p, c.d_ws.cap,
-                                 c.stream) != SBE_OK)
+    s.d_out.need(d_ws + wsb);
+    hip_check(hipMemcpyAsync(s.d_in.p, hp, stage, hipMemcpyHostToDevice, s.stream), "H2D");
+    uint8_t* dout = s.d_out.b();
+    uint64_t* dmo = reinterpret_cast<uint64_t*>(dout + d_off);
+    uint64_t* dcnt = reinterpret_cast<uint64_t*>(dout + d_cnt);
+    if (sbe_reassemble_fragments(s.d_in.b() + o_data, reinterpret_cast<const uint64_t*>(s.d_in.p), s.d_in.b() + o_fl, nf,
+                                 dout, dmo, dcnt, dout + d_ws, wsb, s.stream) != SBE_OK)
         fail("sbe_reassemble_fragments");
-    uint64_t counts[2];
-    hip_check(hipMemcpyAsync(counts, d_counts, 16, hipMemcpyDeviceToHost, c.stream), "D2H");
-    hip_check(hipStreamSynchronize(c.stream), "sync");
-    const uint64_t m = counts[0];
+    c.h_aux.need(16);
+    uint64_t* counts = reinterpret_cast<uint64_t*>(c.h_aux.p);
+    hip_check(hipMemcpyAsync(counts, dcnt, 16, hipMemcpyDeviceToHost, s.stream), "D2H");
+    hip_check(hipStreamSynchronize(s.stream), "sync");
+    const uint64_t m = counts[0], carry = counts[1];
     b.offsets.resize(m + 1);
     b.status.assign(m, 0);
-    hip_check(hipMemcpyAsync(b.offsets.data(), d_off, (m + 1) * 8, hipMemcpyDeviceToHost, c.stream), "D2H");
-    hip_check(hipStreamSynchronize(c.stream), "sync");
-    const uint64_t out_bytes = b.offsets[m] + counts[1];
-    std::vector<uint8_t> all(out_bytes);
-    if (out_bytes) {
-        hip_check(hipMemcpyAsync(all.data(), c.d_out.p, out_bytes, hipMemcpyDeviceToHost, c.stream), "D2H");
-        hip_check(hipStreamSynchronize(c.stream), "sync");
-    }
-    acc_.assign(all.begin() + b.offsets[m], all.end());
-    all.resize(b.offsets[m]);
-    b.bytes = std::move(all);
+    hip_check(hipMemcpyAsync(b.offsets.data(), dmo, (m + 1) * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
+    hip_check(hipStreamSynchronize(s.stream), "sync");
+    const uint64_t msg_bytes = b.offsets[m];
+    b.bytes = HostBytesAccess::make((size_t)msg_bytes);
+    acc_.resize(carry);
+    if (msg_bytes) hip_check(hipMemcpyAsync(b.bytes.data(), dout, msg_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+    if (carry) hip_check(hipMemcpyAsync(acc_.data(), dout + msg_bytes, carry, hipMemcpyDeviceToHost, s.stream), "D2H");
+    hip_check(hipStreamSynchronize(s.stream), "sync");
     return b;
 }
 
@@ -676,19 +1318,19 @@ void MessageHandler::on_egress(const std::uint8_t* data, std::size_t len) {
 }
 
 void MessageHandler::on_egress_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
-    Desc d = run_decode(data, rec_off, n, SBE_DEC_ON_EGRESS);
+    auto d = run_decode(data, rec_off, n, SBE_DEC_ON_EGRESS);
     for (size_t i = 0; i < n; ++i) {
         const uint8_t* rec = data + rec_off[i];
-        switch (d.status[i]) {
+        switch (d->status(i)) {
             case SBE_ST_EG_ACK_SIMPLE:
             case SBE_ST_EG_ACK:
-                if (ack_cb_) ack_cb_(*ack_from(rec, d, i));
+                if (ack_cb_) ack_cb_(*ack_from(rec, *d, i));
                 break;
             case SBE_ST_EG_TM:
                 if (tm_cb_) {
-                    auto v = [&](int k) {
-                        return std::string_view(reinterpret_cast<const char*>(rec) + d.off[5 * i + k], d.len[5 * i + k]);
-                    };
+                    const uint32_t* off = d->off(i);
+                    const uint32_t* len = d->len(i);
+                    auto v = [&](int k) { return std::string_view(reinterpret_cast<const char*>(rec) + off[k], len[k]); };
                     tm_cb_(v(0), v(1), v(2), v(3), v(4));
                 }
                 break;

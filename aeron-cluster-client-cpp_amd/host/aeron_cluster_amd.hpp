@@ -20,7 +20,10 @@
 // plus batched overloads, which are the point of the GPU path: one launch per batch.
 //
 // Everything computes on the GPU.  There is no CPU codec here: without a gfx950 device every
-// entry point throws std::runtime_error("sbecodec: ...").
+// entry point throws std::runtime_error("sbecodec: ...").  Host work is staging and result
+// building only: batches move through a two-stream pipeline (host threads stage chunk k+1 in
+// page-locked memory while chunk k is copied, coded and copied back), on min(16, cores) host
+// threads (AERON_AMD_HOST_THREADS).
 #pragma once
 
 #include <cstdint>
@@ -36,13 +39,44 @@ namespace aeron_cluster {
 // include/aeron_cluster/config.hpp:169-199
 namespace SBEConstants {
 constexpr std::uint16_t CLUSTER_SCHEMA_ID = 111;
+constexpr std::uint16_t CLUSTER_SCHEMA_VERSION = 8;
 constexpr std::uint16_t TOPIC_SCHEMA_ID = 1;
+constexpr std::uint16_t TOPIC_SCHEMA_VERSION = 1;
+constexpr std::uint16_t SESSION_CONNECT_TEMPLATE_ID = 3;
 constexpr std::uint16_t SESSION_EVENT_TEMPLATE_ID = 2;
+constexpr std::uint16_t SESSION_CLOSE_TEMPLATE_ID = 4;
+constexpr std::uint16_t SESSION_KEEPALIVE_TEMPLATE_ID = 5;
 constexpr std::uint16_t TOPIC_MESSAGE_TEMPLATE_ID = 1;
 constexpr std::uint16_t ACKNOWLEDGMENT_TEMPLATE_ID = 2;
+constexpr std::uint16_t SESSION_CONNECT_BLOCK_LENGTH = 16;
+constexpr std::uint16_t SESSION_EVENT_BLOCK_LENGTH = 32;
+constexpr std::uint16_t TOPIC_MESSAGE_BLOCK_LENGTH = 48;
+constexpr std::uint16_t ACKNOWLEDGMENT_BLOCK_LENGTH = 8;
+constexpr std::int32_t SESSION_EVENT_OK = 0;
+constexpr std::int32_t SESSION_EVENT_ERROR = 1;
+constexpr std::int32_t SESSION_EVENT_REDIRECT = 2;
+constexpr std::int32_t SESSION_EVENT_AUTHENTICATION_REJECTED = 3;
+constexpr std::int32_t SESSION_EVENT_CLOSED = 4;
+constexpr std::size_t SBE_HEADER_LENGTH = 8;
 }  // namespace SBEConstants
 
-// include/aeron_cluster/sbe_messages.hpp:306-328 (fields), :332-377 (predicates)
+// The reference's debug helpers (include/aeron_cluster/sbe_messages.hpp:252-301, bodies
+// src/sbe_encoder.cpp:328-485).  Host-side formatting only: ParseResult::get_description and the
+// reference's tools (tools/message_inspector.cpp) call them; none of them is on the codec path.
+namespace SBEUtils {
+void print_hex_dump(const std::uint8_t* data, std::size_t length, const std::string& prefix = "",
+                    std::size_t max_bytes = 0);
+std::string get_session_event_code_string(std::int32_t code);           // :370-385
+std::string get_message_type_name(std::uint16_t template_id, std::uint16_t schema_id);  // :387-409
+bool is_valid_correlation_id(std::int64_t correlation_id);             // :411-413
+std::int64_t generate_correlation_id();                                 // :415-419
+std::string format_timestamp(std::int64_t timestamp);                   // :421-433
+bool is_valid_sbe_message(const std::uint8_t* data, std::size_t length);  // :435-457
+std::vector<std::string> extract_readable_strings(const std::uint8_t* data, std::size_t length,
+                                                  std::size_t min_length = 3);  // :459-485
+}  // namespace SBEUtils
+
+// include/aeron_cluster/sbe_messages.hpp:306-328 (fields), :332-411 (predicates, description)
 struct ParseResult {
     bool success = false;
     std::string error_message;
@@ -74,6 +108,11 @@ struct ParseResult {
     bool is_acknowledgment() const {
         return template_id == SBEConstants::ACKNOWLEDGMENT_TEMPLATE_ID && schema_id == SBEConstants::TOPIC_SCHEMA_ID;
     }
+    // sbe_messages.hpp:382-406: a topic message whose type or payload names order content
+    bool is_order_message() const;
+    // src/sbe_encoder.cpp:490-510: "<type name>[ (code: …)| (type: …)][ [ID: <8 chars>...]]" or
+    // "Parse Error: <error_message>"
+    std::string get_description() const;
 };
 
 // include/aeron_cluster/ack_decoder.hpp:9-15
@@ -91,9 +130,35 @@ struct TopicMessageFields {
     std::int64_t timestamp = 0;  // 0 → the encoder's clock, as the reference does
 };
 
+namespace detail {
+struct HostBytesAccess;
+struct Descriptors;
+}  // namespace detail
+
+// Bytes in page-locked host memory taken from a recycled pool: the device's DMA engines copy the
+// encoded stream straight into it (no staging copy, no zero fill), and the caller reads it in place.
+// Copies share the block; the block returns to the pool with the last copy.
+class HostBytes {
+public:
+    const std::uint8_t* data() const { return p_; }
+    std::uint8_t* data() { return p_; }
+    std::size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    const std::uint8_t* begin() const { return p_; }
+    const std::uint8_t* end() const { return p_ + n_; }
+    std::uint8_t operator[](std::size_t i) const { return p_[i]; }
+    std::vector<std::uint8_t> to_vector() const { return std::vector<std::uint8_t>(begin(), end()); }
+
+private:
+    friend struct detail::HostBytesAccess;
+    std::shared_ptr<void> block_;
+    std::uint8_t* p_ = nullptr;
+    std::size_t n_ = 0;
+};
+
 // A packed batch of encoded records: record i = bytes[offsets[i], offsets[i+1]).
 struct EncodedBatch {
-    std::vector<std::uint8_t> bytes;
+    HostBytes bytes;
     std::vector<std::uint64_t> offsets;
     std::vector<std::uint8_t> status;  // SBE_ENC_* per record
     std::string_view record(std::size_t i) const {
@@ -120,11 +185,65 @@ public:
                                            EncodeLength length = EncodeLength::Wire);
 };
 
+class ParsedBatch;
+
 class MessageParser {
 public:
+    // src/sbe_encoder.cpp:513-551 (never throws; success = false + error_message)
     static ParseResult parse_message(const std::uint8_t* data, std::size_t length);
-    // Batch: records data[rec_off[i], rec_off[i+1]), one GPU launch.
+    // src/sbe_encoder.cpp:957-1143 called directly (sbe_messages.hpp:423): no dispatch — a header
+    // other than template 1 / schema 1 gives "Not a TopicMessage (got template_id=T, schema_id=S)",
+    // fewer than 8 bytes the flyweight's E107 ("SBE TopicMessage decoding failed: buffer too short
+    // for flyweight [E107]"); otherwise the GPU decode of the record.
+    static ParseResult decode_topic_message_with_sbe(const std::uint8_t* data, std::size_t length);
+    // src/sbe_encoder.cpp:833-954 called directly (sbe_messages.hpp:424): the printable-run
+    // heuristic on any record whose header says template 2 / schema 1.
+    static ParseResult decode_acknowledgment_with_sbe(const std::uint8_t* data, std::size_t length);
+    // src/sbe_encoder.cpp:554-575: parse_message plus the reference's diagnostics (hex dump of
+    // records of 1..200 bytes on stdout; DEBUG_LOG lines when AERON_CLUSTER_DEBUG=1).
+    static ParseResult parse_message_debug(const std::uint8_t* data, std::size_t length,
+                                           const std::string& debug_prefix = "");
+    // src/sbe_encoder.cpp:577-586: "INVALID" below 8 bytes, else the header's type name
+    static std::string get_message_type(const std::uint8_t* data, std::size_t length);
+    // src/sbe_encoder.cpp:588-603: the i64 after the header of a schema-111 message, else 0
+    static std::int64_t extract_correlation_id(const std::uint8_t* data, std::size_t length);
+    // src/sbe_encoder.cpp:605-616
+    static bool is_acknowledgment_for(const std::uint8_t* data, std::size_t length, const std::string& message_id);
+
+    // Batch: records data[rec_off[i], rec_off[i+1]), ParseResults built on the host threads.
     static std::vector<ParseResult> parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
+    // Batch without materialising: the device descriptors and views into `data` (valid while the
+    // caller's bytes are), ParseResults built on demand.  See ParsedBatch.
+    static ParsedBatch decode_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
+};
+
+// parse_message's outcome for a batch, kept as the device descriptors (host copy) plus views into
+// the caller's records.  result(i) == MessageParser::parse_message(record i); the string_view
+// accessors give the same bytes without building the ParseResult.
+class ParsedBatch {
+public:
+    std::size_t size() const { return n_; }
+    ParseResult result(std::size_t i) const;
+    ParseResult operator[](std::size_t i) const { return result(i); }
+    bool success(std::size_t i) const;
+    std::uint8_t status(std::size_t i) const;  // SBE_ST_* of include/sbecodec.h
+    std::uint16_t template_id(std::size_t i) const;
+    std::uint16_t schema_id(std::size_t i) const;
+    std::int64_t timestamp(std::size_t i) const;
+    std::uint64_t sequence_number(std::size_t i) const;
+    // TopicMessage: message_type / message_id (uuid) / payload / headers views; other statuses:
+    // the views ParseResult would copy (Ack defaults and error texts are not views: use result(i)).
+    std::string_view view(std::size_t i, int field) const;
+    // Calls fn(i, result(i)) in record order on the calling thread; the ParseResults of each
+    // 4096-record block are built on the host threads first.
+    void for_each(const std::function<void(std::size_t, const ParseResult&)>& fn) const;
+
+private:
+    friend class MessageParser;
+    std::shared_ptr<const detail::Descriptors> desc_;  // host copy of the device descriptors
+    const std::uint8_t* data_ = nullptr;               // the caller's records (borrowed)
+    const std::uint64_t* rec_off_ = nullptr;           // the caller's offsets (borrowed)
+    std::size_t n_ = 0;
 };
 
 std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len);

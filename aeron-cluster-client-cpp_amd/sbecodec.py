@@ -30,7 +30,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 5
+ABI_VERSION = 6
 ENC_REF_TRUNCATE8 = 0x1
 ENC_PUBLISH_TOPIC = 0x2
 ENC_OK, ENC_OVERFLOW = 0, 6
@@ -147,8 +147,12 @@ def _load():
     lib.sbe_comm_destroy.argtypes = [ctypes.c_void_p]
     lib.sbe_gather_encoded.restype = ctypes.c_int
     lib.sbe_gather_encoded.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    lib.sbe_gather_plan.restype = ctypes.c_int
+    lib.sbe_gather_plan.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.POINTER(ctypes.c_uint64)]
     if lib.sbe_abi_version() != ABI_VERSION:
         _abi_mismatch()
     return lib
@@ -462,7 +466,10 @@ def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=J
                         str_off=None, out=None, out_capacity=None, out_off=None, status=None, workspace=None,
                         stream=None) -> OrderJson:
     """Order::to_json (what=JSON_ORDER_PAYLOAD) or publish_order's headers JSON
-    (what=JSON_PUBLISH_HEADERS) of n Orders, str_len [n][8] (ORDER_FIELDS order)."""
+    (what=JSON_PUBLISH_HEADERS) of n Orders, str_len [n][8] (ORDER_FIELDS order).
+    Asynchronous on `stream` when the caller passes `out` or `out_capacity`; when this call sizes
+    the output itself it synchronises `stream` once to read the total (out_off[n]) and reruns the
+    launches at that size if the default bound was short."""
     arena = _dev(arena, torch.uint8, "arena")
     str_len = _dev(str_len, torch.int32, "str_len")
     customer_id = _dev(customer_id, torch.int64, "customer_id")
@@ -500,6 +507,8 @@ def order_to_json_batch(arena, str_len, customer_id, timestamp, quantity, what=J
 
     run(out, cap)
     if grow and n:  # out_off always holds the full sizes: one rerun at the measured size
+        s = stream if stream is not None else torch.cuda.current_stream()
+        s.synchronize()  # the launches ran on `stream`, which need not be torch's current stream
         total = int(out_off[n].item())
         if total > cap:
             out = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -540,12 +549,28 @@ class Comm:
             pass
 
 
+def gather_plan(ranks, root: int = 0):
+    """sbe_gather_plan on the host: ranks = [(bytes, records, dst_capacity, dst_off_capacity)] per
+    rank (capacities read from the root's entry).  Returns (rc, byte_base, rec_base, totals) with
+    the bases as lists of world + 1 prefix sums; rc is 0 or ENOSPC (-3)."""
+    world = len(ranks)
+    flat = (ctypes.c_uint64 * (4 * max(world, 1)))(*[int(v) & (2**64 - 1) for r in ranks for v in r])
+    bb = (ctypes.c_uint64 * (world + 1))()
+    rb = (ctypes.c_uint64 * (world + 1))()
+    tot = (ctypes.c_uint64 * 2)()
+    rc = lib().sbe_gather_plan(flat, world, int(root), bb, rb, tot)
+    return rc, list(bb), list(rb), (int(tot[0]), int(tot[1]))
+
+
 def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, dst_off=None, stream=None):
     """Collective: every rank's encoded shard (out, out_off [n+1]) back to back on `root`, offsets
-    rebased.  The root passes dst (uint8, large enough for every shard) and dst_off (int64 [N+1]);
-    returns (dst[:bytes], dst_off, bytes, N) on the root and (None, None, bytes, N) elsewhere."""
+    rebased.  The root passes dst (uint8, large enough for every shard) and dst_off (int64, N + 1
+    entries); returns (dst[:bytes], dst_off, bytes, N) on the root and (None, None, bytes, N)
+    elsewhere.  A short dst / dst_off raises ENOSPC on every rank before any transfer."""
     out = _dev(out, torch.uint8, "out")
     out_off = _dev(out_off, torch.int64, "out_off")
+    if out_off.numel() < int(n) + 1:
+        raise SbeError(f"out_off holds {out_off.numel()} entries, the shard needs n + 1 = {int(n) + 1}")
     am_root = comm.rank == root
     if am_root:
         dst = _dev(dst, torch.uint8, "dst")
@@ -555,7 +580,8 @@ def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, ds
     totals = (ctypes.c_uint64 * 2)()
     rc = lib().sbe_gather_encoded(comm._h, int(root), _ptr(out), _ptr(out_off), int(n),
                                   _ptr(dst) if am_root else None, int(dst.numel()) if am_root else 0,
-                                  _ptr(dst_off) if am_root else None, totals, _stream(stream))
+                                  _ptr(dst_off) if am_root else None, int(dst_off.numel()) if am_root else 0,
+                                  totals, _stream(stream))
     _check(rc, "sbe_gather_encoded")
     nbytes, nrec = int(totals[0]), int(totals[1])
     if am_root:

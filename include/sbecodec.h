@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 5
+#define SBECODEC_ABI_VERSION 6
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -359,15 +359,27 @@ int sbe_comm_destroy(sbe_comm* comm);
 /* Collective over the communicator.  Every rank passes its shard: out (its encoded stream, 16-B
  * aligned) with out_off [n+1] (device u64, out_off[0] == 0) as sbe_encode_*_batch wrote them.
  * The root receives the shards back to back in rank order into dst (dst_capacity bytes) and the
- * rebased offsets into dst_off ([N+1] device u64, N = Σ n_r: record j of rank r at
- * Σ_{q<r} bytes_q + out_off_r[j]); other ranks pass dst = dst_off = NULL.  totals (host u64[2], or
- * NULL) = {Σ bytes, N} on every rank.  On `stream`: an all-gather of the ranks' {bytes, n}, one
- * 32-B-per-rank device→host copy and a synchronisation of `stream` (the root sizes its receives
- * from it), then one group of ncclSend / ncclRecv at the prefix offsets (RCCL has no gatherv) and
- * the root's offset rebase; returns once those are enqueued.  SBE_ENOSPC (nothing sent) when the
- * root's dst_capacity is too small. */
+ * rebased offsets into dst_off (dst_off_capacity device u64 entries; N + 1 are written, N = Σ n_r:
+ * record j of rank r at Σ_{q<r} bytes_q + out_off_r[j]); other ranks pass dst = dst_off = NULL and
+ * capacities 0.  totals (host u64[2], or NULL) = {Σ bytes, N} on every rank.  On `stream`: an
+ * all-gather of the ranks' {bytes, n, root capacities}, one 32-B-per-rank device→host copy and a
+ * synchronisation of `stream` (the root sizes its receives from it), the plan of sbe_gather_plan,
+ * then one group of ncclSend / ncclRecv at the prefix offsets (RCCL has no gatherv) and the root's
+ * offset rebase; returns once those are enqueued.  SBE_ENOSPC on every rank (nothing sent) when the
+ * root's dst or dst_off is too small.  RCCL is loaded on the first sbe_comm_* call (the RCCL the
+ * process already holds, else librccl.so.1); nothing else in this library needs it. */
 int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint64_t* out_off, uint64_t n,
-                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t* totals, void* stream);
+                       uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t dst_off_capacity,
+                       uint64_t* totals, void* stream);
+
+/* The gather's plan (host only, no device): from every rank's {bytes, records, dst_capacity,
+ * dst_off_capacity} (ranks: host u64 [world][4], the capacities read from the root's entry) the
+ * byte and record base of each rank's shard on the root (byte_base / rec_base: host u64
+ * [world + 1], exclusive prefix sums; the last entry is the total) and totals {Σ bytes, Σ records}
+ * (or NULL).  SBE_ENOSPC when the root's dst holds fewer than Σ bytes or its dst_off fewer than
+ * Σ records + 1 entries; SBE_EINVAL on a bad world / root. */
+int sbe_gather_plan(const uint64_t* ranks, int world, int root, uint64_t* byte_base, uint64_t* rec_base,
+                    uint64_t* totals);
 
 /* ================================== profiling ================================== */
 /* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every

@@ -6,7 +6,10 @@
 // Build + run (GPU box): make -C scripts host_latency && scripts/host_latency
 #include <chrono>
 #include <cstdint>
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -20,7 +23,9 @@ static double us_since(clk::time_point t0) {
     return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
 }
 
-int main() {
+int main(int argc, char** argv) {
+    // optional: one batch size only (profiling runs), skipping the single-call section
+    const size_t only = argc > 1 ? (size_t)std::strtoull(argv[1], nullptr, 10) : 0;
     if (!gpu_codec_available()) {
         std::fprintf(stderr, "no gfx950 device\n");
         return 2;
@@ -30,10 +35,10 @@ int main() {
     // warm up the device context
     for (int i = 0; i < 20; ++i) (void)SBEEncoder::encode_topic_message(topic, type, uuid, payload, headers, 1);
     const std::vector<uint8_t> rec = SBEEncoder::encode_topic_batch(
-        {TopicMessageFields{topic, type, uuid, payload, headers, 1760000000000000000LL}}, EncodeLength::Wire).bytes;
+        {TopicMessageFields{topic, type, uuid, payload, headers, 1760000000000000000LL}}, EncodeLength::Wire).bytes.to_vector();
 
     // single-record calls: the reference's per-call surface
-    {
+    if (!only) {
         const int iters = 2000;
         auto t0 = clk::now();
         for (int i = 0; i < iters; ++i) (void)SBEEncoder::encode_topic_message(topic, type, uuid, payload, headers, 1);
@@ -47,17 +52,28 @@ int main() {
         std::printf("{\"op\": \"single_call\", \"encode_topic_message_us\": %.2f, \"parse_message_us\": %.2f, "
                     "\"decode_ack_us\": %.2f}\n", enc, par, ack);
     }
-    // batches: mirror (stage + H2D + kernels + D2H + host materialisation) vs the oracle on one thread
-    for (size_t n : {1, 4, 16, 64, 256, 1024, 4096, 16384, 65536, 262144}) {
+    // batches: mirror (stage + H2D + kernels + D2H, pipelined over two streams) vs the oracle on
+    // one thread.  decode = MessageParser::decode_batch (device descriptors + views, ParseResults on
+    // demand); parse = MessageParser::parse_batch (every ParseResult built, and destroyed by the
+    // next iteration, inside the timing)
+    for (size_t n : {1, 4, 16, 64, 256, 1024, 4096, 16384, 65536, 262144, 1048576}) {
+        if (only && n != only) continue;
         std::vector<TopicMessageFields> msgs(n, TopicMessageFields{topic, type, uuid, payload, headers, 1760000000000000000LL});
-        const int reps = n <= 1024 ? 200 : (n <= 16384 ? 20 : 4);
-        EncodedBatch b;
+        const int reps = n <= 1024 ? 200 : (n <= 16384 ? 40 : (n <= 262144 ? 10 : 4));
+        EncodedBatch b = SBEEncoder::encode_topic_batch(msgs, EncodeLength::Wire);
         auto t0 = clk::now();
         for (int r = 0; r < reps; ++r) b = SBEEncoder::encode_topic_batch(msgs, EncodeLength::Wire);
         const double enc = us_since(t0) / reps;
+        ParsedBatch pb = MessageParser::decode_batch(b.bytes.data(), b.offsets.data(), n);
         t0 = clk::now();
-        for (int r = 0; r < reps; ++r) (void)MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), n);
+        for (int r = 0; r < reps; ++r) pb = MessageParser::decode_batch(b.bytes.data(), b.offsets.data(), n);
         const double dec = us_since(t0) / reps;
+        std::vector<ParseResult> prs = MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), n);
+        t0 = clk::now();
+        for (int r = 0; r < reps; ++r) prs = MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), n);
+        const double par = us_since(t0) / reps;
+        bool ok = prs.size() == n && pb.size() == n && prs[n - 1].success && prs[n - 1].payload == payload &&
+                  pb.view(n - 1, 2) == uuid && b.offsets[n] == 256 * n;
         // oracle (CPU restatement, 1 thread) on the same records
         std::vector<uint8_t> arena;
         std::vector<uint32_t> lens;
@@ -71,20 +87,24 @@ int main() {
         std::vector<uint64_t> off(n + 1), dts(n);
         std::vector<uint16_t> dh(4 * n);
         std::vector<uint32_t> vo(5 * n), vl(5 * n);
+        const int creps = std::max(1, reps / 2);
         t0 = clk::now();
-        for (int r = 0; r < reps; ++r)
+        for (int r = 0; r < creps; ++r)
             orc_encode_batch(arena.data(), nullptr, lens.data(), ts.data(), n, 0, 0, out.data(), off.data(), st.data(), 1);
-        const double cenc = us_since(t0) / reps;
+        const double cenc = us_since(t0) / creps;
         t0 = clk::now();
-        for (int r = 0; r < reps; ++r)
+        for (int r = 0; r < creps; ++r)
             orc_decode_batch(out.data(), off.data(), n, SBE_DEC_PARSE_MESSAGE, dst.data(), dfl.data(), dh.data(),
                              dts.data(), vo.data(), vl.data(), 1);
-        const double cdec = us_since(t0) / reps;
-        std::printf("{\"op\": \"batch\", \"records\": %zu, \"mirror_encode_us\": %.1f, \"mirror_parse_us\": %.1f, "
-                    "\"oracle_encode_us\": %.1f, \"oracle_parse_us\": %.1f, \"mirror_rec_per_s\": %.4g, "
-                    "\"oracle_rec_per_s\": %.4g, \"gpu_ahead\": %s}\n",
-                    n, enc, dec, cenc, cdec, n / ((enc + dec) * 1e-6), n / ((cenc + cdec) * 1e-6),
-                    (enc + dec) < (cenc + cdec) ? "true" : "false");
+        const double cdec = us_since(t0) / creps;
+        ok = ok && std::memcmp(out.data(), b.bytes.data(), b.bytes.size()) == 0;
+        std::printf("{\"op\": \"batch\", \"records\": %zu, \"mirror_encode_us\": %.1f, \"mirror_decode_us\": %.1f, "
+                    "\"mirror_parse_us\": %.1f, \"oracle_encode_us\": %.1f, \"oracle_parse_us\": %.1f, "
+                    "\"mirror_enc_dec_rec_per_s\": %.4g, \"mirror_enc_parse_rec_per_s\": %.4g, \"oracle_rec_per_s\": %.4g, "
+                    "\"gpu_ahead\": %s, \"bytes_ok\": %s}\n",
+                    n, enc, dec, par, cenc, cdec, n / ((enc + dec) * 1e-6), n / ((enc + par) * 1e-6),
+                    n / ((cenc + cdec) * 1e-6), (enc + dec) < (cenc + cdec) ? "true" : "false", ok ? "true" : "false");
+        std::fflush(stdout);
     }
     return 0;
 }

@@ -3,6 +3,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstring>
+#include <iomanip>
 #include <iostream>
 #include <random>
 #include <sstream>
@@ -44,6 +45,245 @@ static std::vector<uint8_t> wire_tm(const std::vector<std::string>& f, uint64_t 
         b.insert(b.end(), s.begin(), s.end());
     }
     return b;
+}
+
+static bool same(const ParseResult& a, const ParseResult& b) {
+    return a.success == b.success && a.error_message == b.error_message && a.message_type == b.message_type &&
+           a.message_id == b.message_id && a.payload == b.payload && a.headers == b.headers && a.timestamp == b.timestamp &&
+           a.sequence_number == b.sequence_number && a.template_id == b.template_id && a.schema_id == b.schema_id &&
+           a.version == b.version && a.block_length == b.block_length && a.correlation_id == b.correlation_id &&
+           a.session_id == b.session_id && a.leader_member_id == b.leader_member_id && a.event_code == b.event_code &&
+           a.leadership_term_id == b.leadership_term_id;
+}
+
+static void put_le(std::vector<uint8_t>& b, uint64_t v, int bytes) {
+    for (int i = 0; i < bytes; ++i) b.push_back((uint8_t)(v >> (8 * i)));
+}
+
+// SessionEvent (template 2 / schema 111, sbe_messages.hpp:43-54) with a u32-prefixed detail
+static std::vector<uint8_t> session_event(int64_t corr, int64_t sess, int64_t term, int32_t leader, int32_t code,
+                                          const std::string& detail) {
+    std::vector<uint8_t> b = {32, 0, 2, 0, 111, 0, 8, 0};
+    put_le(b, (uint64_t)corr, 8);
+    put_le(b, (uint64_t)sess, 8);
+    put_le(b, (uint64_t)term, 8);
+    put_le(b, (uint32_t)leader, 4);
+    put_le(b, (uint32_t)code, 4);
+    if (!detail.empty()) {
+        put_le(b, detail.size(), 4);
+        b.insert(b.end(), detail.begin(), detail.end());
+    }
+    return b;
+}
+
+// a schema-111 session message {24,1,111,8} + 24 block bytes around an embedded record
+static std::vector<uint8_t> wrapped(const std::vector<uint8_t>& inner) {
+    std::vector<uint8_t> b = {24, 0, 1, 0, 111, 0, 8, 0};
+    put_le(b, 7, 8);
+    put_le(b, 9, 8);
+    put_le(b, 0, 8);
+    b.insert(b.end(), inner.begin(), inner.end());
+    return b;
+}
+
+// The fields the predicates and get_description read, from the oracle restatement's descriptor of
+// the record (independent of the mirror's materialisation).
+static ParseResult oracle_fields(const std::vector<uint8_t>& rec) {
+    uint8_t st = 0, fl = 0;
+    uint16_t h[4] = {0, 0, 0, 0};
+    uint64_t ts = 0;
+    uint32_t vo[5] = {0}, vl[5] = {0};
+    orc_decode_one(rec.data(), rec.size(), SBE_DEC_PARSE_MESSAGE, &st, &fl, h, &ts, vo, vl);
+    ParseResult r;
+    auto v = [&](int k) { return std::string(reinterpret_cast<const char*>(rec.data()) + vo[k], vl[k]); };
+    if (st == SBE_ST_TM || st == SBE_ST_ACK || st == SBE_ST_SESSION_EVENT || st == SBE_ST_ERR_UNKNOWN_TYPE) {
+        r.template_id = h[1];
+        r.schema_id = h[2];
+    }
+    r.success = st < SBE_ST_ERR_NULL_EMPTY;
+    if (st == SBE_ST_TM) {
+        r.message_type = v(1);
+        r.message_id = v(2);
+        r.payload = v(3);
+        r.headers = v(4);
+    } else if (st == SBE_ST_ACK) {
+        r.message_type = "Acknowledgment";
+        r.message_id = (fl & SBE_FL_ID_DEFAULT) ? "ack_" + std::to_string(ts) : v(0);
+        r.payload = (fl & SBE_FL_PAYLOAD_DEFAULT) ? std::string("SUCCESS") : v(1);
+        r.headers = v(2);
+    } else if (st == SBE_ST_SESSION_EVENT) {
+        r.message_type = "SessionEvent";
+        r.payload = v(3);
+        std::memcpy(&r.event_code, rec.data() + 36, 4);
+    }
+    return r;
+}
+
+// examples/basic_client_example.cpp:272-329, the message callback of BASELINE config #1: which
+// branch a ParseResult takes (1 order, 2 acknowledgment, 3 other topic message, 0 none)
+static int callback_branch(const ParseResult& r) {
+    if (r.is_order_message()) return 1;
+    if (r.is_acknowledgment()) return 2;
+    if (r.is_topic_message()) return 3;
+    return 0;
+}
+
+static void surface_tests(const std::vector<std::string>& f5, const std::vector<uint8_t>& wire,
+                          const std::vector<uint8_t>& sack, const std::vector<uint8_t>& ack45) {
+    auto tm = [&](const std::string& type, const std::string& uuid, const std::string& payload) {
+        return wire_tm({"orders", type, uuid, payload, "{\"h\":1}"}, 1760000000000000001ULL);
+    };
+    std::vector<uint8_t> ack_qty = {8, 0, 2, 0, 1, 0, 1, 0};
+    put_le(ack_qty, 1700000000000ULL, 8);
+    for (std::string s : {"id_77", "quantity", "x"}) {
+        ack_qty.push_back((uint8_t)s.size());
+        ack_qty.push_back(0);
+        ack_qty.insert(ack_qty.end(), s.begin(), s.end());
+    }
+    std::vector<uint8_t> ack12 = {8, 0, 2, 0, 1, 0, 1, 0, 1, 2, 3, 4};
+    std::vector<uint8_t> t9 = wire;
+    t9[2] = 9;
+    std::vector<uint8_t> emb_t5 = wire, emb_s7 = wire;
+    emb_t5[2] = 5;
+    emb_s7[4] = 7;
+    struct Case {
+        std::vector<uint8_t> rec;
+        int branch;
+        std::string description;
+    };
+    const std::vector<Case> cases = {
+        {wire, 1, "TopicMessage (type: CREATE_ORDER) [ID: msg_1...]"},
+        {tm("REPLAY_COMPLETE", "uuid-abcdefgh", "{\"x\":1}"), 3, "TopicMessage (type: REPLAY_COMPLETE) [ID: uuid-abc...]"},
+        {tm("TRADE", "t1", "{\"side\":\"BUY\"}"), 1, "TopicMessage (type: TRADE) [ID: t1...]"},
+        {tm("CANCEL_ORDER", "", "{}"), 1, "TopicMessage (type: CANCEL_ORDER)"},
+        {wire_tm(f5, 5, 8), 3, "TopicMessage"},
+        {sack, 2, "Acknowledgment (type: Acknowledgment) [ID: ack_1000...]"},
+        {ack45, 2, "Acknowledgment (type: Acknowledgment) [ID: msg_1...]"},
+        {ack_qty, 1, "Acknowledgment (type: Acknowledgment) [ID: id_77...]"},  // payload run "quantity"
+        {session_event(0x1122334455667788LL, 5, 6, 1, 0, ""), 0, "SessionEvent (code: OK)"},
+        {session_event(1, 5, 6, 2, 2, "10.0.0.2:9002"), 0, "SessionEvent (code: REDIRECT)"},
+        {session_event(1, 5, 6, 2, 9, "x"), 0, "SessionEvent (code: UNKNOWN(9))"},
+        {wrapped(wire), 1, "TopicMessage (type: CREATE_ORDER) [ID: msg_1...]"},
+        {wrapped(sack), 2, "Acknowledgment (type: Acknowledgment) [ID: ack_1000...]"},
+        {std::vector<uint8_t>(wire.begin(), wire.begin() + 3), 0, "Parse Error: Failed to decode message header"},
+        {t9, 0, "Parse Error: Unknown message type: template=9, schema=1"},
+        {std::vector<uint8_t>(wire.begin(), wire.begin() + 50), 0,
+         "Parse Error: SBE TopicMessage decoding failed: buffer too short [E100]"},
+        {std::vector<uint8_t>({32, 0, 2, 0, 111, 0, 8, 0, 1, 2, 3, 4}), 0, "Parse Error: Failed to decode SessionEvent"},
+        {wrapped({}), 0, "Parse Error: Session message too short to contain embedded message"},
+        {wrapped({1, 0, 1, 0, 1}), 0, "Parse Error: Embedded message too short"},
+        {wrapped(emb_t5), 0, "Parse Error: Unknown embedded message template_id: 5"},
+        {wrapped(emb_s7), 0, "Parse Error: Unknown embedded message schema_id: 7"},
+        {ack12, 0, "Parse Error: Buffer too short for Acknowledgment message. Need at least 16 bytes, got 12"},
+        {wrapped(ack12), 0, "Parse Error: Buffer too short for Acknowledgment message. Need at least 16 bytes, got 12"},
+        {{}, 0, "Parse Error: Null or empty data"},
+    };
+    std::vector<uint8_t> all;
+    std::vector<uint64_t> off{0};
+    std::vector<ParseResult> single;
+    for (const Case& c : cases) {
+        const ParseResult r = MessageParser::parse_message(c.rec.empty() ? nullptr : c.rec.data(), c.rec.size());
+        single.push_back(r);
+        const std::string d = r.get_description();
+        if (d != c.description) std::fprintf(stderr, "  description '%s' != '%s'\n", d.c_str(), c.description.c_str());
+        CHECK(d == c.description);
+        CHECK(callback_branch(r) == c.branch);
+        if (!c.rec.empty()) {  // the same branch from the oracle restatement's decode
+            const ParseResult o = oracle_fields(c.rec);
+            CHECK(callback_branch(o) == c.branch);
+            CHECK(o.success == r.success && o.message_type == r.message_type && o.message_id == r.message_id &&
+                  o.payload == r.payload && o.template_id == r.template_id && o.schema_id == r.schema_id &&
+                  o.event_code == r.event_code);
+        }
+        all.insert(all.end(), c.rec.begin(), c.rec.end());
+        off.push_back(all.size());
+    }
+    // the session event's fields (sbe_encoder.cpp:629-637)
+    CHECK(single[8].correlation_id == 0x1122334455667788LL && single[8].session_id == 5 &&
+          single[8].leadership_term_id == 6 && single[8].leader_member_id == 1 && single[9].payload == "10.0.0.2:9002");
+    // batch paths == single-record path, record by record
+    const auto batch = MessageParser::parse_batch(all.data(), off.data(), cases.size());
+    const ParsedBatch pb = MessageParser::decode_batch(all.data(), off.data(), cases.size());
+    CHECK(batch.size() == cases.size() && pb.size() == cases.size());
+    for (size_t i = 0; i < cases.size(); ++i) {
+        CHECK(same(batch[i], single[i]));
+        CHECK(same(pb.result(i), single[i]));
+        CHECK(pb.success(i) == single[i].success && pb.template_id(i) == single[i].template_id &&
+              pb.schema_id(i) == single[i].schema_id && pb.timestamp(i) == single[i].timestamp &&
+              pb.sequence_number(i) == single[i].sequence_number);
+        if (pb.status(i) == SBE_ST_TM)
+            CHECK(pb.view(i, 1) == single[i].message_type && pb.view(i, 2) == single[i].message_id &&
+                  pb.view(i, 3) == single[i].payload && pb.view(i, 4) == single[i].headers);
+    }
+    size_t visited = 0;
+    pb.for_each([&](size_t i, const ParseResult& r) {
+        CHECK(i == visited && same(r, single[i]));
+        ++visited;
+    });
+    CHECK(visited == cases.size());
+
+    // MessageParser's other public statics (sbe_messages.hpp:423-450, sbe_encoder.cpp:554-616)
+    CHECK(same(MessageParser::decode_topic_message_with_sbe(wire.data(), wire.size()),
+               MessageParser::parse_message(wire.data(), wire.size())));
+    CHECK(MessageParser::decode_topic_message_with_sbe(sack.data(), sack.size()).error_message ==
+          "Not a TopicMessage (got template_id=2, schema_id=1)");
+    const auto wtm = wrapped(wire);
+    CHECK(MessageParser::decode_topic_message_with_sbe(wtm.data(), wtm.size()).error_message ==
+          "Not a TopicMessage (got template_id=1, schema_id=111)");
+    auto e107 = MessageParser::decode_topic_message_with_sbe(wire.data(), 5);
+    CHECK(!e107.success && e107.template_id == 0 &&
+          e107.error_message == "SBE TopicMessage decoding failed: buffer too short for flyweight [E107]");
+    CHECK(same(MessageParser::decode_acknowledgment_with_sbe(ack45.data(), ack45.size()),
+               MessageParser::parse_message(ack45.data(), ack45.size())));
+    CHECK(MessageParser::decode_acknowledgment_with_sbe(wire.data(), wire.size()).error_message ==
+          "Message is not an Acknowledgment. Expected: template_id=2, schema_id=1. Got: template_id=1, schema_id=1");
+    CHECK(MessageParser::decode_acknowledgment_with_sbe(wire.data(), 3).error_message == "Buffer too short for SBE header");
+    CHECK(MessageParser::decode_acknowledgment_with_sbe(ack12.data(), ack12.size()).error_message ==
+          "Buffer too short for Acknowledgment message. Need at least 16 bytes, got 12");
+    CHECK(MessageParser::get_message_type(wire.data(), wire.size()) == "TopicMessage");
+    CHECK(MessageParser::get_message_type(sack.data(), sack.size()) == "Acknowledgment");
+    CHECK(MessageParser::get_message_type(wire.data(), 7) == "INVALID");
+    CHECK(MessageParser::get_message_type(cases[8].rec.data(), 8) == "SessionEvent");
+    const uint8_t h_conn[8] = {16, 0, 3, 0, 111, 0, 8, 0}, h_c9[8] = {0, 0, 9, 0, 111, 0, 0, 0},
+                  h_t9[8] = {0, 0, 9, 0, 1, 0, 0, 0}, h_s7[8] = {0, 0, 1, 0, 7, 0, 0, 0};
+    CHECK(MessageParser::get_message_type(h_conn, 8) == "SessionConnectRequest");
+    CHECK(MessageParser::get_message_type(h_c9, 8) == "UnknownClusterMessage(9)");
+    CHECK(MessageParser::get_message_type(h_t9, 8) == "UnknownTopicMessage(9)");
+    CHECK(MessageParser::get_message_type(h_s7, 8) == "UnknownSchema(7,1)");
+    CHECK(MessageParser::extract_correlation_id(cases[8].rec.data(), cases[8].rec.size()) == 0x1122334455667788LL);
+    CHECK(MessageParser::extract_correlation_id(cases[8].rec.data(), 15) == 0);
+    CHECK(MessageParser::extract_correlation_id(wire.data(), wire.size()) == 0);
+    CHECK(MessageParser::is_acknowledgment_for(ack45.data(), ack45.size(), "msg_1"));
+    CHECK(MessageParser::is_acknowledgment_for(ack45.data(), ack45.size(), "orders"));  // payload holds it
+    CHECK(!MessageParser::is_acknowledgment_for(ack45.data(), ack45.size(), "zzz"));
+    CHECK(!MessageParser::is_acknowledgment_for(wire.data(), wire.size(), "msg_1"));  // a TopicMessage
+    {  // parse_message_debug: the hex dump of records up to 200 bytes goes to stdout (:557-559)
+        std::ostringstream cap;
+        std::streambuf* old = std::cout.rdbuf(cap.rdbuf());
+        const ParseResult r = MessageParser::parse_message_debug(wire.data(), wire.size(), "p");
+        std::cout.rdbuf(old);
+        CHECK(same(r, MessageParser::parse_message(wire.data(), wire.size())));
+        CHECK(cap.str().rfind("p  0000: 10 00 01 00 01 00 01 00  88 77 66 55 44 33 22 11  |.........wfUD3\".|\n", 0) == 0);
+        // 71 bytes, 64 shown (max_bytes 64), then the rest counted
+        CHECK(cap.str().find("p  0040: ") == std::string::npos && cap.str().find("p  ... (7 more bytes)\n") != std::string::npos);
+        std::cout << std::setfill(' ');
+        std::vector<uint8_t> big = wire_tm({"orders", "CREATE_ORDER", "u", std::string(300, 'p'), "h"}, 3);
+        cap.str("");
+        old = std::cout.rdbuf(cap.rdbuf());
+        (void)MessageParser::parse_message_debug(big.data(), big.size());
+        std::cout.rdbuf(old);
+        CHECK(cap.str().empty());
+    }
+    // SBEUtils (src/sbe_encoder.cpp:370-485)
+    CHECK(SBEUtils::format_timestamp(1760000000123456789LL) == "2025-10-09 08:53:20 UTC.123456789");
+    CHECK(SBEUtils::is_valid_sbe_message(wire.data(), wire.size()) && !SBEUtils::is_valid_sbe_message(wire.data(), 20) &&
+          !SBEUtils::is_valid_sbe_message(h_s7, 8));
+    const auto strs = SBEUtils::extract_readable_strings(ack45.data(), ack45.size(), 3);
+    CHECK(strs.size() == 3 && strs[0] == "msg_1" && strs[1] == "orders" && strs[2] == "corr");
+    CHECK(SBEUtils::get_session_event_code_string(3) == "AUTHENTICATION_REJECTED" &&
+          SBEUtils::get_session_event_code_string(4) == "CLOSED" && SBEUtils::get_session_event_code_string(1) == "ERROR");
+    CHECK(SBEUtils::generate_correlation_id() > 0 && SBEUtils::is_valid_correlation_id(1) &&
+          !SBEUtils::is_valid_correlation_id(0));
 }
 
 int main() {
@@ -418,6 +658,7 @@ int main() {
         const auto ids = pub.publish_topic_batch(msgs);
         CHECK(ids.size() == 50 && sent.size() == 50 && sent[49].size() == 34 + 6 + 12 + ids[49].size() + 7 + 7);
     }
+    surface_tests(f5, wire, sack, ack45);
     std::printf("host api test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_side_entry_points(lib):
     lib.sbe_abi_version.restype = ctypes.c_int
-    assert lib.sbe_abi_version() == 5
+    assert lib.sbe_abi_version() == 6
     lib.sbe_encode_workspace_size.restype = ctypes.c_size_t
     lib.sbe_encode_workspace_size.argtypes = [ctypes.c_uint64]
     assert lib.sbe_encode_workspace_size(1_000_000) >= 16 * (1_000_000 // 256)
@@ -65,8 +65,9 @@ def test_host_side_entry_points(lib):
     assert lib.sbe_comm_init(ctypes.byref(h), 0, 0, uid) == -1
     assert lib.sbe_comm_init(ctypes.byref(h), 2, 2, uid) == -1
     assert lib.sbe_comm_init(None, 1, 0, uid) == -1
-    lib.sbe_gather_encoded.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp, vp]
-    assert lib.sbe_gather_encoded(None, 0, None, None, 0, None, 0, None, None, None) == -1
+    lib.sbe_gather_encoded.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
+                                       ctypes.c_uint64, vp, vp]
+    assert lib.sbe_gather_encoded(None, 0, None, None, 0, None, 0, None, 0, None, None) == -1
     lib.sbe_comm_destroy.argtypes = [vp]
     assert lib.sbe_comm_destroy(None) == 0
 
@@ -110,3 +111,10 @@ def test_profiling_ring_without_launches(lib):
     assert lib.sbe_profile_read(0, buf, 4) == 0       # nothing launched yet
     assert lib.sbe_profile_read(2, buf, 4) == -1      # unknown kernel
     assert lib.sbe_profile_enable(0) == 0
+
+
+def test_codec_library_does_not_link_rccl():
+    """RCCL is dlopen-ed by the first sbe_comm_* call: the codec loads without it."""
+    out = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"\(NEEDED\).*\[(.+?)\]", out)
+    assert needed and not any("rccl" in n for n in needed), needed

@@ -82,5 +82,13 @@ def test_gather_one_rank_communicator(codec):
         small = torch.empty(total - 1, dtype=torch.uint8, device=dev)
         with pytest.raises(codec.SbeError, match="ENOSPC"):
             codec.gather_encoded(comm, enc.out, enc.out_off, n, root=0, dst=small, dst_off=dst_off)
+        # an offsets array one entry short is refused before any write
+        short_off = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        with pytest.raises(codec.SbeError, match="ENOSPC"):
+            codec.gather_encoded(comm, enc.out, enc.out_off, n, root=0, dst=dst, dst_off=short_off)
+        torch.cuda.synchronize()
+        assert int((short_off != -1).sum().item()) == 0
+        with pytest.raises(codec.SbeError, match="n \\+ 1"):
+            codec.gather_encoded(comm, enc.out, enc.out_off[:n], n, root=0, dst=dst, dst_off=dst_off)
     finally:
         comm.close()

@@ -142,3 +142,27 @@ def test_gpu_publish_order_pipeline(codec):
         assert d["status"][i] == codec.ST_TM
         assert rec[vo[3]:vo[3] + vl[3]] == pay[int(pay_off[i]):int(pay_off[i + 1])]
         assert rec[vo[4]:vo[4] + vl[4]] == hdr[int(hdr_off[i]):int(hdr_off[i + 1])]
+
+
+@pytest.mark.gpu
+def test_gpu_side_stream_regrow(codec):
+    """A self-sized call on a side stream that is not torch's current stream: the regrow read of
+    out_off[n] waits for that stream: sizes, statuses and texts are the oracle's."""
+    import torch
+    n = 2000
+    fields, cid, ts, q = T.order_batch(n, 11, True)
+    # long strings of control bytes (each escapes to 6 bytes): the kernels run for a while
+    fields = [tuple((b"\x01" * 700) if j == 0 else f for j, f in enumerate(rec)) for rec in fields]
+    arena, str_len = T.pack_order_fields(fields)
+    exp, exp_off = T.oracle_order_json(arena, str_len, cid, ts, q, 0, nthreads=8)
+    side = torch.cuda.Stream()
+    dev_in = [torch.from_numpy(arena.copy()).cuda(), torch.from_numpy(str_len.astype(np.int32)).cuda(),
+              torch.from_numpy(np.asarray(cid, np.int64)).cuda(), torch.from_numpy(np.asarray(ts, np.int64)).cuda(),
+              torch.from_numpy(np.asarray(q, np.float64)).cuda()]
+    torch.cuda.synchronize()
+    r = codec.order_to_json_batch(*dev_in, 0, stream=side)
+    side.synchronize()
+    off = r.out_off.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(off, exp_off)
+    assert (r.status.cpu().numpy()[:n] == 0).all()
+    assert r.out[: int(off[-1])].cpu().numpy().tobytes() == exp
