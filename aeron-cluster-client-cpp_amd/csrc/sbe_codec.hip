@@ -1,23 +1,27 @@
 // sbe_codec.hip — MI355X (gfx950) batch SBE codec: HIP kernels + the C ABI of include/sbecodec.h.
 //
-// Byte packing, not a contraction: no MFMA.  Both kernels are HBM-stream kernels built around
-// one record per lane, one 64-record tile per single-wave workgroup, and an LDS window that turns
-// the per-record byte scatter/gather into coalesced 16-byte HBM accesses.
+// Byte packing, not a contraction: no MFMA.  Both kernels are HBM-stream kernels whose LDS windows
+// turn the per-record byte scatter / gather into coalesced 16-byte HBM accesses.
 //
-//  encode  (SBEEncoder::encode_topic_message, src/sbe_encoder.cpp:131-167)
-//    1. lane loads its record's 5 lengths + timestamp, wave-scans output (and, packed, input) sizes
-//    2. tile/block byte counts (K1) and their exclusive scan (K2) give every tile its offsets
-//    3. K3, one wave per 64-record tile, per output window: the window's input strings (packed
-//       mode) are staged into LDS with global_load_dwordx4; each lane writes its record into an
-//       XOR-swizzled LDS output window (string interiors as aligned dwords: one LDS read, one
-//       v_alignbyte, one ds_write_b32; literals and string edges as bytes); the wave then stores
-//       the window with global_store_dwordx4
+//  encode  (SBEEncoder::encode_topic_message, src/sbe_encoder.cpp:131-167, and the session / Lite
+//           layouts), two launches:
+//    sbe_enc_sums  one 1024-thread workgroup per 4096-record superblock: each 32-record tile's
+//                  output / packed-input byte prefix inside its superblock, the superblock totals
+//    sbe_enc_pack  persistent, one wave per workgroup, tiles of 32 records (two lanes per record):
+//                  record offsets by a DPP wave scan; output windows of <= 8 KiB holding whole
+//                  records; the next window's input strings loaded into registers while the current
+//                  one is composed (b128 chunk composition from the staged input: five LDS dword
+//                  reads + four v_alignbyte per 16-byte chunk, a zone fix-up pass for string starts
+//                  inside a chunk, literal headers / lengths as byte stores); the window stored with
+//                  16-byte buffer stores (nt)
 //  decode  (MessageParser::parse_message :513-551 / MessageHandler::on_egress
-//           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105)
-//    1. the wave stages its tile's contiguous bytes into the same swizzled LDS window with
-//       global_load_dwordx4
+//           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105 /
+//           the Lite flyweights), one launch, one wave per 64-record tile:
+//    1. the tile's bytes are staged window by window (16 KiB windows, 12 KiB for batches of records
+//       over 256 B on average) into an XOR-swizzled LDS window with 16-byte loads; the second
+//       window's loads are issued before the first one is parsed
 //    2. each lane parses its record from LDS (template-ID dispatch per lane) and writes the
-//       descriptor SoA; bytes outside the window are read from global memory.
+//       descriptor SoA; records no window can hold are parsed from HBM.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_scan.hpp>
@@ -37,8 +41,18 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;                 // records per workgroup (one per lane)
-constexpr uint32_t kWin = 16384;          // LDS window bytes (encode output / decode input)
-constexpr uint32_t kWinDw = kWin / 4;
+// LDS window bytes of the decode kernel: kWin for records up to 256 B on average (a 64-record
+// tile in one window), kWinWide for longer ones (more workgroups per CU; they take two or more
+// windows either way).  sbe_decode_batch_sized picks by the batch's average record size.
+#ifndef SBE_DEC_WIN
+#define SBE_DEC_WIN 16384
+#endif
+#ifndef SBE_DEC_WIN_WIDE
+#define SBE_DEC_WIN_WIDE 12288
+#endif
+constexpr uint32_t kWin = SBE_DEC_WIN;
+constexpr uint32_t kWinWide = SBE_DEC_WIN_WIDE;
+constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWinWide kernel runs
 
 // ------------------------------------------------------------------------------------------
 // LDS window.  Dword i of the window lives at i ^ ((i >> 6) & 28): within each 256-B row (64
@@ -175,6 +189,12 @@ __device__ __forceinline__ void dst_store(T* p, T v) {
 #ifndef SBE_ENC_RPT
 #define SBE_ENC_RPT 32
 #endif
+#ifndef SBE_NO_RECLANE  // A/B: every window through the chunk-owner passes (pack_window)
+#define SBE_NO_RECLANE 0
+#endif
+#ifndef SBE_CR_B64  // record-lane composition: source dwords as ds_read_b64 pairs
+#define SBE_CR_B64 0
+#endif
 constexpr int kSbRec = 2 * 64 * SBE_ENC_RPT;          // records per superblock (one K1 workgroup): 128 tiles
 constexpr int kSbThreads = 1024;
 constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
@@ -189,6 +209,9 @@ static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt
 //   LayTMS  SessionMessageHeader + TopicMessage  src/session_manager.cpp:936-967, :1118-1144
 //   LayL2   CommitOffsetLite (301)           include/model/CommitOffsetLite.h:114-118
 //   LayL3   OrderRequestLite / OrderNotificationLite (201 / 202)  OrderRequestLite.h:114-118
+#ifndef SBE_TM_STORE_ROWS0  // window store rows of the 3- and 5-string layouts issued unconditionally
+#define SBE_TM_STORE_ROWS0 8
+#endif
 template <int kPre_, int kBlk_, int kNF_, bool kTM_>
 struct Lay {
     static constexpr int32_t kPre = kPre_;
@@ -201,7 +224,7 @@ struct Lay {
     static constexpr int32_t ovh(bool trunc) { return kOvh - (trunc ? 8 : 0); }
     // window store rows issued unconditionally (store_window): CommitOffsetLite's 32-record tiles
     // (~77-B records) are ~2.5 KiB, three of the eight 1-KiB rows
-    static constexpr int kStoreRows0 = kNF == 2 ? 3 : 8;
+    static constexpr int kStoreRows0 = kNF == 2 ? 3 : SBE_TM_STORE_ROWS0;
 };
 using LayTM = Lay<0, 16, 5, true>;
 using LayTMS = Lay<32, 16, 5, true>;
@@ -1409,9 +1432,23 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
             u[k] = bsrc0 + X - 2 * f;
             int32_t i = u[k] >> 2;
             i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
+#if SBE_CR_B64
+            // three 8-byte reads from the even dword at or below i (fewer LDS instructions, 64 banks)
+            {
+                const lds_cu32x2* q2 = reinterpret_cast<lds_cu32x2*>(reinterpret_cast<lds_cu32*>(inb) + (i & ~1));
+                const u32x2 e0 = q2[0], e1 = q2[1], e2 = q2[2];
+                const bool odd = (i & 1) != 0;
+                d[k][0] = odd ? e0.y : e0.x;
+                d[k][1] = odd ? e1.x : e0.y;
+                d[k][2] = odd ? e1.y : e1.x;
+                d[k][3] = odd ? e2.x : e1.y;
+                d[k][4] = odd ? e2.y : e2.x;
+            }
+#else
             lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
 #pragma unroll
             for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
+#endif
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
@@ -1578,7 +1615,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         // current window (fast) or the whole tile window by window
         if (fast) {
-            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
+            if (SBE_NO_RECLANE || !compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
             store_window<LY::kStoreRows0>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,
@@ -2203,7 +2240,8 @@ __device__ void dec_lite(const R_t& R, uint32_t len, Desc& d) {
     d.off[4] = R.u32(8);
 }
 
-constexpr int kDecRegs = kWin / 16 / kWave;  // uint4 staging registers per lane (one window)
+template <uint32_t kW>
+constexpr int dec_regs() { return (int)(kW / 16 / kWave); }  // uint4 staging registers per lane (one window)
 
 
 template <uint32_t kMode, typename R_t>
@@ -2231,22 +2269,24 @@ __device__ __noinline__ Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint
 // (bit k: chunk lane + 64 k holds a key-slice dword or a backslash byte), classified from the
 // staging registers (tiles with records over kSeqLaneRec bytes: `wide`), so the "_sequence_number"
 // scan needs no LDS pass of its own.
-__device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane, uint4 (&I)[kDecRegs]) {
+template <uint32_t kW>
+__device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane,
+                                          uint4 (&I)[dec_regs<kW>()]) {
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
     const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + wb;
 #pragma unroll
-    for (int k = 0; k < kDecRegs; ++k) {
+    for (int k = 0; k < dec_regs<kW>(); ++k) {
         const uint32_t ch = lane + kWave * k;
         I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
     }
 }
 
-template <uint32_t kMode>
+template <uint32_t kMode, uint32_t kW>
 __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint64_t we, bool wide, int lane,
-                                               const uint4 (&I)[kDecRegs]) {
+                                               const uint4 (&I)[dec_regs<kW>()]) {
     const uint32_t nch = (uint32_t)((we - wb) >> 4);
 #pragma unroll
-    for (int k = 0; k < kDecRegs; ++k) {
+    for (int k = 0; k < dec_regs<kW>(); ++k) {
         const uint32_t ch = lane + kWave * k;
         if (ch < nch) lds_write_chunk(win, ch, I[k]);
     }
@@ -2256,7 +2296,7 @@ __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint6
         // zero chunks of the last row are never suspect
         const uint32_t nrow = (nch + kWave - 1) / kWave;
 #pragma unroll
-        for (int k = 0; k < kDecRegs; ++k) {
+        for (int k = 0; k < dec_regs<kW>(); ++k) {
             if ((uint32_t)k < nrow) {
                 Suspect S;
                 S.add(I[k]);
@@ -2267,12 +2307,12 @@ __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint6
     return sm;
 }
 
-template <uint32_t kMode>
+template <uint32_t kMode, uint32_t kW>
 __device__ __forceinline__ uint32_t dec_stage(const DecArgs& a, uint32_t* win, uint64_t wb, uint64_t we, bool wide,
                                               int lane) {
-    uint4 I[kDecRegs];
-    dec_issue(a, wb, we, lane, I);
-    return dec_commit<kMode>(win, wb, we, wide, lane, I);
+    uint4 I[dec_regs<kW>()];
+    dec_issue<kW>(a, wb, we, lane, I);
+    return dec_commit<kMode, kW>(win, wb, we, wide, lane, I);
 }
 
 // One workgroup (one wave) per 64-record tile.  The tile's bytes are staged window by window:
@@ -2326,9 +2366,9 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
 #ifndef SBE_DEC_MINW
 #define SBE_DEC_MINW 3
 #endif
-template <uint32_t kMode>
+template <uint32_t kMode, uint32_t kWin>
 __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
-    __shared__ uint32_t win[kWinDw];
+    __shared__ uint32_t win[kWin / 4];
     const int lane = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
     const uint64_t r = t0 + (uint64_t)lane;
@@ -2353,9 +2393,9 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     uint64_t wb = T0 & ~15ull;
     uint64_t we = wb + kWin < end ? wb + kWin : (end > wb ? end : wb);
     const bool wide = __ballot(valid && rl > kSeqLaneRec) != 0;
-    uint4 I[kDecRegs];
-    dec_issue(a, wb, we, lane, I);
-    uint32_t sm = dec_commit<kMode>(win, wb, we, wide, lane, I);
+    uint4 I[dec_regs<kWin>()];
+    dec_issue<kWin>(a, wb, we, lane, I);
+    uint32_t sm = dec_commit<kMode, kWin>(win, wb, we, wide, lane, I);
     // The second window starts at the first record the first one cannot hold, which the record
     // offsets already tell: its loads go out before the first window is parsed (tiles of records
     // over 256 B on average take two windows; each would otherwise wait one more HBM round trip).
@@ -2371,7 +2411,7 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
                 wb2 = rsf & ~15ull;
                 we2 = wb2 + kWin < end ? wb2 + kWin : end;
                 pre = true;
-                dec_issue(a, wb2, we2, lane, I);
+                dec_issue<kWin>(a, wb2, we2, lane, I);
             }
         }
     }
@@ -2379,7 +2419,7 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
     if (pre) {
         wsync();
-        sm = dec_commit<kMode>(win, wb2, we2, wide, lane, I);
+        sm = dec_commit<kMode, kWin>(win, wb2, we2, wide, lane, I);
         wsync();
         dec_window<kMode>(win, wb2, we2, rs, rl, wide, sm, done, d, lane);
     }
@@ -2408,7 +2448,7 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
             if (!again) break;
             we = wb + kWin < end ? wb + kWin : end;
             wsync();
-            sm = dec_stage<kMode>(a, win, wb, we, wide, lane);
+            sm = dec_stage<kMode, kWin>(a, win, wb, we, wide, lane);
             wsync();
             dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
         }
@@ -3017,8 +3057,8 @@ int sbe_encode_lite_batch(const sbe_lite_batch* in, uint64_t n, uint32_t templat
     return enc_launch<LayL3>(q, n, 0, 0, out, out_capacity, out_off, status, workspace, workspace_bytes, stream);
 }
 
-int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
-                     const sbe_decoded* out, void* stream) {
+int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint64_t in_bytes, uint32_t mode,
+                           const sbe_decoded* out, void* stream) {
     if (mode != SBE_DEC_PARSE_MESSAGE && mode != SBE_DEC_ON_EGRESS && mode != SBE_DEC_LITE) return SBE_EINVAL;
     if (n == 0) return SBE_OK;
     if (!in || !rec_off || !out || !out->status || !out->flags || !out->hdr || !out->ts || !out->view_off ||
@@ -3039,14 +3079,28 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     const dim3 grid((uint32_t)tiles), block(kWave);
     hipEvent_t e0, e1;
     prof_slot(1, &e0, &e1);
+    const bool wide = in_bytes > (uint64_t)kWideAvg * n;  // records over kWideAvg bytes on average
+#define SBE_DEC_LAUNCH(M)                                                                                  \
+    do {                                                                                                   \
+        if (wide)                                                                                          \
+            hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinWide>), grid, block, 0, s, e0, e1, 0, a);      \
+        else                                                                                               \
+            hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWin>), grid, block, 0, s, e0, e1, 0, a);          \
+    } while (0)
     if (mode == SBE_DEC_ON_EGRESS)
-        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_ON_EGRESS>), grid, block, 0, s, e0, e1, 0, a);
+        SBE_DEC_LAUNCH(SBE_DEC_ON_EGRESS);
     else if (mode == SBE_DEC_LITE)
-        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_LITE>), grid, block, 0, s, e0, e1, 0, a);
+        SBE_DEC_LAUNCH(SBE_DEC_LITE);
     else
-        hipExtLaunchKernelGGL((sbe_decode_kernel<SBE_DEC_PARSE_MESSAGE>), grid, block, 0, s, e0, e1, 0, a);
+        SBE_DEC_LAUNCH(SBE_DEC_PARSE_MESSAGE);
+#undef SBE_DEC_LAUNCH
     prof_commit(1, e0);
     return record_hip(hipGetLastError());
+}
+
+int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     const sbe_decoded* out, void* stream) {
+    return sbe_decode_batch_sized(in, rec_off, n, 0, mode, out, stream);
 }
 
 int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,

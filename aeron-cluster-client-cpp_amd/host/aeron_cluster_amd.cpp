@@ -1,8 +1,8 @@
 // aeron_cluster_amd.cpp — host side of the reference codec surface over the C ABI.
 // Host memory in, host memory out (the reference's API contract).  Every batch call runs a
-// two-slot pipeline: the batch is cut into chunks of a few MiB; while chunk k is copied to HBM,
-// coded by the HIP kernels of include/sbecodec.h and copied back on stream k%2, the host threads
-// stage chunk k+1 in page-locked memory, so host staging, H2D, kernels and D2H overlap.  Encoded
+// chunk pipeline: the batch is cut into chunks of a few MiB; the host threads stage chunk k+1 in
+// page-locked memory while chunk k is copied to HBM (copy-in stream), coded by the HIP kernels of
+// include/sbecodec.h (compute stream) and chunk k-1 is copied back (copy-out stream).  Encoded
 // bytes land by DMA directly in a recycled page-locked block the caller receives (HostBytes);
 // decode descriptors land in one the same way, and ParseResults are built from them on the host
 // threads.  Results are materialised from the device descriptors (views into the caller's own
@@ -222,41 +222,100 @@ struct HostBuf {
     }
 };
 
-// One pipeline slot: a stream, its staging buffers, and an event marking its input copy done.
-struct Slot {
-    hipStream_t stream = nullptr;
-    hipEvent_t in_done = nullptr;
-    bool pending = false;  // in_done recorded and not yet waited for
-    HostBuf pin_in;
-    DevBuf d_in, d_out;
-    void wait_input_free() {
-        if (pending) hip_check(hipEventSynchronize(in_done), "hipEventSynchronize");
-        pending = false;
+// Three-stream chunk pipeline: host→device copies, kernels and device→host copies each on a
+// stream of their own, ordered per chunk by events, so that chunk k+1's H2D, chunk k's kernels and
+// chunk k-1's D2H run at once (on one stream the copy engine serialises H2D behind D2H).  Chunk k
+// uses slot k % kSlots: its page-locked staging buffer and its device buffers.
+struct Pipeline {
+    static constexpr int kSlots = 3;
+    struct Slot {
+        hipEvent_t in_done = nullptr, comp_done = nullptr, out_done = nullptr;
+        bool used = false;  // its events were recorded by an earlier chunk
+        HostBuf pin;
+        DevBuf d_in, d_out;
+    };
+    hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
+    Slot slot[kSlots];
+    // one-chunk calls: copy-in, kernels and copy-out in order on the compute stream, no events
+    // (a small batch is latency-bound: each event record / wait costs more than it overlaps)
+    bool serial = false;
+
+    void create() {
+        for (hipStream_t* st : {&s_in, &s_comp, &s_out})
+            hip_check(hipStreamCreateWithFlags(st, hipStreamNonBlocking), "hipStreamCreate");
+        for (Slot& sl : slot)
+            for (hipEvent_t* e : {&sl.in_done, &sl.comp_done, &sl.out_done})
+                hip_check(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+    }
+    void destroy() {
+        for (Slot& sl : slot)
+            for (hipEvent_t e : {sl.in_done, sl.comp_done, sl.out_done})
+                if (e) (void)hipEventDestroy(e);
+        for (hipStream_t st : {s_in, s_comp, s_out})
+            if (st) (void)hipStreamDestroy(st);
+    }
+    // chunk k's slot, once the host may rewrite its staging buffer (its last H2D is done)
+    Slot& begin(size_t k) {
+        Slot& sl = slot[serial ? 0 : k % kSlots];
+        if (sl.used) hip_check(hipEventSynchronize(sl.in_done), "hipEventSynchronize");
+        return sl;
+    }
+    void drain() {
+        if (serial) {
+            hip_check(hipStreamSynchronize(s_comp), "hipStreamSynchronize");
+            return;
+        }
+        for (hipStream_t st : {s_in, s_comp, s_out}) hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    }
+    // device buffers of the slot at least this large (growing drains the pipeline first: the old
+    // buffers may still be in use by queued work)
+    void reserve(Slot& sl, size_t in_bytes, size_t out_bytes) {
+        if (in_bytes <= sl.d_in.cap && out_bytes <= sl.d_out.cap) return;
+        drain();
+        sl.d_in.need(in_bytes);
+        sl.d_out.need(out_bytes);
+    }
+    // the slot's staged bytes to d_in, plus (direct) `dbytes` page-locked caller bytes to d_in + doff
+    void copy_in(Slot& sl, size_t bytes, const void* direct = nullptr, size_t doff = 0, size_t dbytes = 0) {
+        hipStream_t st = serial ? s_comp : s_in;
+        if (!serial && sl.used) hip_check(hipStreamWaitEvent(s_in, sl.comp_done, 0), "hipStreamWaitEvent");  // d_in read
+        hip_check(hipMemcpyAsync(sl.d_in.p, sl.pin.p, bytes, hipMemcpyHostToDevice, st), "H2D");
+        if (dbytes) hip_check(hipMemcpyAsync(sl.d_in.b() + doff, direct, dbytes, hipMemcpyHostToDevice, st), "H2D");
+        if (!serial) hip_check(hipEventRecord(sl.in_done, s_in), "hipEventRecord");
+    }
+    // the stream to launch the chunk's kernels on (after its input copy and the slot's last D2H)
+    hipStream_t compute(Slot& sl) {
+        if (serial) return s_comp;
+        hip_check(hipStreamWaitEvent(s_comp, sl.in_done, 0), "hipStreamWaitEvent");
+        if (sl.used) hip_check(hipStreamWaitEvent(s_comp, sl.out_done, 0), "hipStreamWaitEvent");
+        return s_comp;
+    }
+    // the stream to issue the chunk's D2H copies on (after its kernels)
+    hipStream_t copy_out(Slot& sl) {
+        if (serial) return s_comp;
+        hip_check(hipEventRecord(sl.comp_done, s_comp), "hipEventRecord");
+        hip_check(hipStreamWaitEvent(s_out, sl.comp_done, 0), "hipStreamWaitEvent");
+        return s_out;
+    }
+    void end(Slot& sl) {
+        if (serial) return;
+        hip_check(hipEventRecord(sl.out_done, s_out), "hipEventRecord");
+        sl.used = true;
     }
 };
 
 // Per-thread device context (the reference's codec functions are reentrant statics).
 struct Ctx {
-    Slot slot[2];
+    Pipeline pipe;
     DevBuf d_aux;   // reassembly / Order JSON
     HostBuf h_aux;
+    std::vector<uint64_t> pin, pout;  // encode plan scratch (kept: first-touch costs on every call otherwise)
     Ctx() {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");
-        for (Slot& s : slot) {
-            hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
-            hip_check(hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming), "hipEventCreate");
-        }
+        pipe.create();
     }
-    ~Ctx() {
-        for (Slot& s : slot) {
-            if (s.in_done) (void)hipEventDestroy(s.in_done);
-            if (s.stream) (void)hipStreamDestroy(s.stream);
-        }
-    }
-    void sync_all() {
-        for (Slot& s : slot) hip_check(hipStreamSynchronize(s.stream), "hipStreamSynchronize");
-        for (Slot& s : slot) s.pending = false;
-    }
+    ~Ctx() { pipe.destroy(); }
+    void sync_all() { pipe.drain(); }
 };
 
 Ctx& ctx() {
@@ -292,9 +351,10 @@ struct Trace {
     void done(size_t n, size_t chunks) {
         if (!on) return;
         std::fprintf(stderr,
-                     "[trace] %s n=%zu chunks=%zu threads=%u total=%.1fus plan=%.1f stage=%.1f wait=%.1f enqueue=%.1f sync=%.1f "
+                     "[trace] t0=%.1f %s n=%zu chunks=%zu threads=%u total=%.1fus plan=%.1f stage=%.1f wait=%.1f enqueue=%.1f sync=%.1f "
                      "finish=%.1f\n",
-                     what, n, chunks, Workers::get().size(), std::chrono::duration<double, std::micro>(clk::now() - t0).count(), plan, stage,
+                     std::chrono::duration<double, std::micro>(t0.time_since_epoch()).count(), what, n, chunks,
+                     Workers::get().size(), std::chrono::duration<double, std::micro>(clk::now() - t0).count(), plan, stage,
                      wait, enqueue, sync, finish);
     }
 };
@@ -340,23 +400,60 @@ void prefix(size_t n, std::vector<uint64_t>& out, V&& val) {
     out[n] = part[ntasks];
 }
 
+// Two exclusive prefix sums in one pass: val(i, x, y) gives item i's two values.
+template <class V>
+void prefix2(size_t n, std::vector<uint64_t>& ox, std::vector<uint64_t>& oy, V&& val) {
+    ox.resize(n + 1);
+    oy.resize(n + 1);
+    Workers& w = Workers::get();
+    const size_t ntasks = n < 32768 ? 1 : std::min<size_t>(w.size() * 2, n / 8192);
+    std::vector<uint64_t> px(ntasks + 1, 0), py(ntasks + 1, 0);
+    auto lo = [&](size_t t) { return n * t / ntasks; };
+    w.parallel_for(ntasks, [&](size_t t) {
+        uint64_t sx = 0, sy = 0;
+        for (size_t i = lo(t); i < lo(t + 1); ++i) {
+            uint64_t x, y;
+            val(i, x, y);
+            ox[i] = sx;
+            oy[i] = sy;
+            sx += x;
+            sy += y;
+        }
+        px[t + 1] = sx;
+        py[t + 1] = sy;
+    });
+    for (size_t t = 0; t < ntasks; ++t) {
+        px[t + 1] += px[t];
+        py[t + 1] += py[t];
+    }
+    w.parallel_for(ntasks, [&](size_t t) {
+        if (t == 0) return;
+        for (size_t i = lo(t); i < lo(t + 1); ++i) {
+            ox[i] += px[t];
+            oy[i] += py[t];
+        }
+    });
+    ox[n] = px[ntasks];
+    oy[n] = py[ntasks];
+}
+
 }  // namespace
 
 namespace detail {
 struct HostBytesAccess {
-    static HostBytes make(size_t n) {
-        HostBytes h;
+    template <class T = uint8_t>
+    static HostArray<T> make(size_t n) {
+        HostArray<T> h;
         if (n) {
-            h.block_ = PinnedPool::get().take(n);
-            h.p_ = static_cast<uint8_t*>(h.block_.get());
+            h.block_ = PinnedPool::get().take(n * sizeof(T));
+            h.p_ = static_cast<T*>(h.block_.get());
         }
         h.n_ = n;
         return h;
     }
-    static HostBytes from(const uint8_t* p, size_t n) {
-        HostBytes h = make(n);
-        if (n) std::memcpy(h.p_, p, n);
-        return h;
+    template <class T>
+    static void zero(HostArray<T>& h) {
+        if (h.n_) std::memset(static_cast<void*>(h.p_), 0, h.n_ * sizeof(T));
     }
 };
 
@@ -406,45 +503,74 @@ using detail::HostBytesAccess;
 
 namespace {
 
-// Decode n records data[rec_off[i], rec_off[i+1]) with `mode` through the two-slot pipeline.
+// [p, p + bytes) inside one page-locked host allocation (hipHostMalloc, or memory registered with
+// host_register, e.g. an Aeron term buffer, or a HostBytes of this library): the copy engines read
+// it in place, with no staging copy.
+bool page_locked(const void* p, size_t bytes) {
+    if (!p || bytes == 0) return false;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+    void* start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)const_cast<void*>(p)) !=
+            hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)const_cast<void*>(p)) !=
+            hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return start && static_cast<const uint8_t*>(p) >= static_cast<const uint8_t*>(start) &&
+           static_cast<const uint8_t*>(p) + bytes <= static_cast<const uint8_t*>(start) + size;
+}
+
+// Decode n records data[rec_off[i], rec_off[i+1]) with `mode` through the chunk pipeline.
 std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
     auto d = std::make_shared<Descriptors>();
     d->n = n;
     if (n == 0) return d;
     Trace tr("decode");
     Ctx& c = ctx();
+    Pipeline& P = c.pipe;
     const uint64_t base = rec_off[0], total = rec_off[n] - base;
     const size_t C = chunk_records(n, (size_t)total);
     const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
     d->layout(C, parse);
     const size_t K = (n + C - 1) / C;
+    P.serial = K == 1;
+    const bool direct = page_locked(data + base, (size_t)total);  // no staging of the record bytes
     d->block = PinnedPool::get().take(K * d->chunk_bytes);
     uint8_t* hblk = static_cast<uint8_t*>(d->block.get());
     tr.lap(tr.plan);
     for (size_t k = 0; k < K; ++k) {
-        Slot& s = c.slot[k & 1];
         const size_t a = k * C, m = std::min(n, a + C) - a;
         const uint64_t lo = rec_off[a], bytes = rec_off[a + m] - lo;
         const size_t o_data = al16((m + 1) * 8), in_bytes = o_data + bytes;
-        s.wait_input_free();
+        Pipeline::Slot& sl = P.begin(k);
         tr.lap(tr.wait);
-        s.pin_in.need(in_bytes + 16);
-        uint8_t* pin = s.pin_in.b();
+        sl.pin.need((direct ? o_data : in_bytes) + 16);
+        uint8_t* pin = sl.pin.b();
         uint64_t* ro = reinterpret_cast<uint64_t*>(pin);
-        // stage: the chunk's offsets rebased to 0 and its bytes (16-B aligned on the device)
+        // stage: the chunk's offsets rebased to 0 and (unless page-locked already) its bytes; on
+        // the device the bytes start 16-B aligned after the offsets
         for_ranges(m + 1, 8192, [&](size_t x, size_t y) {
             for (size_t i = x; i < y; ++i) ro[i] = rec_off[a + i] - lo;
         });
-        for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) {
-            std::memcpy(pin + o_data + x, data + lo + x, y - x);
-        });
+        if (!direct)
+            for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) {
+                std::memcpy(pin + o_data + x, data + lo + x, y - x);
+            });
         tr.lap(tr.stage);
-        s.d_in.need(in_bytes + 16);
-        s.d_out.need(d->chunk_bytes);
-        hip_check(hipMemcpyAsync(s.d_in.p, pin, in_bytes, hipMemcpyHostToDevice, s.stream), "H2D");
-        hip_check(hipEventRecord(s.in_done, s.stream), "hipEventRecord");
-        s.pending = true;
-        uint8_t* db = s.d_out.b();
+        P.reserve(sl, in_bytes + 16, d->chunk_bytes);
+        if (direct)
+            P.copy_in(sl, (m + 1) * 8, data + lo, o_data, (size_t)bytes);
+        else
+            P.copy_in(sl, in_bytes);
+        hipStream_t st = P.compute(sl);
+        uint8_t* db = sl.d_out.b();
         sbe_decoded out{db,
                         db + d->o_fl,
                         reinterpret_cast<uint16_t*>(db + d->o_hdr),
@@ -452,10 +578,12 @@ std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec
                         reinterpret_cast<uint32_t*>(db + d->o_off),
                         reinterpret_cast<uint32_t*>(db + d->o_len),
                         parse ? reinterpret_cast<uint64_t*>(db + d->o_seq) : nullptr};
-        if (sbe_decode_batch(s.d_in.b() + o_data, reinterpret_cast<const uint64_t*>(s.d_in.p), m, mode, &out, s.stream) !=
-            SBE_OK)
+        if (sbe_decode_batch_sized(sl.d_in.b() + o_data, reinterpret_cast<const uint64_t*>(sl.d_in.p), m, bytes, mode,
+                                   &out, st) != SBE_OK)
             fail("sbe_decode_batch");
-        hip_check(hipMemcpyAsync(hblk + k * d->chunk_bytes, db, d->chunk_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
+        st = P.copy_out(sl);
+        hip_check(hipMemcpyAsync(hblk + k * d->chunk_bytes, db, d->chunk_bytes, hipMemcpyDeviceToHost, st), "D2H");
+        P.end(sl);
         tr.lap(tr.enqueue);
     }
     c.sync_all();
@@ -473,33 +601,38 @@ struct EncodePlan {
     bool wrap16 = false;
 };
 
-// Encode n records (nf strings, a u64 and a u32 each) through the two-slot pipeline.  launch(...)
-// issues one sbe_encode_*_batch call for a chunk.
+// Encode n records (nf strings, a u64 and a u32 each) through the chunk pipeline.  launch(...)
+// issues one sbe_encode_*_batch call for a chunk on the given stream.
 template <class Field, class U64, class U32, class Launch>
 EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, EncodePlan plan, Launch&& launch) {
     EncodedBatch b;
-    b.offsets.assign(n + 1, 0);
-    b.status.assign(n, 0);
-    if (n == 0) return b;
     Trace tr("encode");
+    b.offsets = HostBytesAccess::make<uint64_t>(n + 1);
+    b.status = HostBytesAccess::make<uint8_t>(n);
+    if (n == 0) {
+        b.offsets[0] = 0;
+        return b;
+    }
     Ctx& c = ctx();
-    std::vector<uint64_t> pin, pout;  // per-record input (string) bytes / output bytes, prefixed
-    prefix(n, pin, [&](size_t i) {
-        uint64_t s = 0;
-        for (int k = 0; k < nf; ++k) s += field(i, k).size();
-        return s;
-    });
-    prefix(n, pout, [&](size_t i) -> uint64_t {
-        uint64_t s = plan.overhead;
+    Pipeline& P = c.pipe;
+    // per-record input (string) bytes and output bytes, prefixed, in one pass
+    std::vector<uint64_t>& pin = c.pin;
+    std::vector<uint64_t>& pout = c.pout;
+    prefix2(n, pin, pout, [&](size_t i, uint64_t& in_b, uint64_t& out_b) {
+        uint64_t si = 0, so = plan.overhead;
+        bool e109 = false;
         for (int k = 0; k < nf; ++k) {
             const size_t L = field(i, k).size();
-            if (plan.e109 && L > SBE_VAR_MAX_LEN) return 0;
-            s += plan.wrap16 ? (L & 0xFFFF) : L;
+            si += L;
+            so += plan.wrap16 ? (L & 0xFFFF) : L;
+            e109 |= plan.e109 && L > SBE_VAR_MAX_LEN;
         }
-        return s;
+        in_b = si;
+        out_b = e109 ? 0 : so;
     });
     const size_t C = chunk_records(n, (size_t)(pin[n] + pout[n]) / 2);
     const size_t K = (n + C - 1) / C;
+    P.serial = K == 1;
     b.bytes = HostBytesAccess::make((size_t)pout[n]);
     // per-chunk device offsets (C + 1) and status (C), copied back beside each other
     const size_t meta_stride = al16((C + 1) * 8 + C);
@@ -508,17 +641,16 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
     const size_t ws_bytes = sbe_encode_workspace_size(C);
     tr.lap(tr.plan);
     for (size_t k = 0; k < K; ++k) {
-        Slot& s = c.slot[k & 1];
         const size_t a = k * C, m = std::min(n, a + C) - a;
         const uint64_t in_lo = pin[a], in_bytes = pin[a + m] - in_lo;
         const uint64_t out_lo = pout[a], out_bytes = pout[a + m] - out_lo;
         // staging layout: arena | u32 lengths [m][nf] | u64 [m] | u32 [m]
         const size_t o_len = al16((size_t)in_bytes), o_u64 = o_len + al16((size_t)m * 4 * nf),
                      o_u32 = o_u64 + al16(m * 8), stage = o_u32 + al16(m * 4);
-        s.wait_input_free();
+        Pipeline::Slot& sl = P.begin(k);
         tr.lap(tr.wait);
-        s.pin_in.need(stage);
-        uint8_t* p = s.pin_in.b();
+        sl.pin.need(stage);
+        uint8_t* p = sl.pin.b();
         uint32_t* lp = reinterpret_cast<uint32_t*>(p + o_len);
         uint64_t* up = reinterpret_cast<uint64_t*>(p + o_u64);
         uint32_t* wp = reinterpret_cast<uint32_t*>(p + o_u32);
@@ -539,20 +671,18 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         tr.lap(tr.stage);
         // device: out bytes | out_off [m+1] | status [m] | workspace
         const size_t d_off = al16((size_t)out_bytes), d_ws = d_off + meta_stride;
-        s.d_in.need(stage);
-        s.d_out.need(d_ws + ws_bytes);
-        hip_check(hipMemcpyAsync(s.d_in.p, p, stage, hipMemcpyHostToDevice, s.stream), "H2D");
-        hip_check(hipEventRecord(s.in_done, s.stream), "hipEventRecord");
-        s.pending = true;
-        const uint8_t* di = s.d_in.b();
-        uint8_t* dout = s.d_out.b();
+        P.reserve(sl, stage, d_ws + ws_bytes);
+        P.copy_in(sl, stage);
+        hipStream_t st = P.compute(sl);
+        const uint8_t* di = sl.d_in.b();
+        uint8_t* dout = sl.d_out.b();
         launch(di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
                reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
-               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, s.stream);
-        if (out_bytes)
-            hip_check(hipMemcpyAsync(b.bytes.data() + out_lo, dout, out_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-        hip_check(hipMemcpyAsync(hmeta + k * meta_stride, dout + d_off, (m + 1) * 8 + m, hipMemcpyDeviceToHost, s.stream),
-                  "D2H");
+               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st);
+        st = P.copy_out(sl);
+        if (out_bytes) hip_check(hipMemcpyAsync(b.bytes.data() + out_lo, dout, out_bytes, hipMemcpyDeviceToHost, st), "D2H");
+        hip_check(hipMemcpyAsync(hmeta + k * meta_stride, dout + d_off, (m + 1) * 8 + m, hipMemcpyDeviceToHost, st), "D2H");
+        P.end(sl);
         tr.lap(tr.enqueue);
     }
     c.sync_all();
@@ -861,12 +991,20 @@ std::string ParseResult::get_description() const {
 
 bool gpu_codec_available() { return sbe_device_ready() == 1; }
 
+void host_register(const void* p, std::size_t len) {
+    hip_check(hipHostRegister(const_cast<void*>(p), len, hipHostRegisterDefault), "hipHostRegister");
+}
+void host_unregister(const void* p) { hip_check(hipHostUnregister(const_cast<void*>(p)), "hipHostUnregister"); }
+
 // ======================================================================================
 // encode
 // ======================================================================================
 EncodedBatch SBEEncoder::encode_topic_batch(const std::vector<TopicMessageFields>& msgs, EncodeLength length) {
+    Trace tr("encode_topic_batch");
     // timestamp 0 → the clock the reference reads (src/sbe_encoder.cpp:134-138)
-    return encode_tm(msgs, length, false, 0, 0, clock_ms());
+    EncodedBatch b = encode_tm(msgs, length, false, 0, 0, clock_ms());
+    tr.done(msgs.size(), 0);
+    return b;
 }
 
 std::vector<std::uint8_t> SBEEncoder::encode_topic_message(const std::string& topic, const std::string& message_type,
@@ -968,8 +1106,10 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
     if (message_ids.size() != n) throw std::invalid_argument("orders_to_json: one message id per order");
     OrderJsonBatch r;
     for (EncodedBatch* b : {&r.payload, &r.headers}) {
-        b->offsets.assign(n + 1, 0);
-        b->status.assign(n, 0);
+        b->offsets = HostBytesAccess::make<uint64_t>(n + 1);
+        b->status = HostBytesAccess::make<uint8_t>(n);
+        HostBytesAccess::zero(b->offsets);
+        HostBytesAccess::zero(b->status);
     }
     if (n == 0) return r;
     auto field = [&](size_t i, int k) -> std::string_view {
@@ -986,7 +1126,8 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
         }
     };
     Ctx& c = ctx();
-    Slot& s = c.slot[0];
+    Pipeline::Slot& s = c.pipe.slot[0];  // serial use of the pipeline's first slot (idle between calls)
+    hipStream_t stream = c.pipe.s_comp;
     std::vector<uint64_t> pin;
     prefix(n, pin, [&](size_t i) {
         uint64_t t = 0;
@@ -995,9 +1136,8 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
     });
     const size_t arena = (size_t)pin[n];
     const size_t o_len = al16(arena), nlen = n * 4 * SBE_ORDER_FIELDS, o_num = o_len + al16(nlen), stage = o_num + n * 24;
-    s.wait_input_free();
-    s.pin_in.need(stage);
-    uint8_t* ap = s.pin_in.b();
+    s.pin.need(stage);
+    uint8_t* ap = s.pin.b();
     uint32_t* lp = reinterpret_cast<uint32_t*>(ap + o_len);
     int64_t* cid = reinterpret_cast<int64_t*>(ap + o_num);
     int64_t* ts = cid + n;
@@ -1024,7 +1164,7 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
     const size_t o_off = 0, o_st = al16(2 * (n + 1) * 8), o_ws = o_st + al16(2 * n);
     const size_t wsb = sbe_order_json_workspace_size(n);
     c.d_aux.need(o_ws + wsb);
-    hip_check(hipMemcpyAsync(s.d_in.p, ap, stage, hipMemcpyHostToDevice, s.stream), "H2D");
+    hip_check(hipMemcpyAsync(s.d_in.p, ap, stage, hipMemcpyHostToDevice, stream), "H2D");
     const uint8_t* di = s.d_in.b();
     const int64_t* d_cid = reinterpret_cast<const int64_t*>(di + o_num);
     sbe_order_batch in{di, nullptr, reinterpret_cast<const uint32_t*>(di + o_len), d_cid, d_cid + n,
@@ -1036,11 +1176,11 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
         for (int attempt = 0;; ++attempt) {
             s.d_out.need(cap);
             if (sbe_order_to_json_batch(&in, n, w ? SBE_JSON_PUBLISH_HEADERS : SBE_JSON_ORDER_PAYLOAD, s.d_out.b(), cap,
-                                        off, st, c.d_aux.b() + o_ws, wsb, s.stream) != SBE_OK)
+                                        off, st, c.d_aux.b() + o_ws, wsb, stream) != SBE_OK)
                 fail("sbe_order_to_json_batch");
-            hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
-            hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, s.stream), "D2H");
-            hip_check(hipStreamSynchronize(s.stream), "sync");
+            hip_check(hipMemcpyAsync(b.offsets.data(), off, (n + 1) * 8, hipMemcpyDeviceToHost, stream), "D2H");
+            hip_check(hipMemcpyAsync(b.status.data(), st, n, hipMemcpyDeviceToHost, stream), "D2H");
+            hip_check(hipStreamSynchronize(stream), "sync");
             if (b.offsets[n] <= cap || attempt > 0) break;
             cap = b.offsets[n];  // the measured size: one rerun
         }
@@ -1048,8 +1188,8 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
             if (b.status[i] != SBE_JSON_OK) throw std::runtime_error("sbecodec: order JSON record did not fit");
         b.bytes = HostBytesAccess::make((size_t)b.offsets[n]);
         if (b.offsets[n]) {
-            hip_check(hipMemcpyAsync(b.bytes.data(), s.d_out.p, b.offsets[n], hipMemcpyDeviceToHost, s.stream), "D2H");
-            hip_check(hipStreamSynchronize(s.stream), "sync");
+            hip_check(hipMemcpyAsync(b.bytes.data(), s.d_out.p, b.offsets[n], hipMemcpyDeviceToHost, stream), "D2H");
+            hip_check(hipStreamSynchronize(stream), "sync");
         }
     }
     return r;
@@ -1243,20 +1383,21 @@ std::optional<LiteRecord> decode_lite(const std::uint8_t* data, std::size_t len)
 EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const std::uint64_t* frag_off,
                                                const std::uint8_t* flags, std::size_t n) {
     Ctx& c = ctx();
-    Slot& s = c.slot[0];
+    Pipeline::Slot& s = c.pipe.slot[0];  // serial use of the pipeline's first slot (idle between calls)
+    hipStream_t stream = c.pipe.s_comp;
     EncodedBatch b;
     // the accumulator so far goes first as a middle fragment (flags 0): it is appended to exactly
     // as the reference's acc_ would be, or cleared by a BEGIN
     const size_t pre = acc_.empty() ? 0 : 1, nf = n + pre;
     if (nf == 0) {
-        b.offsets.assign(1, 0);
+        b.offsets = HostBytesAccess::make<uint64_t>(1);
+        b.offsets[0] = 0;
         return b;
     }
     const uint64_t base = n ? frag_off[0] : 0, body = n ? frag_off[n] - base : 0, total = acc_.size() + body;
     const size_t o_fl = (nf + 1) * 8, o_data = al16(o_fl + nf), stage = o_data + total;
-    s.wait_input_free();
-    s.pin_in.need(stage + 16);
-    uint8_t* hp = s.pin_in.b();
+    s.pin.need(stage + 16);
+    uint8_t* hp = s.pin.b();
     uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
     uint8_t* hf = hp + o_fl;
     std::memcpy(hp + o_data, acc_.data(), acc_.size());
@@ -1274,28 +1415,29 @@ EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const s
     const size_t d_off = al16(total), d_cnt = d_off + (nf + 1) * 8, d_ws = al16(d_cnt + 16);
     const size_t wsb = sbe_reassemble_workspace_size(nf);
     s.d_out.need(d_ws + wsb);
-    hip_check(hipMemcpyAsync(s.d_in.p, hp, stage, hipMemcpyHostToDevice, s.stream), "H2D");
+    hip_check(hipMemcpyAsync(s.d_in.p, hp, stage, hipMemcpyHostToDevice, stream), "H2D");
     uint8_t* dout = s.d_out.b();
     uint64_t* dmo = reinterpret_cast<uint64_t*>(dout + d_off);
     uint64_t* dcnt = reinterpret_cast<uint64_t*>(dout + d_cnt);
     if (sbe_reassemble_fragments(s.d_in.b() + o_data, reinterpret_cast<const uint64_t*>(s.d_in.p), s.d_in.b() + o_fl, nf,
-                                 dout, dmo, dcnt, dout + d_ws, wsb, s.stream) != SBE_OK)
+                                 dout, dmo, dcnt, dout + d_ws, wsb, stream) != SBE_OK)
         fail("sbe_reassemble_fragments");
     c.h_aux.need(16);
     uint64_t* counts = reinterpret_cast<uint64_t*>(c.h_aux.p);
-    hip_check(hipMemcpyAsync(counts, dcnt, 16, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), "sync");
+    hip_check(hipMemcpyAsync(counts, dcnt, 16, hipMemcpyDeviceToHost, stream), "D2H");
+    hip_check(hipStreamSynchronize(stream), "sync");
     const uint64_t m = counts[0], carry = counts[1];
-    b.offsets.resize(m + 1);
-    b.status.assign(m, 0);
-    hip_check(hipMemcpyAsync(b.offsets.data(), dmo, (m + 1) * 8, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), "sync");
+    b.offsets = HostBytesAccess::make<uint64_t>(m + 1);
+    b.status = HostBytesAccess::make<uint8_t>(m);
+    HostBytesAccess::zero(b.status);
+    hip_check(hipMemcpyAsync(b.offsets.data(), dmo, (m + 1) * 8, hipMemcpyDeviceToHost, stream), "D2H");
+    hip_check(hipStreamSynchronize(stream), "sync");
     const uint64_t msg_bytes = b.offsets[m];
     b.bytes = HostBytesAccess::make((size_t)msg_bytes);
     acc_.resize(carry);
-    if (msg_bytes) hip_check(hipMemcpyAsync(b.bytes.data(), dout, msg_bytes, hipMemcpyDeviceToHost, s.stream), "D2H");
-    if (carry) hip_check(hipMemcpyAsync(acc_.data(), dout + msg_bytes, carry, hipMemcpyDeviceToHost, s.stream), "D2H");
-    hip_check(hipStreamSynchronize(s.stream), "sync");
+    if (msg_bytes) hip_check(hipMemcpyAsync(b.bytes.data(), dout, msg_bytes, hipMemcpyDeviceToHost, stream), "D2H");
+    if (carry) hip_check(hipMemcpyAsync(acc_.data(), dout + msg_bytes, carry, hipMemcpyDeviceToHost, stream), "D2H");
+    hip_check(hipStreamSynchronize(stream), "sync");
     return b;
 }
 

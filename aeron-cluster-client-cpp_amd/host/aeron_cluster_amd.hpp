@@ -135,32 +135,44 @@ struct HostBytesAccess;
 struct Descriptors;
 }  // namespace detail
 
-// Bytes in page-locked host memory taken from a recycled pool: the device's DMA engines copy the
-// encoded stream straight into it (no staging copy, no zero fill), and the caller reads it in place.
-// Copies share the block; the block returns to the pool with the last copy.
-class HostBytes {
+// An array in page-locked host memory taken from a recycled pool: the device's DMA engines copy
+// results straight into it (no staging copy, no zero fill, no page faults on reuse), and the caller
+// reads it in place.  Copies share the block; the block returns to the pool with the last copy.
+template <class T>
+class HostArray {
 public:
-    const std::uint8_t* data() const { return p_; }
-    std::uint8_t* data() { return p_; }
+    const T* data() const { return p_; }
+    T* data() { return p_; }
     std::size_t size() const { return n_; }
     bool empty() const { return n_ == 0; }
-    const std::uint8_t* begin() const { return p_; }
-    const std::uint8_t* end() const { return p_ + n_; }
-    std::uint8_t operator[](std::size_t i) const { return p_[i]; }
-    std::vector<std::uint8_t> to_vector() const { return std::vector<std::uint8_t>(begin(), end()); }
+    const T* begin() const { return p_; }
+    const T* end() const { return p_ + n_; }
+    T* begin() { return p_; }
+    T* end() { return p_ + n_; }
+    const T& operator[](std::size_t i) const { return p_[i]; }
+    T& operator[](std::size_t i) { return p_[i]; }
+    const T& back() const { return p_[n_ - 1]; }
+    std::vector<T> to_vector() const { return std::vector<T>(begin(), end()); }
+    friend bool operator==(const HostArray& a, const std::vector<T>& v) {
+        if (a.n_ != v.size()) return false;
+        for (std::size_t i = 0; i < a.n_; ++i)
+            if (!(a.p_[i] == v[i])) return false;
+        return true;
+    }
 
 private:
     friend struct detail::HostBytesAccess;
     std::shared_ptr<void> block_;
-    std::uint8_t* p_ = nullptr;
+    T* p_ = nullptr;
     std::size_t n_ = 0;
 };
+using HostBytes = HostArray<std::uint8_t>;
 
 // A packed batch of encoded records: record i = bytes[offsets[i], offsets[i+1]).
 struct EncodedBatch {
     HostBytes bytes;
-    std::vector<std::uint64_t> offsets;
-    std::vector<std::uint8_t> status;  // SBE_ENC_* per record
+    HostArray<std::uint64_t> offsets;
+    HostArray<std::uint8_t> status;  // SBE_ENC_* per record
     std::string_view record(std::size_t i) const {
         return {reinterpret_cast<const char*>(bytes.data()) + offsets[i], static_cast<std::size_t>(offsets[i + 1] - offsets[i])};
     }
@@ -393,5 +405,11 @@ std::size_t offer_batch(const EncodedBatch& batch, const OfferFn& offer);
 
 // true when a gfx950 device is usable (all entry points above need one).
 bool gpu_codec_available();
+
+// Page-locks a long-lived host buffer (e.g. an Aeron term buffer mapped from /dev/shm) for the
+// device's copy engines: batches decoded from registered (or hipHostMalloc'd) memory are copied to
+// HBM in place, without the staging copy.  The memory stays registered until host_unregister.
+void host_register(const void* p, std::size_t len);
+void host_unregister(const void* p);
 
 }  // namespace aeron_cluster

@@ -126,6 +126,10 @@ def _load():
     lib.sbe_decode_batch.restype = ctypes.c_int
     lib.sbe_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.POINTER(_Decoded), ctypes.c_void_p]
+    if hasattr(lib, "sbe_decode_batch_sized"):
+        lib.sbe_decode_batch_sized.restype = ctypes.c_int
+        lib.sbe_decode_batch_sized.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                               ctypes.c_uint32, ctypes.POINTER(_Decoded), ctypes.c_void_p]
     lib.sbe_eval_sequence_numbers.restype = ctypes.c_int
     lib.sbe_eval_sequence_numbers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(_Decoded), ctypes.c_void_p, ctypes.c_void_p]
@@ -374,10 +378,12 @@ def alloc_decoded(n: int, device) -> Decoded:
 
 
 def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = None, stream=None,
-                 seq=None) -> Decoded:
+                 seq=None, in_bytes: int = 0) -> Decoded:
     """Batch decode of the records data[rec_off[i]:rec_off[i+1]] (rec_off int64 [n+1]).
     Parse mode with seq (int64 [n]): the same launch writes ParseResult.sequence_number of the
-    records flagged FL_SEQ_KEY / FL_SEQ_ESC (others are not written; seq=True allocates it zeroed)."""
+    records flagged FL_SEQ_KEY / FL_SEQ_ESC (others are not written; seq=True allocates it zeroed).
+    in_bytes: the records' total bytes when the caller knows them (rec_off[n] - rec_off[0]); only
+    picks the kernel shape (sbe_decode_batch_sized), results are the same."""
     data = _dev(data, torch.uint8, "data")
     rec_off = _dev(rec_off, torch.int64, "rec_off")
     n = int(rec_off.numel()) - 1
@@ -389,7 +395,11 @@ def decode_batch(data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = No
         seq = _dev(seq, torch.int64, "seq")
     d = _Decoded(*(getattr(out, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")),
                  None if seq is None else seq.data_ptr())
-    rc = lib().sbe_decode_batch(_ptr(data), _ptr(rec_off), n, mode, ctypes.byref(d), _stream(stream))
+    if in_bytes and hasattr(lib(), "sbe_decode_batch_sized"):
+        rc = lib().sbe_decode_batch_sized(_ptr(data), _ptr(rec_off), n, int(in_bytes), mode, ctypes.byref(d),
+                                          _stream(stream))
+    else:
+        rc = lib().sbe_decode_batch(_ptr(data), _ptr(rec_off), n, mode, ctypes.byref(d), _stream(stream))
     _check(rc, "sbe_decode_batch")
     keys = ("status", "flags", "hdr", "ts", "view_off", "view_len")
     if n < out.status.numel():

@@ -61,7 +61,9 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--records", type=int, default=1_000_000, help="records per GPU (headline)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0)")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="host threads of the CPU baseline (0: the cores this process may use, capped by "
+                        "OMP_NUM_THREADS, which the GPU box sets to its 16-core share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-config5", action="store_true", help="skip the config-5 strong-scaling leg")
     p.add_argument("--config5-records", type=int, default=134_217_728)
@@ -134,33 +136,79 @@ def make_inputs(n, rank, dev):
             torch.from_numpy(ts.view(np.int64)).to(dev))
 
 
+def host_cpu():
+    """nproc, the cores this process may run on, and the CPU model (state them)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": allowed, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def default_cpu_threads():
+    cpu = host_cpu()
+    t = cpu["affinity"] or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        t = min(t, int(omp))
+    return max(1, t)
+
+
 def cpu_baseline(n_sample, budget_s, threads):
-    """Oracle restatement (a C port of src/sbe_encoder.cpp encode + parse_message) on the host
-    cores: repeat the round trip over an n_sample-record slice of the same workload until budget_s.
-    It is NOT the reference's own speed: the reference builds std::strings, runs jsoncpp and
-    evaluates DEBUG_LOG arguments per record, so this flatters the CPU."""
+    """Timed on the host cores, same run, bounded sample of the headline workload:
+    - the oracle restatement (a C port of src/sbe_encoder.cpp encode + parse_message), one thread and
+      `threads` OpenMP threads: the full round trip;
+    - the reference's own compiled code where it compiles here: the SBE flyweight sequence of
+      SBEEncoder::encode_topic_message (src/sbe_encoder.cpp:141-164, oracle/_ref built from
+      /root/reference/include/model), encode only, one thread and `threads` threads.
+    Neither is the reference's full speed: its parse_message also builds std::strings, runs jsoncpp
+    and evaluates DEBUG_LOG arguments per record."""
     import sbe_testlib as T
     arena, L, ts = T.fixed256_orders(n_sample)
     T.oracle_encode(arena[:222], L[:1], ts[:1])  # load/build
 
-    def run(nthreads, budget):
+    def timed(fn, budget):
         done, t0 = 0, time.perf_counter()
         while True:
-            out, off, _ = T.oracle_encode(arena, L, ts, nthreads=nthreads)
-            d = T.oracle_decode(out, off, T.DEC_PARSE, nthreads=nthreads)
-            T.oracle_seq_batch(out, off, d, nthreads=nthreads)
+            fn()
             done += n_sample
             el = time.perf_counter() - t0
             if el >= budget:
                 return done / el
 
-    r1 = run(1, budget_s * 0.25)
-    rt = run(threads, budget_s * 0.75)
+    def roundtrip(nthreads):
+        out, off, _ = T.oracle_encode(arena, L, ts, nthreads=nthreads)
+        d = T.oracle_decode(out, off, T.DEC_PARSE, nthreads=nthreads)
+        T.oracle_seq_batch(out, off, d, nthreads=nthreads)
+
+    r1 = timed(lambda: roundtrip(1), budget_s * 0.2)
+    rt = timed(lambda: roundtrip(threads), budget_s * 0.4)
+    ref = None
+    if T.ref_available():
+        eo, eoff, _ = T.oracle_encode(arena, L, ts, flags=1)  # REF_TRUNCATE8: encode_topic_message's bytes
+        ro, roff = T.ref_encode_batch(arena, L, ts, wire=False, nthreads=threads)
+        same = bool(np.array_equal(ro, eo) and np.array_equal(roff, eoff))
+        run, _, _ = T.ref_encode_prepared(arena, L, ts, wire=False)
+        f1 = timed(lambda: run(1), budget_s * 0.15)
+        ft = timed(lambda: run(threads), budget_s * 0.25)
+        ref = {"what": "SBEEncoder::encode_topic_message's flyweight sequence (src/sbe_encoder.cpp:141-164), "
+                       "the reference's generated TopicMessage.h compiled from /root/reference (oracle/_ref), "
+                       "encode only, records/s",
+               "value_1thread": f1, "value": ft, "threads": threads, "bytes_equal_to_restatement": same}
     return dict(value=rt, unit="records/s", cores=threads, kind="port",
                 sample=f"{n_sample} fixed-256 records, encode+parse_message round trip repeated for "
-                       f"{budget_s:.0f} s (oracle/sbe_oracle.c, a C restatement, OpenMP {threads} threads; "
+                       f"{budget_s * 0.6:.0f} s (oracle/sbe_oracle.c, a C restatement, OpenMP {threads} threads; "
                        f"1 thread: {r1:.4g} rec/s)",
-                value_1thread=r1,
+                value_1thread=r1, host=host_cpu(), reference_flyweights_encode=ref,
                 reference_indicative={
                     "note": "the reference's own functions, survey container (Xeon, 8 vCPU), BASELINE.md §2; "
                             "the restatement runs without their std::string / jsoncpp / DEBUG_LOG costs",
@@ -221,12 +269,14 @@ def config5(args, world, rank, dev):
         torch.cuda.synchronize()
         barrier(world)
         t_eg = max_over_ranks((time.perf_counter() - t0) / reps, world)
+        verify = None
         if rank == 0:
-            ok = ok and nbytes == 256 * N and nrec == N and int(dst_off[N].item()) == 256 * N
-            # spot check: the last record of each shard sits where a single-GPU encode puts it
-            for r in range(world):
-                a, b = shard.shard_range(N, world, r)
-                ok = ok and int(dst_off[b - 1].item()) == 256 * (b - 1)
+            ok = ok and nbytes == 256 * N and nrec == N
+            # byte check of the whole gathered stream on the root (outside the timed region): every
+            # record is a function of its global index (T.config5_shard), so the root re-encodes the
+            # batch chunk by chunk on its own GPU and compares bytes and offsets with what arrived
+            verify = verify_gathered(dst, dst_off, N, dev, ws)
+            ok = ok and verify["mismatched_chunks"] == 0
         into_root = 256 * (N - m) if rank == 0 else 0
         into_root = int(max_over_ranks(float(into_root), world))
         res["encode_gather"] = {"seconds": t_eg, "records_per_s": N / t_eg,
@@ -234,6 +284,8 @@ def config5(args, world, rank, dev):
                                 "GBps_into_root": into_root / max(t_eg - t_enc, 1e-9) / 1e9,
                                 "frac_of_xgmi_root_ingress": into_root / max(t_eg - t_enc, 1e-9) / 1e9 / XGMI_ROOT_GBS,
                                 "collective": "sbe_gather_encoded (ncclAllGather of sizes + grouped ncclSend/ncclRecv)"}
+        if rank == 0:
+            res["encode_gather"]["verify"] = verify
         g.close()
         del dst, dst_off
     else:
@@ -243,6 +295,27 @@ def config5(args, world, rank, dev):
     del arena, L, ts, out, out_off, status, ws
     torch.cuda.empty_cache()
     return res
+
+
+def verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 22):
+    """The root's gathered config-5 stream == a single-GPU encode of the same records: records
+    [a, b) regenerated from their global indices, encoded here, compared byte for byte with
+    dst[256 a : 256 b] and dst_off[a : b + 1] (fixed-256 records: offsets 256 i)."""
+    import sbe_testlib as T
+    bad, t0 = 0, time.perf_counter()
+    out = torch.empty(256 * chunk + 16, dtype=torch.uint8, device=dev)
+    off = torch.empty(chunk + 1, dtype=torch.int64, device=dev)
+    for a in range(0, N, chunk):
+        b = min(N, a + chunk)
+        arena, L, ts = T.config5_shard(a, b, dev)
+        sbecodec.encode_topic_batch(arena, L, ts, out=out, out_off=off[: b - a + 1], status=False, workspace=ws)
+        same = torch.equal(out[: 256 * (b - a)], dst[256 * a: 256 * b]) and \
+            torch.equal(off[: b - a + 1] + 256 * a, dst_off[a: b + 1])
+        bad += 0 if same else 1
+    torch.cuda.synchronize()
+    return {"records": N, "chunk_records": chunk, "mismatched_chunks": bad,
+            "method": "root re-encodes the closed-form config-5 records chunk by chunk and compares bytes + offsets",
+            "seconds": time.perf_counter() - t0}
 
 
 def main():
@@ -360,7 +433,7 @@ def main():
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
-            cpu = cpu_baseline(min(n, 200_000), args.cpu_seconds, args.cpu_threads)
+            cpu = cpu_baseline(min(n, 200_000), args.cpu_seconds, args.cpu_threads or default_cpu_threads())
         ach = gbs(dom["bytes_per_record"], dom["ms"])
         line = {
             "metric": METRIC, "value": value, "unit": "records/s", "n_gpus": world, "steps": args.steps,

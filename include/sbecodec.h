@@ -263,6 +263,14 @@ typedef struct sbe_decoded {
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream);
 
+/* sbe_decode_batch with the batch's total record bytes (rec_off[n] - rec_off[0]) as the caller
+ * knows them, used only to pick the kernel shape: batches of records over 256 B on average
+ * (session frames, long payloads) run with 12 KiB LDS windows (more workgroups per CU), others
+ * with 16 KiB (a 64-record tile in one window).  in_bytes = 0: the 16 KiB kernel.  Outputs are
+ * identical either way. */
+int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint64_t in_bytes, uint32_t mode,
+                           const sbe_decoded* out, void* stream);
+
 /* ParseResult.sequence_number (src/sbe_encoder.cpp:1031-1125) as a separate launch, for
  * descriptors decoded with seq == NULL: for every record that
  * sbe_decode_batch(SBE_DEC_PARSE_MESSAGE) left with status SBE_ST_TM and flag SBE_FL_SEQ_KEY or

@@ -209,6 +209,27 @@ int ref_tm_encode(const uint8_t* const* s, const uint32_t* len, uint64_t ts, int
     return 0;
 }
 
+// ref_tm_encode over a packed batch (record i's strings back to back after record i-1's), for the
+// CPU baseline: the reference's own flyweight sequence per record, records spread over nthreads
+// OpenMP threads.  out holds the records back to back at out_off[i] (n + 1 entries, computed by the
+// caller from the lengths: wire ? 34 : 26 + Σlen).  Returns the number of records that failed.
+int ref_tm_encode_batch(const uint8_t* arena, const uint32_t* str_len, const uint64_t* ts, uint64_t n, int wire,
+                        uint8_t* out, const uint64_t* out_off, const uint64_t* in_off, int nthreads) {
+    int bad = 0;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : bad)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        const uint8_t* s[5];
+        uint64_t at = in_off[i];
+        for (int k = 0; k < 5; ++k) {
+            s[k] = arena + at;
+            at += str_len[5 * i + k];
+        }
+        uint64_t len = 0;
+        bad += ref_tm_encode(s, str_len + 5 * i, ts[i], wire, out + out_off[i], out_off[i + 1] - out_off[i], &len) != 0;
+    }
+    return bad;
+}
+
 // The encoder block of ClusterClient::publish_topic (src/cluster_client.cpp:1823-1858) in its call
 // order, with the protocol.hpp:8-12 constants: buffer of 8+8+Σ+128 zero bytes, MessageHeader
 // wrap(buf, 0, SBE_VERSION, size) and the four setters, TopicMessage wrapForEncode(buf, 8,

@@ -1,0 +1,112 @@
+"""Interleaved A/B timing of library builds in ONE process over several workloads: for each build,
+rounds of timed blocks with HIP events on the pack and decode kernels (the library's profiling
+ring), medians per (build, workload).  Every build's output is checked against the first build's
+(bytes and descriptors).  Workloads:
+  fixed   1 M fixed-256 Order TopicMessages, encode + parse decode (the headline)
+  var     4 M variable-length TopicMessages (config 4's generator), encode + parse decode
+  mixed   1 M mixed TM / Ack records (config 3), parse decode
+  session 1 M session-framed fixed-256, encode + parse decode
+Usage: python scripts/ab_rows.py lib1.so lib2.so ... [--work fixed,var,mixed] [--rounds R] [--steps K]"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "aeron-cluster-client-cpp_amd"), os.path.join(ROOT, "tests")]
+import sbe_testlib as T  # noqa: E402
+import sbecodec  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("libs", nargs="+")
+ap.add_argument("--work", default="fixed,var,mixed")
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--var-records", type=int, default=4_000_000)
+args = ap.parse_args()
+
+sbecodec.use_library(os.path.abspath(args.libs[0]))
+sbecodec.require_device()
+dev = torch.device("cuda:0")
+
+
+def prep(kind):
+    if kind in ("fixed", "session"):
+        n = 1_000_000
+        arena, L, ts = T.fixed256_orders(n)
+        a = torch.from_numpy(arena).to(dev)
+        l = torch.from_numpy(L.view(np.int32)).to(dev)
+        t = torch.from_numpy(ts.view(np.int64)).to(dev)
+        return dict(n=n, a=a, l=l, t=t, enc=True, session=kind == "session")
+    if kind == "var":
+        n = args.var_records
+        a, l, t = T.var_orders_t(n, dev)
+        return dict(n=n, a=a, l=l, t=t, enc=True, session=False)
+    if kind == "mixed":
+        data, off = T.mixed_records(1_000_000)
+        return dict(n=1_000_000, data=torch.from_numpy(data).to(dev),
+                    off=torch.from_numpy(off.view(np.int64)).to(dev), enc=False)
+    raise SystemExit(f"unknown workload {kind}")
+
+
+works = {k: prep(k) for k in args.work.split(",")}
+for w in works.values():
+    n = w["n"]
+    w["bytes"] = int(w["off"][-1]) if "off" in w else (
+        int(w["l"].sum()) + n * (34 if not w["session"] else 32 + 26))
+    if w["enc"]:
+        cap = int(w["l"].sum()) + 66 * n
+        w["out"] = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
+        w["off_o"] = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        w["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
+    w["seq"] = torch.zeros(n, dtype=torch.int64, device=dev)
+
+res = {(p, k): {"pack": [], "dec": []} for p in args.libs for k in works}
+ref = {}
+for rnd in range(args.rounds):
+    for p in args.libs:
+        sbecodec.use_library(os.path.abspath(p))
+        for k, w in works.items():
+            n = w["n"]
+            ws = sbecodec.alloc_workspace(n, dev) if w["enc"] else None
+            dec = sbecodec.alloc_decoded(n, dev)
+
+            def step():
+                if w["enc"]:
+                    if w["session"]:
+                        sbecodec.encode_session_batch(w["a"], w["l"], w["t"], 7, 8, out=w["out"], out_off=w["off_o"],
+                                                      status=w["st"], workspace=ws)
+                    else:
+                        sbecodec.encode_topic_batch(w["a"], w["l"], w["t"], out=w["out"], out_off=w["off_o"],
+                                                    status=w["st"], workspace=ws)
+                    sbecodec.decode_batch(w["out"], w["off_o"], out=dec, seq=w["seq"], in_bytes=w["bytes"])
+                else:
+                    sbecodec.decode_batch(w["data"], w["off"], out=dec, seq=w["seq"], in_bytes=w["bytes"])
+
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            if rnd == 0:  # every build must produce the same bytes and descriptors
+                h = (int(dec.status.to(torch.int64).sum()), int(dec.view_off.to(torch.int64).sum()),
+                     int(dec.view_len.to(torch.int64).sum()), int(dec.ts.sum()))
+                if w["enc"]:
+                    m = int(w["off_o"][-1])
+                    h += (m, int(w["out"][:m].to(torch.int64).sum()), int(w["off_o"].sum()))
+                ref.setdefault(k, h)
+                assert h == ref[k], f"{p} {k}: output differs from {args.libs[0]}"
+            sbecodec.profile_enable(1)
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            res[(p, k)]["pack"] += sbecodec.profile_read(sbecodec.PROF_PACK)
+            res[(p, k)]["dec"] += sbecodec.profile_read(sbecodec.PROF_DECODE)
+            sbecodec.profile_enable(0)
+            del ws, dec
+for k in works:
+    for p in args.libs:
+        r = res[(p, k)]
+        pk = f"pack med {np.median(r['pack']) * 1e3:8.1f} us" if r["pack"] else " " * 21
+        print(f"{k:8s} {os.path.basename(p):22s} {pk} | decode med {np.median(r['dec']) * 1e3:8.1f} us "
+              f"(min {np.min(r['dec']) * 1e3:8.1f})", flush=True)

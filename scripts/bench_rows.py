@@ -99,7 +99,9 @@ def row_mixed(steps, warmup):
     data, off = T.mixed_records(n)
     d, o = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
     out = sbecodec.alloc_decoded(n, "cuda")
-    s, _, dk = timed(lambda: sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out), steps, warmup)
+    nb = int(off[-1])
+    s, _, dk = timed(lambda: sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out, in_bytes=nb), steps,
+                     warmup)
     k = 200_000
     dk_, ok_ = data[: int(off[k])], off[: k + 1]
     set_cpu(cpu_rate(lambda: T.oracle_decode(dk_, ok_, T.DEC_PARSE, nthreads=CPU_THREADS), k),
@@ -116,13 +118,13 @@ def row_var(steps, warmup):
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
     ws = sbecodec.alloc_workspace(n, "cuda")
     dec = sbecodec.alloc_decoded(n, "cuda")
+    outb = int(a.numel()) + 34 * n  # the stream's bytes (every record encodable)
 
     def step():
         sbecodec.encode_topic_batch(a, l, t, out=ob, out_off=oo, status=st, workspace=ws)
-        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec, in_bytes=outb)
 
     s, pk, dk = timed(step, steps, warmup)
-    outb = int(a.numel()) + 34 * n
     k = 200_000
     ak, Lk, tk = T.var_orders(k)
 
@@ -147,7 +149,7 @@ def row_session(steps, warmup):
 
     def step():
         sbecodec.encode_session_batch(a, l, t, 7, 8, out=ob, out_off=oo, status=st, workspace=ws)
-        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec, in_bytes=n * (32 + 248))
 
     s, pk, dk = timed(step, steps, warmup)
     rec = 32 + 248
@@ -175,13 +177,13 @@ def row_lite(t_id, steps, warmup):
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
     ws = sbecodec.alloc_workspace(n, "cuda")
     dec = sbecodec.alloc_decoded(n, "cuda")
+    outb = arena.size + (20 + 2 * nf) * n
 
     def step():
         sbecodec.encode_lite_batch(t_id, a, l, ti, sq, out=ob, out_off=oo, status=st, workspace=ws)
-        sbecodec.decode_batch(ob, oo, sbecodec.DEC_LITE, out=dec)
+        sbecodec.decode_batch(ob, oo, sbecodec.DEC_LITE, out=dec, in_bytes=outb)
 
     s, pk, dk = timed(step, steps, warmup)
-    outb = arena.size + (20 + 2 * nf) * n
     k = 200_000
     ak, Lk, tk, sk = T.lite_records(k, t_id)
 

@@ -215,6 +215,14 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
             CHECK(pb.view(i, 1) == single[i].message_type && pb.view(i, 2) == single[i].message_id &&
                   pb.view(i, 3) == single[i].payload && pb.view(i, 4) == single[i].headers);
     }
+    {  // the same batch from registered (page-locked) memory: decoded in place, same results
+        std::vector<uint8_t> reg(all.begin(), all.end());
+        reg.resize(reg.size() + 4096);
+        host_register(reg.data(), reg.size());
+        const auto rb = MessageParser::parse_batch(reg.data(), off.data(), cases.size());
+        host_unregister(reg.data());
+        for (size_t i = 0; i < cases.size(); ++i) CHECK(same(rb[i], single[i]));
+    }
     size_t visited = 0;
     pb.for_each([&](size_t i, const ParseResult& r) {
         CHECK(i == visited && same(r, single[i]));

@@ -245,8 +245,42 @@ def ref():
         L.ref_lite_encode.argtypes = [ctypes.c_uint32, vp, vp, ctypes.c_uint32, u64, vp, u64, vp]
         L.ref_lite_decode.argtypes = [vp, u64, vp, vp, vp, vp]
         L.ref_publish_topic.argtypes = [vp, vp, u64, vp, u64, vp]
+        L.ref_tm_encode_batch.argtypes = [vp, vp, vp, u64, i, vp, vp, vp, i]
         _ref = L
     return _ref
+
+
+def ref_encode_batch(arena, str_len, ts, wire=False, nthreads=1):
+    """The reference's own flyweight sequence of SBEEncoder::encode_topic_message
+    (src/sbe_encoder.cpp:141-164) over a packed batch (oracle/_ref, ref_tm_encode_batch), OpenMP
+    over nthreads.  Returns (out bytes, out_off)."""
+    run, out, out_off = ref_encode_prepared(arena, str_len, ts, wire)
+    run(nthreads)
+    return out[: int(out_off[-1])], out_off
+
+
+def ref_encode_prepared(arena, str_len, ts, wire=False):
+    """ref_encode_batch with its arrays made once: returns (run(nthreads), out, out_off), run()
+    encoding the batch into out again (timing loops)."""
+    L = np.ascontiguousarray(str_len, dtype=np.uint32).reshape(-1, 5)
+    n = L.shape[0]
+    sizes = L.sum(axis=1, dtype=np.uint64)
+    in_off = np.zeros(n + 1, np.uint64)
+    np.cumsum(sizes, out=in_off[1:])
+    out_off = np.zeros(n + 1, np.uint64)
+    np.cumsum(sizes + (34 if wire else 26), out=out_off[1:])
+    out = np.zeros(int(out_off[-1]) + 16, np.uint8)
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    ts = np.ascontiguousarray(ts, dtype=np.uint64)
+    lib = ref()
+
+    def run(nthreads):
+        bad = lib.ref_tm_encode_batch(arena.ctypes.data, L.ctypes.data, ts.ctypes.data, n, 1 if wire else 0,
+                                      out.ctypes.data, out_off.ctypes.data, in_off.ctypes.data, int(nthreads))
+        if bad:
+            raise RuntimeError(f"reference encode failed on {bad} records")
+
+    return run, out, out_off
 
 
 def ref_encode(fields, ts, wire):

@@ -2,6 +2,8 @@
 batch encoded whole and as the 8 shard_range shards an 8-GPU node would encode; the shards'
 streams concatenate (what the gather assembles) to exactly the single-batch stream, and sampled
 records match the oracle.  Plus sbe_gather_encoded on a one-rank RCCL communicator."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -92,3 +94,23 @@ def test_gather_one_rank_communicator(codec):
             codec.gather_encoded(comm, enc.out, enc.out_off[:n], n, root=0, dst=dst, dst_off=dst_off)
     finally:
         comm.close()
+
+
+def test_bench_gather_verifier_catches_a_bad_byte(codec):
+    """bench.py's config-5 gather check (verify_gathered) on a one-GPU stand-in for the root's
+    gathered stream: clean → no mismatch; one flipped byte or one wrong offset → that chunk."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    dev = torch.device("cuda")
+    N = 3_000_000
+    arena, L, ts = T.config5_shard(0, N, dev)
+    enc = codec.encode_topic_batch(arena, L, ts)
+    ws = codec.alloc_workspace(1 << 20, dev)
+    dst, dst_off = enc.out, enc.out_off
+    assert bench.verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 20)["mismatched_chunks"] == 0
+    dst[256 * 2_500_000 + 77] ^= 1
+    assert bench.verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 20)["mismatched_chunks"] == 1
+    dst[256 * 2_500_000 + 77] ^= 1
+    dst_off[5] += 1
+    assert bench.verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 20)["mismatched_chunks"] == 1

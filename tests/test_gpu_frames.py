@@ -6,7 +6,7 @@ import pytest
 import torch
 
 import sbe_testlib as T
-from test_gpu_parity import assert_same_decode, gpu_decode, to_dev
+from test_gpu_parity import SHAPES, assert_same_decode, gpu_decode, shape, to_dev  # noqa: F401 (fixture)
 
 pytestmark = pytest.mark.gpu
 
@@ -135,12 +135,13 @@ def lite_decode_records():
     return recs
 
 
-def test_lite_decode_edges_every_alignment(codec):
+def test_lite_decode_edges_every_alignment(codec, shape):
     base = lite_decode_records()
     for shift in range(16):
         recs = [bytes(shift)] + base if shift else base
         data, off = T.pack_records(recs)
-        assert_same_decode(gpu_decode(codec, data, off, T.DEC_LITE), T.oracle_decode(data, off, T.DEC_LITE))
+        assert_same_decode(gpu_decode(codec, data, off, T.DEC_LITE, in_bytes=shape),
+                           T.oracle_decode(data, off, T.DEC_LITE))
 
 
 @pytest.mark.parametrize("t", [301, 202])

@@ -31,10 +31,20 @@ def gpu_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
     return out, off, enc.status.cpu().numpy()
 
 
-def gpu_decode(codec, data, rec_off, mode):
+# the two decode kernel shapes (16 KiB windows; 12 KiB windows for records over 256 B on average,
+# chosen by sbe_decode_batch_sized): in_bytes 0 selects the first, a huge value the second
+SHAPES = {"w16k": 0, "w12k": 1 << 62}
+
+
+@pytest.fixture(params=list(SHAPES))
+def shape(request):
+    return SHAPES[request.param]
+
+
+def gpu_decode(codec, data, rec_off, mode, in_bytes=0):
     d = to_dev(data if data.size else np.zeros(16, np.uint8), torch.uint8)
     r = to_dev(np.asarray(rec_off, np.uint64), torch.int64)
-    dec = codec.decode_batch(d, r, mode=mode)
+    dec = codec.decode_batch(d, r, mode=mode, in_bytes=in_bytes)
     torch.cuda.synchronize()
     return dec.numpy()
 
@@ -195,20 +205,20 @@ def test_encode_empty_batch(codec):
 
 
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
-def test_decode_edges(codec, mode):
+def test_decode_edges(codec, shape, mode):
     recs = [r for _, r in T.edge_records()]
     data, off = T.pack_records(recs)
-    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+    assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
 
 
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
-def test_decode_edges_every_alignment(codec, mode):
+def test_decode_edges_every_alignment(codec, shape, mode):
     # the same records behind 0..15 bytes of lead-in, so each one starts at every offset mod 16
     recs = [r for _, r in T.edge_records()]
     for lead in range(16):
         allr = [b"\0" * lead] + recs
         data, off = T.pack_records(allr)
-        assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+        assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
 
 
 def seq_key_records():
@@ -242,14 +252,14 @@ def seq_key_records():
 
 
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
-def test_decode_seq_key_positions(codec, mode):
+def test_decode_seq_key_positions(codec, shape, mode):
     recs = seq_key_records()
     for lead in (0, 1, 2, 3, 5, 9, 14):
         data, off = T.pack_records([b"\0" * lead] + recs)
         exp = T.oracle_decode(data, off, mode)
         if mode == T.DEC_PARSE:
             assert 100 < int((exp["flags"] & T.FL_SEQ_KEY != 0).sum()) < len(recs)
-        assert_same_decode(gpu_decode(codec, data, off, mode), exp)
+        assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), exp)
 
 
 def long_seq_key_records(seed):
@@ -282,23 +292,23 @@ def long_seq_key_records(seed):
 
 
 @pytest.mark.parametrize("seed", [1, 2])
-def test_decode_seq_key_long_payloads(codec, seed):
+def test_decode_seq_key_long_payloads(codec, shape, seed):
     recs = long_seq_key_records(seed)
     for lead in (0, 3, 8):
         data, off = T.pack_records([b"\0" * lead] + recs)
         exp = T.oracle_decode(data, off, T.DEC_PARSE)
         assert 100 < int((exp["flags"] & T.FL_SEQ_KEY != 0).sum()) < len(recs)
-        assert_same_decode(gpu_decode(codec, data, off, T.DEC_PARSE), exp)
+        assert_same_decode(gpu_decode(codec, data, off, T.DEC_PARSE, in_bytes=shape), exp)
 
 
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
-def test_decode_mixed(codec, mode):
+def test_decode_mixed(codec, shape, mode):
     data, off = T.mixed_records(50000)
-    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+    assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
 
 
 @pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
-def test_decode_large_records(codec, mode):
+def test_decode_large_records(codec, shape, mode):
     # records far larger than the 16 KiB LDS window (global-memory read path)
     rng = np.random.default_rng(11)
     recs = []
@@ -308,7 +318,7 @@ def test_decode_large_records(codec, mode):
         recs.append(r if k % 4 else r + b"\0" * 8)
         recs.append(T.ack_wire(f[0][:500], f[1][:300], f[2][:70], k) + b"\0" * (k % 9))
     data, off = T.pack_records(recs)
-    assert_same_decode(gpu_decode(codec, data, off, mode), T.oracle_decode(data, off, mode))
+    assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
 
 
 @pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
