@@ -189,12 +189,6 @@ __device__ __forceinline__ void dst_store(T* p, T v) {
 #ifndef SBE_ENC_RPT
 #define SBE_ENC_RPT 32
 #endif
-#ifndef SBE_NO_RECLANE  // A/B: every window through the chunk-owner passes (pack_window)
-#define SBE_NO_RECLANE 0
-#endif
-#ifndef SBE_CR_B64  // record-lane composition: source dwords as ds_read_b64 pairs
-#define SBE_CR_B64 0
-#endif
 constexpr int kSbRec = 2 * 64 * SBE_ENC_RPT;          // records per superblock (one K1 workgroup): 128 tiles
 constexpr int kSbThreads = 1024;
 constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
@@ -209,9 +203,6 @@ static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt
 //   LayTMS  SessionMessageHeader + TopicMessage  src/session_manager.cpp:936-967, :1118-1144
 //   LayL2   CommitOffsetLite (301)           include/model/CommitOffsetLite.h:114-118
 //   LayL3   OrderRequestLite / OrderNotificationLite (201 / 202)  OrderRequestLite.h:114-118
-#ifndef SBE_TM_STORE_ROWS0  // window store rows of the 3- and 5-string layouts issued unconditionally
-#define SBE_TM_STORE_ROWS0 8
-#endif
 template <int kPre_, int kBlk_, int kNF_, bool kTM_>
 struct Lay {
     static constexpr int32_t kPre = kPre_;
@@ -224,7 +215,7 @@ struct Lay {
     static constexpr int32_t ovh(bool trunc) { return kOvh - (trunc ? 8 : 0); }
     // window store rows issued unconditionally (store_window): CommitOffsetLite's 32-record tiles
     // (~77-B records) are ~2.5 KiB, three of the eight 1-KiB rows
-    static constexpr int kStoreRows0 = kNF == 2 ? 3 : SBE_TM_STORE_ROWS0;
+    static constexpr int kStoreRows0 = kNF == 2 ? 3 : 8;
 };
 using LayTM = Lay<0, 16, 5, true>;
 using LayTMS = Lay<32, 16, 5, true>;
@@ -1308,32 +1299,9 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
 // bytes always belong to that record, string bytes starting >= 26 B in): zone of the chunk's
 // first byte, five LDS dword reads and four v_alignbyte, later zones merged over the tail where a
 // string starts inside the chunk; then the record's literal bytes (session / SBE header, fixed
-// block, u16 lengths) as byte stores.  No record table, no walk: every lane works from its own
-// record's registers.
+// block, u16 lengths), split over the record's two lanes.  No record table, no walk: every lane
+// works from its own record's registers.
 static_assert(kLpr == 2, "record-lane composition splits a record between two lanes");
-
-// N literal bytes (N / 4 dwords w) at window position x: the 0..3 bytes up to the first 4-aligned
-// position and the 0..3 after the last whole dword as byte stores, the rest as dword stores of the
-// realigned words (a 4-aligned dword never crosses a padded 256-byte row)
-template <int N>
-__device__ __forceinline__ void put_lit(lds_u8* wout, int32_t x, const uint32_t* w) {
-    static_assert(N % 4 == 0, "literal prefixes are whole dwords");
-    const uint32_t a = (uint32_t)(-x) & 3u;  // bytes before the first 4-aligned position
-#pragma unroll
-    for (uint32_t j = 0; j < 3; ++j)
-        if (j < a) wout[wout_addr(x + (int32_t)j)] = (uint8_t)(w[0] >> (8 * j));
-    const int32_t xa = x + (int32_t)a;
-#pragma unroll
-    for (int k = 0; k < N / 4; ++k) {
-        if (k == N / 4 - 1 && a != 0) break;
-        const uint32_t v = a ? __builtin_amdgcn_alignbyte(w[k + 1 < N / 4 ? k + 1 : k], w[k], a) : w[k];
-        *reinterpret_cast<lds_u32*>(wout + wout_addr(xa + 4 * k)) = v;
-    }
-#pragma unroll
-    for (uint32_t t = 0; t < 3; ++t)  // bytes a + 4 (N/4 - 1) + t of the prefix, from its last dword
-        if (a != 0 && t < 4 - a)
-            wout[wout_addr(x + N - 4 + (int32_t)(a + t))] = (uint8_t)(w[N / 4 - 1] >> (8 * (a + t)));
-}
 
 template <class LY>
 __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, lds_i32* rt,
@@ -1432,23 +1400,9 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
             u[k] = bsrc0 + X - 2 * f;
             int32_t i = u[k] >> 2;
             i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
-#if SBE_CR_B64
-            // three 8-byte reads from the even dword at or below i (fewer LDS instructions, 64 banks)
-            {
-                const lds_cu32x2* q2 = reinterpret_cast<lds_cu32x2*>(reinterpret_cast<lds_cu32*>(inb) + (i & ~1));
-                const u32x2 e0 = q2[0], e1 = q2[1], e2 = q2[2];
-                const bool odd = (i & 1) != 0;
-                d[k][0] = odd ? e0.y : e0.x;
-                d[k][1] = odd ? e1.x : e0.y;
-                d[k][2] = odd ? e1.y : e1.x;
-                d[k][3] = odd ? e2.x : e1.y;
-                d[k][4] = odd ? e2.y : e2.x;
-            }
-#else
             lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
 #pragma unroll
             for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
-#endif
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
@@ -1485,38 +1439,55 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     I.term = ea.term_id;
     I.sess = ea.sess_id;
     I.tmpl = ea.tmpl;
-    if (q == 0) {
-        uint32_t w[LY::kLit / 4];
+    // The literal bytes split over the record's two lanes, one instruction stream for both (no
+    // divergent header / lengths branches): lane q writes half of the header's aligned dwords (q = 0
+    // the bytes before the first aligned one, q = 1 those after the last) and the lengths of fields
+    // f = 2k + q, each as one ds_write_b16 where it is 2-aligned.
+    {
+        constexpr int kW = LY::kLit / 4, kH = (kW + 1) / 2;
+        uint32_t w[kW];
 #pragma unroll
-        for (int j = 0; j < LY::kLit / 4; ++j) w[j] = lit_word_v<LY>(I, j);
-        if ((rw & 15) == 0) {
-            // a 16-aligned record (fixed-size records of a 16-multiple): its whole literal chunks
-            // as ds_write_b128, the rest as one b64 / b32 (chunks never cross a padded row)
+        for (int j = 0; j < kW; ++j) w[j] = lit_word_v<LY>(I, j);
+        const uint32_t a = (uint32_t)(-rw) & 3u;  // header bytes before the first 4-aligned position
+        const int32_t xa = rw + (int32_t)a;
+        const int nA = a ? kW - 1 : kW;            // whole aligned dwords of the header
+        // dword k of the aligned run (k compile-time per unrolled step, lane-dependent by q)
 #pragma unroll
-            for (int c = 0; c < LY::kLit / 16; ++c) {
-                i32x4 v4;
-                v4.x = (int32_t)w[4 * c];
-                v4.y = (int32_t)w[4 * c + 1];
-                v4.z = (int32_t)w[4 * c + 2];
-                v4.w = (int32_t)w[4 * c + 3];
-                *reinterpret_cast<lds_i32x4*>(wout + wout_addr(rw + 16 * c)) = v4;
-            }
-            constexpr int kT = (LY::kLit % 16) / 4, kB = LY::kLit / 16 * 4;  // tail dwords, first tail dword
-            lds_u8* const t = wout + wout_addr(rw + 4 * kB);
-            if (kT >= 2)
-                *reinterpret_cast<lds_u64*>(t) = (uint64_t)w[kB] | ((uint64_t)w[kB + 1 < LY::kLit / 4 ? kB + 1 : kB] << 32);
-            if (kT == 1 || kT == 3)
-                *reinterpret_cast<lds_u32*>(t + 4 * (kT - 1)) = w[kB + kT - 1 < LY::kLit / 4 ? kB + kT - 1 : 0];
-        } else {
-            put_lit<LY::kLit>(wout, rw, w);
+        for (int k = 0; k < kH; ++k) {
+            const int kk = q ? kH + k : k;
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < kW; ++j)
+                if (j == kk) v = a ? __builtin_amdgcn_alignbyte(w[j + 1 < kW ? j + 1 : j], w[j], a) : w[j];
+            if (kk < nA) *reinterpret_cast<lds_u32*>(wout + wout_addr(xa + 4 * kk)) = v;
         }
-    } else {
+        if (a) {  // q = 0: the a bytes before the run; q = 1: the 4 - a bytes after it
+            const uint32_t src = q ? w[kW - 1] : w[0];
+            const int32_t x0 = q ? rw + LY::kLit - 4 + (int32_t)a : rw;
+            const uint32_t sh0 = q ? a : 0u, cnt = q ? 4u - a : a;
 #pragma unroll
-        for (int f = 0; f < LY::kNF; ++f) {
-            const int32_t P = f == 0 ? LY::kLit : zs[f - 1] - 2;
-            const uint32_t L = S.L[f];
-            if (P < rl) wout[wout_addr(rw + P)] = (uint8_t)L;
-            if (P + 1 < rl) wout[wout_addr(rw + P + 1)] = (uint8_t)(L >> 8);
+            for (uint32_t t = 0; t < 3; ++t)
+                if (t < cnt) wout[wout_addr(x0 + (int32_t)t)] = (uint8_t)(src >> (8 * (sh0 + t)));
+        }
+#pragma unroll
+        for (int k = 0; k < (LY::kNF + 1) / 2; ++k) {
+            const int f = 2 * k + q;
+            if (f >= LY::kNF) continue;
+            int32_t P = LY::kLit;
+            uint32_t L = S.L[0];
+#pragma unroll
+            for (int g = 1; g < LY::kNF; ++g)
+                if (g == f) {
+                    P = zs[g - 1] - 2;
+                    L = S.L[g];
+                }
+            const int32_t X = rw + P;
+            if (P + 1 < rl && ((X & 1) == 0)) {
+                *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wout + wout_addr(X)) = (uint16_t)L;
+            } else {
+                if (P < rl) wout[wout_addr(X)] = (uint8_t)L;
+                if (P + 1 < rl) wout[wout_addr(X + 1)] = (uint8_t)(L >> 8);
+            }
         }
     }
     return true;
@@ -1615,7 +1586,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         // current window (fast) or the whole tile window by window
         if (fast) {
-            if (SBE_NO_RECLANE || !compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
+            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
             wsync();
             store_window<LY::kStoreRows0>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,

@@ -73,8 +73,8 @@ def build(name):
     os.makedirs(OUT, exist_ok=True)
     try:
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                               tmp, "-o", os.path.join(OUT, f"{name}.so"), "-L/opt/rocm/lib", "-lrccl",
-                               "-Wl,-rpath,/opt/rocm/lib"])
+                               tmp, "-o", os.path.join(OUT, f"{name}.so"), "-ldl",
+                              ])
     finally:
         os.remove(tmp)
 

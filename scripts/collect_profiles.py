@@ -25,6 +25,8 @@ KERNELS = {"sbe_enc_pack<(anonymous namespace)::Lay<0, 16, 5, true>, true, 0>": 
            "sbe_enc_pack<(anonymous namespace)::Lay<0, 16, 5, true>, false, 0>": "sbe_enc_pack<plain,wire>",
            "sbe_enc_sums<(anonymous namespace)::Lay<0, 16, 5, true>, false, 0>": "sbe_enc_sums<plain,wire>",
            "sbe_decode_kernel<0u>": "sbe_decode_kernel<parse_message>",
+           "sbe_decode_kernel<0u, 16384u>": "sbe_decode_kernel<parse_message>",
+           "sbe_decode_kernel<0u, 12288u>": "sbe_decode_kernel<parse_message,wide>",
            "sbe_seqnum_kernel": "sbe_seqnum_kernel"}
 
 
