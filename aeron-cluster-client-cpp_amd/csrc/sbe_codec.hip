@@ -492,6 +492,35 @@ __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 // window, which the wave then stores with global_store_dwordx4 (1 KiB per instruction).
 constexpr int kStageRegs = (kEWIn / 16 + kWave - 1) / kWave;  // uint4 staging registers per lane
 
+// Diagnosis build only (-DSBE_PACK_PHASES, scripts/abv.py): per-wave core-clock time of the pack
+// loop's phases, read back by sbe_debug_phases.  The product build compiles the laps away.
+#ifdef SBE_PACK_PHASES
+__device__ uint64_t g_pack_phase[16384 * 8];
+struct Ph {
+    uint64_t t, acc[8];
+    __device__ void start() {
+        t = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < 8; ++k) acc[k] = 0;
+    }
+    __device__ void lap(int k) {
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ void put(int lane) {  // lane k writes phase k: a vector store
+        uint64_t v = 0;
+        for (int k = 0; k < 8; ++k) v = lane == k ? acc[k] : v;
+        if (lane < 8 && blockIdx.x < 16384) g_pack_phase[8 * blockIdx.x + lane] = v;
+    }
+};
+#else
+struct Ph {
+    __device__ void start() {}
+    __device__ void lap(int) {}
+    __device__ void put(int) {}
+};
+#endif
+
 struct TileIn {  // raw per-lane loads of one tile
     uint32_t L[5];
     uint64_t ts;      // timestamp (TopicMessage) / sequence (Lite)
@@ -774,7 +803,8 @@ __device__ __forceinline__ void compose(const EncArgs& a, lds_u8* wout, lds_cu8*
     W.flush();
 }
 
-// window chunks → HBM: 16-byte stores; the chunks holding T0 / we partially go byte by byte.
+// window chunks → HBM: 16-byte stores; the (at most two) chunks holding lo / we partially go
+// through store_edges.
 // Rows of 64 chunks [0, kRows0) are stored unconditionally; the rows after them only when the
 // window reaches them (a uniform branch).  kRows0 = all rows for layouts whose windows are usually
 // full; layouts of small records whose 32-record tiles are a few KiB (CommitOffsetLite) skip the
@@ -801,16 +831,48 @@ __device__ __forceinline__ void store_rows(uint8_t* out, lds_cu8* wout, uint64_t
         x.x = v[k].x; x.y = v[k].y; x.z = v[k].z; x.w = v[k].w;
         __builtin_amdgcn_raw_buffer_store_b128(x, rs, full ? (int)(16u * ch) : 0x7ffffff0, 0, kOutAux);
     }
-#pragma unroll
-    for (int k = 0; k < kRows0; ++k) {
-        const uint32_t ch = lane + kWave * (k0 + k);
-        if (ch >= nch || (ch >= c_lo && ch < c_hi)) continue;
-        const uint64_t g = wb + 16ull * ch;
-        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-#pragma unroll
-        for (uint32_t j = 0; j < 16; ++j)
-            if (g + j >= lo && g + j < we) out[g + j] = (uint8_t)(w4[j >> 2] >> (8 * (j & 3)));
+}
+
+typedef __attribute__((address_space(1))) uint8_t g_w8;
+typedef __attribute__((address_space(1))) uint16_t g_w16;
+typedef __attribute__((address_space(1))) uint32_t g_w32;
+
+// The window's partial chunks: lane 0 the one holding lo (bytes before lo belong to the previous
+// window or tile), lane 1 the one holding we.  Bytes [s, e) of a 16-B aligned chunk as at most
+// eight stores (byte, short, four dwords, short, byte), one instruction stream for both lanes.
+__device__ __forceinline__ void store_edges(uint8_t* out, lds_cu8* wout, uint64_t wb, uint64_t lo, uint64_t we,
+                                            uint32_t c_lo, uint32_t c_hi, int lane) {
+    const int32_t nb = (int32_t)(we - wb), lb = (int32_t)(lo - wb);
+    // head chunk c_lo - 1 (when lo is not chunk aligned), tail chunk c_hi (when we is not, and it
+    // is not the head chunk too: the head then ends at we)
+    const bool head = lane == 0 && c_lo > 0 && lb < nb;
+    const bool tail = lane == 1 && (nb & 15) != 0 && c_hi >= c_lo;
+    if (!(head || tail)) return;
+    const int32_t c = head ? (int32_t)c_lo - 1 : (int32_t)c_hi;
+    const int32_t s0 = head ? lb - 16 * c : 0;
+    const int32_t e = min(16, nb - 16 * c);
+    const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(wout + 16 * c + (c >> 4) * kRowPad);
+    auto byte_at = [&](int32_t p) { return (uint8_t)(v[p >> 2] >> (8 * (p & 3))); };
+    auto half_at = [&](int32_t p) { return (uint16_t)(v[p >> 2] >> (8 * (p & 3))); };  // p even: same dword
+    g_w8* const g = reinterpret_cast<g_w8*>(reinterpret_cast<uintptr_t>(out) + wb + 16 * (uint32_t)c);
+    int32_t p = s0;
+    if ((p & 1) && p < e) {
+        g[p] = byte_at(p);
+        ++p;
     }
+    if ((p & 2) && p + 2 <= e) {
+        *reinterpret_cast<g_w16*>(g + p) = half_at(p);
+        p += 2;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (4 * j >= p && 4 * j + 4 <= e) reinterpret_cast<g_w32*>(g)[j] = v[j];
+    int32_t p2 = max(p, e & ~3);
+    if (p2 + 2 <= e) {
+        *reinterpret_cast<g_w16*>(g + p2) = half_at(p2);
+        p2 += 2;
+    }
+    if (p2 < e) g[p2] = byte_at(p2);
 }
 
 constexpr int kStoreRows = kEW / 16 / kWave;  // rows of 64 chunks in a window
@@ -828,6 +890,7 @@ __device__ __forceinline__ void store_window(uint8_t* out, lds_cu8* wout, uint64
         if (nch > (uint32_t)(kWave * kRows0))
             store_rows<kStoreRows - kRows0>(out, wout, wb, lo, we, nch, c_lo, c_hi, rs, lane, kRows0);
     }
+    store_edges(out, wout, wb, lo, we, c_lo, c_hi, lane);
 }
 
 // ---- packed mode: chunk / fixup / literal passes ---------------------------------------------
@@ -1282,7 +1345,7 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
     // chunks per lane for this window: 1, 2, 4 or 8 (the lane's range: 16 kk = 2^lg bytes)
     const int kk = wlen <= 1024 ? 1 : wlen <= 2048 ? 2 : wlen <= 4096 ? 4 : kCpl;
     const int lg = kk == 1 ? 4 : kk == 2 ? 5 : kk == 4 ? 6 : 7;
-    static_assert(kCpl == 8, "chunk ownership sizes");
+    static_assert(kCpl == 8 || kCpl == 4, "chunk ownership sizes");
     const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);
     wsync();
     chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
@@ -1306,7 +1369,7 @@ static_assert(kLpr == 2, "record-lane composition splits a record between two la
 template <class LY>
 __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, lds_i32* rt,
                                                 const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
-                                                int lane, int ra, int rb) {
+                                                int lane, int ra, int rb, Ph& ph) {
     const int q = lane % kLpr, r = lane / kLpr;
     const bool live = S.rec_out != 0 && r >= ra && r < rb;
     const int32_t rw = (int32_t)S.rs - wrel;  // record start in the window
@@ -1428,8 +1491,10 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         reinterpret_cast<lds_i32x4*>(rt + kRecEnt * r)[1] = eb4;
     }
     wsync();
+    ph.lap(1);
     zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);
     wsync();
+    ph.lap(2);
     if (!live) return true;
     // literal bytes: q = 0 the header prefix (TopicMessage.h:221-238, :362-437), q = 1 the lengths
     // (:515-1231; a REF_TRUNCATE8 record ends 8 bytes short of the wire record, cutting trailing ones)
@@ -1547,6 +1612,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
     const uint64_t G = gridDim.x;
     uint64_t t = blockIdx.x;
     if (t >= ntiles) return;
+    Ph ph;
+    ph.start();
 
     uint64_t sb_next = 0, sp_out = 0, sp_in = 0;
     TileIn x = tile_load<LY, kPacked>(a, t, lane, sb_next);
@@ -1578,20 +1645,27 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
             fast_n = true;
         } else if (have_next) {
             Sn = tile_prepare<LY, kPacked, kLen>(a, x, tn, lane, sp_out, sp_in);
+            ph.lap(7);
             const uint64_t t2 = tn + G;
             x = tile_load<LY, kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
             fast_n = kPacked && !Sn.wrapped && !tile_big(Sn, lane);
             if (fast_n) Wn = tile_window(Sn, 0, lane, sink);
         }
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
+        ph.lap(0);
         // current window (fast) or the whole tile window by window
         if (fast) {
-            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb))
+            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb, ph)) {
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
+                ph.lap(6);
+            } else {
+                ph.lap(3);
+            }
             wsync();
-            store_window<LY::kStoreRows0>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,
+            store_window<(LY::kStoreRows0 < kStoreRows ? LY::kStoreRows0 : kStoreRows)>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,
                                           S.T0 + (int64_t)(W.wrel + W.wlen), lane);
             wsync();
+            ph.lap(4);
         } else {
             const int32_t wrel0 = -(int32_t)(S.T0 & 15);
             for (int32_t wrel = wrel0; wrel < (int32_t)S.len; wrel += kEW) {
@@ -1625,10 +1699,12 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
                 store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
                 wsync();
             }
+            ph.lap(6);
         }
         if (!have_next) break;
         if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in
         wsync();
+        ph.lap(5);
         if (!more_win) {
             S = Sn;
             tn += G;
@@ -1636,6 +1712,7 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         W = Wn;
         fast = fast_n;
     }
+    ph.put(lane);
 }
 
 #include "seqnum.hpp"
@@ -3403,6 +3480,19 @@ int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t
     hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + tot[1], tot[0]);
     return record_hip(hipGetLastError());
 }
+
+#ifdef SBE_PACK_PHASES
+// diagnosis build: the pack kernel's per-wave phase clocks (8 per workgroup, first `nwg` workgroups)
+int sbe_debug_phases(uint64_t* host, int nwg) {
+    if (nwg > 16384) nwg = 16384;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pack_phase), sizeof(uint64_t) * 8 * (size_t)nwg, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int sbe_debug_phases_clear() {
+    static uint64_t zero[16384 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pack_phase), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int sbe_profile_enable(int every) {
     if (every < 0) return SBE_EINVAL;

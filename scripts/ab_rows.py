@@ -6,8 +6,10 @@ ring), medians per (build, workload).  Every build's output is checked against t
   var     4 M variable-length TopicMessages (config 4's generator), encode + parse decode
   mixed   1 M mixed TM / Ack records (config 3), parse decode
   session 1 M session-framed fixed-256, encode + parse decode
+  lite301 / lite201  1 M CommitOffsetLite / OrderRequestLite records, encode + Lite decode
 Usage: python scripts/ab_rows.py lib1.so lib2.so ... [--work fixed,var,mixed] [--rounds R] [--steps K]"""
 import argparse
+import ctypes
 import os
 import sys
 
@@ -26,6 +28,7 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--var-records", type=int, default=4_000_000)
 ap.add_argument("--no-check", action="store_true", help="ablation builds (wrong bytes by design): skip the check")
+ap.add_argument("--phases", action="store_true", help="builds with -DSBE_PACK_PHASES: print the pack loop's phase shares")
 args = ap.parse_args()
 
 sbecodec.use_library(os.path.abspath(args.libs[0]))
@@ -49,16 +52,22 @@ def prep(kind):
         data, off = T.mixed_records(1_000_000)
         return dict(n=1_000_000, data=torch.from_numpy(data).to(dev),
                     off=torch.from_numpy(off.view(np.int64)).to(dev), enc=False)
+    if kind.startswith("lite"):
+        t_id, n = int(kind[4:]), 1_000_000
+        arena, L, tid, seq = T.lite_records(n, t_id)
+        return dict(n=n, a=torch.from_numpy(arena).to(dev), l=torch.from_numpy(L.view(np.int32)).to(dev),
+                    ti=torch.from_numpy(tid.view(np.int32)).to(dev), sq=torch.from_numpy(seq.view(np.int64)).to(dev),
+                    enc=True, session=False, lite=t_id, cap=arena.size + (20 + 2 * T.LITE_NF[t_id]) * n)
     raise SystemExit(f"unknown workload {kind}")
 
 
 works = {k: prep(k) for k in args.work.split(",")}
 for w in works.values():
     n = w["n"]
-    w["bytes"] = int(w["off"][-1]) if "off" in w else (
+    w["bytes"] = int(w["off"][-1]) if "off" in w else w["cap"] if "lite" in w else (
         int(w["l"].sum()) + n * (34 if not w["session"] else 32 + 26))
     if w["enc"]:
-        cap = int(w["l"].sum()) + 66 * n
+        cap = w.get("cap", int(w["l"].sum()) + 66 * n)
         w["out"] = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
         w["off_o"] = torch.empty(n + 1, dtype=torch.int64, device=dev)
         w["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -75,6 +84,11 @@ for rnd in range(args.rounds):
             dec = sbecodec.alloc_decoded(n, dev)
 
             def step():
+                if "lite" in w:
+                    sbecodec.encode_lite_batch(w["lite"], w["a"], w["l"], w["ti"], w["sq"], out=w["out"],
+                                               out_off=w["off_o"], status=w["st"], workspace=ws)
+                    sbecodec.decode_batch(w["out"], w["off_o"], sbecodec.DEC_LITE, out=dec, in_bytes=w["bytes"])
+                    return
                 if w["enc"]:
                     if w["session"]:
                         sbecodec.encode_session_batch(w["a"], w["l"], w["t"], 7, 8, out=w["out"], out_off=w["off_o"],
@@ -104,6 +118,17 @@ for rnd in range(args.rounds):
             res[(p, k)]["pack"] += sbecodec.profile_read(sbecodec.PROF_PACK)
             res[(p, k)]["dec"] += sbecodec.profile_read(sbecodec.PROF_DECODE)
             sbecodec.profile_enable(0)
+            if args.phases and rnd == 0 and w["enc"] and hasattr(sbecodec.lib(), "sbe_debug_phases"):
+                nwg = 16384
+                buf = np.zeros(8 * nwg, np.uint64)
+                sbecodec.lib().sbe_debug_phases(buf.ctypes.data_as(ctypes.c_void_p), nwg)
+                ph = buf.reshape(nwg, 8).astype(np.float64)
+                live = ph.sum(1) > 0
+                tot = ph[live].sum(0)
+                names = ["load+win+issue", "chunks", "fixup", "literal", "store", "stage_wr", "slow", "prepare"]
+                print(f"phases {k:8s} {os.path.basename(p):18s} waves {int(live.sum())} mean wave clk "
+                      f"{ph[live].sum(1).mean():.0f}: " + " ".join(f"{nm} {v / tot.sum():.3f}" for nm, v in zip(names, tot)),
+                      flush=True)
             del ws, dec
 for k in works:
     for p in args.libs:
