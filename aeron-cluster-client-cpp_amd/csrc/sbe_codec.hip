@@ -53,6 +53,12 @@ constexpr int kTile = 64;                 // records per workgroup (one per lane
 constexpr uint32_t kWin = SBE_DEC_WIN;
 constexpr uint32_t kWinWide = SBE_DEC_WIN_WIDE;
 constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWinWide kernel runs
+// Tiles of shorter records leave most of a 16 KiB window empty, and the window's LDS is what caps
+// the workgroups (and so the bytes in flight) per CU: batches of records up to kMidAvg / kSmallAvg
+// bytes on average take a 14 / 8 KiB window (64 records of 204 B average fill 12.8 KiB; a tile past
+// the window takes a second one, as any tile does).
+constexpr uint32_t kWinMid = 14336, kWinSmall = 8192;
+constexpr uint64_t kMidAvg = 204, kSmallAvg = 112;
 
 // ------------------------------------------------------------------------------------------
 // LDS window.  Dword i of the window lives at i ^ ((i >> 6) & 28): within each 256-B row (64
@@ -1895,6 +1901,10 @@ __device__ __forceinline__ bool has_slice(uint4 v) {
     return min(min(slice_dist(v.x), slice_dist(v.y)), min(slice_dist(v.z), slice_dist(v.w))) == 0u;
 }
 
+__device__ __forceinline__ uint32_t bs_any(uint32_t w) {  // 0x80 in some byte iff w holds a '\\' (plus noise above it)
+    const uint32_t x = w ^ 0x5c5c5c5cu;
+    return (x - 0x01010101u) & ~x;
+}
 __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte of w equal to 'q' (plus borrow noise above a hit)
     const uint32_t x = w ^ 0x71717171u;
     return (x - 0x01010101u) & ~x;
@@ -1911,11 +1921,15 @@ __device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
     for (uint32_t c = a0 >> 4; c < c1; c += 2) {
         const uint4 v0 = lds_read_chunk_raw(R.win, c);
         const uint4 v1 = c + 1 < c1 ? lds_read_chunk_raw(R.win, c + 1) : make_uint4(0, 0, 0, 0);
-        const uint32_t t0 = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w)) & 0x80808080u;
-        const uint32_t t1 = (q_bytes(v1.x) | q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
-        const uint32_t b0 = bs_bytes_exact(v0.x) | bs_bytes_exact(v0.y) | bs_bytes_exact(v0.z) | bs_bytes_exact(v0.w);
-        const uint32_t b1 = bs_bytes_exact(v1.x) | bs_bytes_exact(v1.y) | bs_bytes_exact(v1.z) | bs_bytes_exact(v1.w);
-        if (((t0 | t1) && (has_slice(v0) || has_slice(v1))) || (b0 | b1)) {
+        // any-tests (exact as "some byte matches": borrow noise only sits above a real match); the
+        // exact per-dword tests below run only for a chunk pair that holds a 'q' forming a key slice,
+        // or a backslash anywhere in its 32 bytes (the range test there decides whether it is inside
+        // the payload)
+        const uint32_t t = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w) | q_bytes(v1.x) |
+                            q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
+        const uint32_t b = (bs_any(v0.x) | bs_any(v0.y) | bs_any(v0.z) | bs_any(v0.w) | bs_any(v1.x) | bs_any(v1.y) |
+                            bs_any(v1.z) | bs_any(v1.w)) & 0x80808080u;
+        if ((t && (has_slice(v0) || has_slice(v1))) || b) {
 #pragma nounroll
             for (uint32_t k = 0; k < 8; ++k) {
                 const uint32_t A = 16 * c + 4 * k;  // window offset of an aligned dword
@@ -3127,11 +3141,20 @@ int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t 
     const dim3 grid((uint32_t)tiles), block(kWave);
     hipEvent_t e0, e1;
     prof_slot(1, &e0, &e1);
-    const bool wide = in_bytes > (uint64_t)kWideAvg * n;  // records over kWideAvg bytes on average
+    // kernel shape by the average record size (in_bytes = 0: unknown, the 16 KiB window)
+    const int shape = in_bytes > (uint64_t)kWideAvg * n   ? 1
+                      : in_bytes == 0                     ? 0
+                      : in_bytes <= (uint64_t)kSmallAvg * n ? 3
+                      : in_bytes <= (uint64_t)kMidAvg * n   ? 2
+                                                          : 0;
 #define SBE_DEC_LAUNCH(M)                                                                                  \
     do {                                                                                                   \
-        if (wide)                                                                                          \
+        if (shape == 1)                                                                                    \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinWide>), grid, block, 0, s, e0, e1, 0, a);      \
+        else if (shape == 2)                                                                               \
+            hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinMid>), grid, block, 0, s, e0, e1, 0, a);       \
+        else if (shape == 3)                                                                               \
+            hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinSmall>), grid, block, 0, s, e0, e1, 0, a);     \
         else                                                                                               \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWin>), grid, block, 0, s, e0, e1, 0, a);          \
     } while (0)

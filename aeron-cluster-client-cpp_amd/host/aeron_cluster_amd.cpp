@@ -528,7 +528,12 @@ bool page_locked(const void* p, size_t bytes) {
 }
 
 // Decode n records data[rec_off[i], rec_off[i+1]) with `mode` through the chunk pipeline.
-std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode) {
+// on_chunk(d, a, m), when given, runs on the calling thread for each chunk (records [a, a+m)) as
+// soon as its descriptors are on the host, while the later chunks are still being copied and
+// decoded: the host's work on chunk k overlaps the device's on chunk k+1.
+using ChunkFn = std::function<void(const Descriptors&, size_t, size_t)>;
+std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode,
+                                        const ChunkFn* on_chunk = nullptr) {
     auto d = std::make_shared<Descriptors>();
     d->n = n;
     if (n == 0) return d;
@@ -585,9 +590,19 @@ std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec
         hip_check(hipMemcpyAsync(hblk + k * d->chunk_bytes, db, d->chunk_bytes, hipMemcpyDeviceToHost, st), "D2H");
         P.end(sl);
         tr.lap(tr.enqueue);
+        if (on_chunk && k > 0 && !P.serial) {  // chunk k-1, while chunk k is in flight
+            hip_check(hipEventSynchronize(P.slot[(k - 1) % Pipeline::kSlots].out_done), "hipEventSynchronize");
+            tr.lap(tr.sync);
+            (*on_chunk)(*d, (k - 1) * C, std::min(n, k * C) - (k - 1) * C);
+            tr.lap(tr.finish);
+        }
     }
     c.sync_all();
     tr.lap(tr.sync);
+    if (on_chunk) {
+        (*on_chunk)(*d, (K - 1) * C, n - (K - 1) * C);
+        tr.lap(tr.finish);
+    }
     tr.done(n, K);
     return d;
 }
@@ -715,13 +730,32 @@ inline int64_t rdi64(const uint8_t* p) {
 inline int32_t rdi32(const uint8_t* p) { return (int32_t)((uint32_t)p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24)); }
 inline uint16_t rdu16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
-ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
-    ParseResult r;
+// r := the ParseResult of record i, every field rewritten; the strings are assigned in place, so a
+// reused ParseResult keeps its buffers (parse_batch into a caller's vector allocates nothing once
+// the strings have grown to the records' sizes)
+void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, size_t i) {
+    r.success = false;
+    r.error_message.clear();
+    r.message_type.clear();
+    r.message_id.clear();
+    r.payload.clear();
+    r.headers.clear();
+    r.timestamp = 0;
+    r.sequence_number = 0;
+    r.template_id = r.schema_id = r.version = r.block_length = 0;
+    r.correlation_id = r.session_id = r.leadership_term_id = 0;
+    r.leader_member_id = r.event_code = 0;
+    r.sequence_key_present = false;
     const uint8_t st = d.status(i), fl = d.flags(i);
     const uint16_t* h = d.hdr(i);
     const uint32_t* off = d.off(i);
     const uint32_t* len = d.len(i);
-    auto view = [&](int k) { return std::string(reinterpret_cast<const char*>(rec) + off[k], len[k]); };
+    struct View {  // record bytes [off[k], off[k] + len[k]), assigned into a string in place
+        const char* p;
+        uint32_t n;
+    };
+    auto view = [&](int k) { return View{reinterpret_cast<const char*>(rec) + off[k], len[k]}; };
+    auto set = [](std::string& s, View v) { s.assign(v.p, v.n); };
     auto take_hdr = [&] {
         r.block_length = h[0];
         r.template_id = h[1];
@@ -732,10 +766,10 @@ ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
     switch (st) {
         case SBE_ST_TM:  // src/sbe_encoder.cpp:1021-1135
             r.success = true;
-            r.message_type = view(1);
-            r.message_id = view(2);
-            r.payload = view(3);
-            r.headers = view(4);
+            set(r.message_type, view(1));
+            set(r.message_id, view(2));
+            set(r.payload, view(3));
+            set(r.headers, view(4));
             r.timestamp = (int64_t)d.ts(i);
             r.sequence_key_present = (fl & SBE_FL_SEQ_KEY) != 0;
             r.sequence_number = d.seq(i);  // src/sbe_encoder.cpp:1031-1125
@@ -745,9 +779,15 @@ ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
             r.success = true;
             r.message_type = "Acknowledgment";
             r.timestamp = (int64_t)d.ts(i);
-            r.message_id = (fl & SBE_FL_ID_DEFAULT) ? "ack_" + std::to_string(d.ts(i)) : view(0);
-            r.payload = (fl & SBE_FL_PAYLOAD_DEFAULT) ? std::string("SUCCESS") : view(1);
-            r.headers = view(2);
+            if (fl & SBE_FL_ID_DEFAULT)
+                r.message_id = "ack_" + std::to_string(d.ts(i));
+            else
+                set(r.message_id, view(0));
+            if (fl & SBE_FL_PAYLOAD_DEFAULT)
+                r.payload = "SUCCESS";
+            else
+                set(r.payload, view(1));
+            set(r.headers, view(2));
             take_hdr();
             break;
         case SBE_ST_SESSION_EVENT:  // src/sbe_encoder.cpp:629-644 (SessionEvent layout sbe_messages.hpp:39-50)
@@ -758,7 +798,7 @@ ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
             r.leadership_term_id = rdi64(rec + 24);
             r.leader_member_id = rdi32(rec + 32);
             r.event_code = rdi32(rec + 36);
-            r.payload = view(3);
+            set(r.payload, view(3));
             r.timestamp = 0;
             take_hdr();
             break;
@@ -788,6 +828,11 @@ ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
             break;
         default: throw std::runtime_error("sbecodec: unexpected parse status");
     }
+}
+
+ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
+    ParseResult r;
+    materialize_into(r, rec, d, i);
     return r;
 }
 
@@ -990,6 +1035,7 @@ std::string ParseResult::get_description() const {
 }
 
 bool gpu_codec_available() { return sbe_device_ready() == 1; }
+unsigned host_threads() { return Workers::get().size(); }
 
 void host_register(const void* p, std::size_t len) {
     hip_check(hipHostRegister(const_cast<void*>(p), len, hipHostRegisterDefault), "hipHostRegister");
@@ -1285,13 +1331,22 @@ bool MessageParser::is_acknowledgment_for(const std::uint8_t* data, std::size_t 
 }
 
 std::vector<ParseResult> MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
-    std::vector<ParseResult> out(n);
-    if (n == 0) return out;
-    auto d = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
-    for_ranges(n, 2048, [&](size_t x, size_t y) {
-        for (size_t i = x; i < y; ++i) out[i] = materialize(data + rec_off[i], *d, i);
-    });
+    std::vector<ParseResult> out;
+    parse_batch(data, rec_off, n, out);
     return out;
+}
+
+void MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n,
+                                std::vector<ParseResult>& out) {
+    if (out.size() != n) out.resize(n);
+    if (n == 0) return;
+    // each chunk's ParseResults are built while the next chunk is on the device
+    const ChunkFn fill = [&](const Descriptors& d, size_t a, size_t m) {
+        for_ranges(m, 1024, [&](size_t x, size_t y) {
+            for (size_t i = a + x; i < a + y; ++i) materialize_into(out[i], data + rec_off[i], d, i);
+        });
+    };
+    run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE, &fill);
 }
 
 ParsedBatch MessageParser::decode_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {

@@ -224,6 +224,11 @@ public:
 
     // Batch: records data[rec_off[i], rec_off[i+1]), ParseResults built on the host threads.
     static std::vector<ParseResult> parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
+    // The same into the caller's vector (resized to n): each ParseResult is rewritten in place and
+    // keeps its string buffers, so a caller that parses batch after batch into one vector does not
+    // allocate once the strings have grown (out[i] == parse_message(record i) either way).
+    static void parse_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n,
+                            std::vector<ParseResult>& out);
     // Batch without materialising: the device descriptors and views into `data` (valid while the
     // caller's bytes are), ParseResults built on demand.  See ParsedBatch.
     static ParsedBatch decode_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n);
@@ -405,6 +410,9 @@ std::size_t offer_batch(const EncodedBatch& batch, const OfferFn& offer);
 
 // true when a gfx950 device is usable (all entry points above need one).
 bool gpu_codec_available();
+// threads (the caller's included) that stage batches and build ParseResults: AERON_AMD_HOST_THREADS,
+// default min(16, cores)
+unsigned host_threads();
 
 // Page-locks a long-lived host buffer (e.g. an Aeron term buffer mapped from /dev/shm) for the
 // device's copy engines: batches decoded from registered (or hipHostMalloc'd) memory are copied to

@@ -223,6 +223,23 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
         host_unregister(reg.data());
         for (size_t i = 0; i < cases.size(); ++i) CHECK(same(rb[i], single[i]));
     }
+    {  // into a reused vector: the same batch, then the records in reverse order over the old
+       // results (every field of a session event / Ack / error result rewritten by another kind)
+        std::vector<ParseResult> reuse;
+        MessageParser::parse_batch(all.data(), off.data(), cases.size(), reuse);
+        CHECK(reuse.size() == cases.size());
+        for (size_t i = 0; i < cases.size(); ++i) CHECK(same(reuse[i], single[i]));
+        std::vector<uint8_t> rev;
+        std::vector<uint64_t> roff{0};
+        for (size_t k = cases.size(); k-- > 0;) {
+            rev.insert(rev.end(), all.begin() + off[k], all.begin() + off[k + 1]);
+            roff.push_back(rev.size());
+        }
+        MessageParser::parse_batch(rev.data(), roff.data(), cases.size(), reuse);
+        for (size_t i = 0; i < cases.size(); ++i) CHECK(same(reuse[i], single[cases.size() - 1 - i]));
+        MessageParser::parse_batch(all.data(), off.data(), 2, reuse);  // shrinks to n
+        CHECK(reuse.size() == 2 && same(reuse[1], single[1]));
+    }
     size_t visited = 0;
     pb.for_each([&](size_t i, const ParseResult& r) {
         CHECK(i == visited && same(r, single[i]));

@@ -31,9 +31,10 @@ def gpu_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
     return out, off, enc.status.cpu().numpy()
 
 
-# the two decode kernel shapes (16 KiB windows; 12 KiB windows for records over 256 B on average,
-# chosen by sbe_decode_batch_sized): in_bytes 0 selects the first, a huge value the second
-SHAPES = {"w16k": 0, "w12k": 1 << 62}
+# the decode kernel shapes (LDS windows of a 64-record tile, chosen by sbe_decode_batch_sized from
+# the average record size in_bytes / n): 16 KiB (in_bytes 0: unknown), 12 KiB (over 256 B), 14 KiB
+# (113..204 B), 8 KiB (up to 112 B).  Values: in_bytes for a batch of n records.
+SHAPES = {"w16k": lambda n: 0, "w12k": lambda n: 1 << 62, "w14k": lambda n: 150 * n, "w8k": lambda n: 1}
 
 
 @pytest.fixture(params=list(SHAPES))
@@ -42,6 +43,8 @@ def shape(request):
 
 
 def gpu_decode(codec, data, rec_off, mode, in_bytes=0):
+    if callable(in_bytes):  # a SHAPES entry
+        in_bytes = in_bytes(len(rec_off) - 1)
     d = to_dev(data if data.size else np.zeros(16, np.uint8), torch.uint8)
     r = to_dev(np.asarray(rec_off, np.uint64), torch.int64)
     dec = codec.decode_batch(d, r, mode=mode, in_bytes=in_bytes)
@@ -319,6 +322,34 @@ def test_decode_large_records(codec, shape, mode):
         recs.append(T.ack_wire(f[0][:500], f[1][:300], f[2][:70], k) + b"\0" * (k % 9))
     data, off = T.pack_records(recs)
     assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS])
+def test_decode_window_chains(codec, shape, mode):
+    # tiles that take many windows: records of 0.3-6 KiB (a 64-record tile spans up to ~30 windows),
+    # records larger than any window among them
+    # (parsed from HBM between staged ones), and runs of short records between long ones
+    rng = np.random.default_rng(29)
+    recs = []
+    for k in range(1500):
+        kind = k % 11
+        if kind == 0:
+            plen = int(rng.integers(16500, 20000))  # past every window
+        elif kind in (1, 2):
+            plen = int(rng.integers(0, 40))
+        else:
+            plen = int(rng.integers(300, 6000))
+        pay = rng.integers(32, 127, plen, dtype=np.uint8).tobytes()
+        if k % 13 == 0 and plen >= 16:
+            at = int(rng.integers(0, plen - 15))
+            pay = pay[:at] + b"_sequence_number" + pay[at + 16:]
+        if k % 7 == 3:
+            recs.append(T.ack_wire(pay[:200], b"orders", pay[200:240], k))
+        else:
+            recs.append(T.tm_wire([b"orders", b"T", b"u" * (k % 30), pay, b"{}"], k) + b"\0" * (k % 5))
+    for lead in (0, 7):
+        data, off = T.pack_records([b"\0" * lead] + recs)
+        assert_same_decode(gpu_decode(codec, data, off, mode, in_bytes=shape), T.oracle_decode(data, off, mode))
 
 
 @pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
