@@ -192,16 +192,9 @@ __device__ __forceinline__ void dst_store(T* p, T v) {
 //                     offsets, LDS-staged input, per-lane record composition into an LDS output
 //                     window, coalesced 16-byte stores
 // ------------------------------------------------------------------------------------------
-#ifndef SBE_ENC_RPT
-#define SBE_ENC_RPT 32
-#endif
-constexpr int kSbRec = 2 * 64 * SBE_ENC_RPT;          // records per superblock (one K1 workgroup): 128 tiles
 constexpr int kSbThreads = 1024;
-constexpr int kRpt = SBE_ENC_RPT;                     // records per K3 tile (one wave)
-constexpr int kLpr = kWave / kRpt;                    // lanes per record in K3
-constexpr int kTilesPerSb = kSbRec / kRpt;
-static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt == 0 &&
-              kTilesPerSb == 2 * kWave, "tile shape");
+constexpr int kTilesPerSb = 2 * kWave;  // tiles per superblock (one K1 workgroup)
+constexpr int kSbRecMin = kTilesPerSb * 32;  // records per superblock of the smallest tile shape
 
 // Record layouts (compile-time): kPre bytes of session header, the 8-byte SBE header, a kBlk-byte
 // fixed block, then kNF u16-length-prefixed strings.
@@ -209,8 +202,18 @@ static_assert(kWave % kRpt == 0 && kSbRec % kSbThreads == 0 && kSbThreads % kRpt
 //   LayTMS  SessionMessageHeader + TopicMessage  src/session_manager.cpp:936-967, :1118-1144
 //   LayL2   CommitOffsetLite (301)           include/model/CommitOffsetLite.h:114-118
 //   LayL3   OrderRequestLite / OrderNotificationLite (201 / 202)  OrderRequestLite.h:114-118
-template <int kPre_, int kBlk_, int kNF_, bool kTM_>
+// kRpt: records per K3 tile (one wave), kLpr = 64 / kRpt lanes per record.  32-record tiles (two
+// lanes a record) for the TopicMessage layout, whose 256-B Order records fill one 8 KiB window
+// per tile; 64-record tiles (a lane a record, chunks rebalanced over the lanes) for the session
+// frames and Lite records, whose 32-record tiles (8.8 / 2.5 / 10.4 KiB) leave windows part full:
+// measured session pack 156 -> 144 us, CommitOffsetLite 61 -> 43, OrderRequestLite 167 -> 150
+// (fixed-256 TopicMessage 90 -> 93, variable-length unchanged).
+template <int kPre_, int kBlk_, int kNF_, bool kTM_, int kRpt_>
 struct Lay {
+    static constexpr int kRpt = kRpt_;
+    static constexpr int kLpr = kWave / kRpt;
+    static constexpr int kSbRec = kTilesPerSb * kRpt;  // records per superblock
+    static_assert((kRpt == 32 || kRpt == 64) && kSbRec % kSbThreads == 0 && kSbThreads % kRpt == 0, "tile shape");
     static constexpr int32_t kPre = kPre_;
     static constexpr int32_t kBlk = kBlk_;
     static constexpr int kNF = kNF_;
@@ -221,14 +224,18 @@ struct Lay {
     static constexpr int32_t ovh(bool trunc) { return kOvh - (trunc ? 8 : 0); }
     // window store rows issued unconditionally (store_window): CommitOffsetLite's 32-record tiles
     // (~77-B records) are ~2.5 KiB, three of the eight 1-KiB rows
-    static constexpr int kStoreRows0 = kNF == 2 ? 3 : 8;
+    static constexpr int kStoreRows0 = kNF == 2 ? (kRpt == 64 ? 5 : 3) : 8;
 };
-using LayTM = Lay<0, 16, 5, true>;
-using LayTMS = Lay<32, 16, 5, true>;
-using LayL2 = Lay<0, 12, 2, false>;
-using LayL3 = Lay<0, 12, 3, false>;
+using LayTM = Lay<0, 16, 5, true, 32>;
+using LayTMS = Lay<32, 16, 5, true, 64>;
+using LayL2 = Lay<0, 12, 2, false, 64>;
+using LayL3 = Lay<0, 12, 3, false, 64>;
 static_assert(LayTM::kOvh == SBE_TM_WIRE_OVERHEAD && LayTM::ovh(true) == SBE_TM_REF_OVERHEAD, "TM layout");
 static_assert(LayL2::kOvh == SBE_LITE_OVERHEAD(2) && LayTMS::kPre == SBE_SESSION_HDR_LEN, "layouts");
+// the layout's tile shape as local constants (functions templated on the layout)
+#define SBE_TILE_SHAPE(LY)                                                  \
+    [[maybe_unused]] constexpr int kRpt = LY::kRpt, kLpr = LY::kLpr; \
+    [[maybe_unused]] constexpr int kSbRec = LY::kSbRec
 
 struct EncArgs {
     const uint8_t* arena;
@@ -290,6 +297,7 @@ __device__ __forceinline__ void rec_sizes(const EncArgs& a, uint64_t r, uint32_t
 // writes the 128 tile prefixes and the superblock's totals.
 template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
+    SBE_TILE_SHAPE(LY);
     __shared__ uint64_t tl[2][kTilesPerSb];
     const int tid = threadIdx.x;
     const uint64_t sb = blockIdx.x;
@@ -300,10 +308,9 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
         uint64_t ib;
         uint8_t st;
         rec_sizes<LY, kLen>(a, r, ob, ib, st);
-        // per tile (kRpt = 32 consecutive lanes, two tiles per wave): one DPP scan over the wave,
-        // the tiles' sums read at lanes 31 and 63 (input side in 64 bits: E109 records may carry
-        // up to 5 x 4 GiB of strings)
-        static_assert(kRpt == 32, "two tiles per wave");
+        // per tile (kRpt consecutive lanes: two 32-record tiles or one 64-record tile per wave):
+        // one DPP scan over the wave, the tiles' sums read at lanes 31 and 63 (input side in 64
+        // bits: E109 records may carry up to 5 x 4 GiB of strings)
         const int lane = tid & (kWave - 1);
         const uint32_t so = wave_incl_scan(ob, lane);
         const uint32_t o31 = lane_u32(so, 31), o63 = lane_u32(so, kWave - 1);
@@ -314,23 +321,29 @@ __global__ __launch_bounds__(kSbThreads) void sbe_enc_sums(EncArgs a) {
             i63 = lane_u64(si, kWave - 1);
         }
         if (lane == 0) {
-            const int tile = j * (kSbThreads / kRpt) + 2 * (tid / kWave);
-            tl[0][tile] = o31;
-            tl[1][tile] = i31;
-            tl[0][tile + 1] = o63 - o31;
-            tl[1][tile + 1] = i63 - i31;
+            const int tile = j * (kSbThreads / kRpt) + (kWave / kRpt) * (tid / kWave);
+            if (kRpt == 32) {
+                tl[0][tile] = o31;
+                tl[1][tile] = i31;
+                tl[0][tile + 1] = o63 - o31;
+                tl[1][tile + 1] = i63 - i31;
+            } else {
+                tl[0][tile] = o63;
+                tl[1][tile] = i63;
+            }
         }
     }
     __syncthreads();
-    if (tid < kWave) {  // exclusive scan of the 128 tile sums, two per lane
+    if (tid < kWave) {  // exclusive scan of the superblock's tile sums, kTilesPerSb / 64 per lane
         const int lane = tid;
-        const uint64_t o0 = tl[0][2 * lane], o1 = tl[0][2 * lane + 1];
-        const uint64_t i0 = tl[1][2 * lane], i1 = tl[1][2 * lane + 1];
+        constexpr int kPer = kTilesPerSb / kWave;
+        const uint64_t o0 = tl[0][kPer * lane], o1 = kPer == 2 ? tl[0][kPer * lane + 1] : 0ull;
+        const uint64_t i0 = tl[1][kPer * lane], i1 = kPer == 2 ? tl[1][kPer * lane + 1] : 0ull;
         const uint64_t io = wave_incl_scan64(o0 + o1, lane), ii = wave_incl_scan64(i0 + i1, lane);
         const uint64_t eo = io - o0 - o1, ei = ii - i0 - i1;
-        const uint64_t t0 = sb * kTilesPerSb + 2 * lane;
+        const uint64_t t0 = sb * kTilesPerSb + kPer * lane;
         *reinterpret_cast<ulonglong2*>(a.tsum + 2 * t0) = make_ulonglong2(eo, ei);
-        *reinterpret_cast<ulonglong2*>(a.tsum + 2 * t0 + 2) = make_ulonglong2(eo + o0, ei + i0);
+        if (kPer == 2) *reinterpret_cast<ulonglong2*>(a.tsum + 2 * t0 + 2) = make_ulonglong2(eo + o0, ei + i0);
         if (lane == kWave - 1) *reinterpret_cast<ulonglong2*>(a.bsum + 2 * sb) = make_ulonglong2(io, ii);
     }
 }
@@ -559,6 +572,7 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
 // increasing order; a clamped repeat of the last tile loads nothing new)
 template <class LY, bool kPacked>
 __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int lane, uint64_t& sb_next) {
+    SBE_TILE_SHAPE(LY);
     TileIn x;
     // unconditional loads at a clamped index: a select on the loaded value here would make the
     // compiler wait for it (tile_prepare applies r < n)
@@ -588,6 +602,7 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
 template <class LY, bool kPacked, int kLen>
 __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
                                                uint64_t& sp_out, uint64_t& sp_in) {
+    SBE_TILE_SHAPE(LY);
     TileSt S;
     const int q = lane % kLpr;
     const uint64_t r = tile * kRpt + lane / kLpr;
@@ -617,8 +632,8 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
     const uint32_t agg_out = lane_u32(inc_out, kWave - 1);
-    static_assert(kLpr == 2, "record lead lane via quad_perm [0,0,2,2]");
-    S.rs = dpp0<0xa0>(inc_out - lo_out);  // the lead (even) lane's value
+    // the record's lead lane's value (kLpr = 2: quad_perm [0,0,2,2])
+    S.rs = kLpr == 2 ? dpp0<0xa0>(inc_out - lo_out) : inc_out - lo_out;
     S.rec_out = rec_out;
     if (kPacked) {
         // every record of the tile encodable: input offsets follow the output ones (34 B apart
@@ -634,7 +649,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
             const uint64_t agg_in = lane_u64(inc_in, kWave - 1);
             S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
             const uint64_t ex = inc_in - lo_in;
-            S.in0 = ((uint64_t)dpp0<0xa0>((uint32_t)(ex >> 32)) << 32) | dpp0<0xa0>((uint32_t)ex);
+            S.in0 = kLpr == 2 ? ((uint64_t)dpp0<0xa0>((uint32_t)(ex >> 32)) << 32) | dpp0<0xa0>((uint32_t)ex) : ex;
         }
     } else {
         S.agg_in = 0;
@@ -684,6 +699,7 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
 template <class LY>
 __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int lane, uintptr_t& swb,
                                             int32_t& nbytes) {
+    SBE_TILE_SHAPE(LY);
     const uint32_t g = wrel > 0 ? (uint32_t)wrel : 0u;
     const int q = lane % kLpr;
     const uint64_t mine = __ballot(q == 0 && S.rec_out && S.rs <= g && g < S.rs + S.rec_out);
@@ -998,6 +1014,7 @@ template <class LY>
 __device__ __forceinline__ bool build_tables(lds_i32* rt, lds_i32* bk, uint64_t* sbase, const TileSt& S,
                                              int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb, int ra, int rb,
                                              int lg, int lane) {
+    SBE_TILE_SHAPE(LY);
     const int q = lane % kLpr, r = lane / kLpr;
     bk[lane] = ra;
     bool outside = false;
@@ -1094,8 +1111,10 @@ __device__ __forceinline__ u32x4 align4(uint32_t e0, uint32_t e1, uint32_t e2, u
 // ds_write_b128 per chunk.
 // Lane l owns the kk chunks [l kk, (l+1) kk) of the window: kk = 8 for a full window, fewer for
 // a window that carries less (kk a power of two, so a lane never straddles a padded 256-B row).
+template <class LY>
 __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* rt, lds_i32* bk, int32_t wlen,
                                            int32_t nb, int kk, int lg, int lane) {
+    SBE_TILE_SHAPE(LY);
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
@@ -1145,14 +1164,20 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
 // (chunk_pass_global composes those whole) have no items.
 template <class LY>
 __device__ __forceinline__ void zone_fixup(lds_u8* wout, lds_cu8* inb, lds_i32* rt, int32_t wlen, int32_t nb,
-                                           int lane) {
+                                           int lane, int ra, int rb) {
+    SBE_TILE_SHAPE(LY);
     const int32_t imax = (nb + kInSlack) / 4 - 5;
     constexpr int kZ = LY::kNF - 1;  // interior string starts per record (z_1 .. z_{kNF-1})
     static_assert(kZ >= 1 && kZ <= 4, "layouts have 2..5 strings");
+    // 64-record tiles: the window's records [ra, rb) only (a window holds part of a tile: fewer
+    // item passes); 32-record tiles: all of them (measured no slower than the restriction)
+    const int r0 = kRpt == 64 ? ra : 0, r1 = kRpt == 64 ? rb : kRpt;
+    const int nitems = kZ * (r1 - r0);
 #pragma unroll
     for (int i0 = 0; i0 < kZ * kRpt; i0 += kWave) {
-        const int i = i0 + lane, j = i / kZ, f = i % kZ;  // string start z_{f+1} of record j
-        if (j >= kRpt) break;
+        if (i0 >= nitems) break;
+        const int i = i0 + lane, j = r0 + i / kZ, f = i % kZ;  // string start z_{f+1} of record j
+        if (j >= r1) continue;
         const RecEnt E = rec_load(rt, j);
         const int32_t zf = f == 0 ? E.z1 : f == 1 ? E.z2 : f == 2 ? E.z3 : E.z4;
         const int32_t zp = f == 0 ? 0 : f == 1 ? E.z1 : f == 2 ? E.z2 : E.z3;
@@ -1200,6 +1225,7 @@ typedef __attribute__((address_space(3))) uint64_t lds_u64;
 template <class LY>
 __device__ __noinline__ void chunk_pass_global(lds_u8* wout, lds_i32* rt, lds_i32* bk, const lds_u64* sbase,
                                                int32_t wlen, int kk, int lg, int lane) {
+    SBE_TILE_SHAPE(LY);
     int32_t r = bk[lane];
     RecEnt E = rec_load(rt, r);
     const int32_t lb = lane << lg;
@@ -1262,6 +1288,7 @@ __device__ __forceinline__ uint32_t lit_word_v(const LitIn& I, int j) {
 // may be clipped by the window or the capacity: dword writes with byte-wise edges (rare, out of line)
 template <class LY>
 __device__ __noinline__ void literal_clip(lds_u8* wout, RecEnt E, LitIn I, int32_t wlen, int q) {
+    SBE_TILE_SHAPE(LY);
     const int32_t hi_all = E.rend < wlen ? E.rend : wlen;
     const int32_t lo_all = E.rw > 0 ? E.rw : 0;
     if (q == 0) {
@@ -1301,6 +1328,7 @@ __device__ __forceinline__ void put_b4(lds_u8* p, uint32_t v) {
 template <class LY>
 __device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, lds_i32* rt, const TileSt& S,
                                              int32_t wlen, int lane) {
+    SBE_TILE_SHAPE(LY);
     const int q = lane % kLpr, r = lane / kLpr;
     if (!S.rec_out) return;
     const RecEnt E = rec_load(rt, r);
@@ -1347,17 +1375,18 @@ __device__ __forceinline__ void literal_pass(const EncArgs& ea, lds_u8* wout, ld
 template <class LY>
 __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds_u8* inb, lds_i32* rt, lds_i32* bk,
                                             uint64_t* sbase, const TileSt& S, int32_t wrel, int32_t wlen,
-                                            uintptr_t swb, int32_t nb, int lane, int ra = 0, int rb = kRpt) {
+                                            uintptr_t swb, int32_t nb, int lane, int ra = 0, int rb = LY::kRpt) {
+    SBE_TILE_SHAPE(LY);
     // chunks per lane for this window: 1, 2, 4 or 8 (the lane's range: 16 kk = 2^lg bytes)
     const int kk = wlen <= 1024 ? 1 : wlen <= 2048 ? 2 : wlen <= 4096 ? 4 : kCpl;
     const int lg = kk == 1 ? 4 : kk == 2 ? 5 : kk == 4 ? 6 : 7;
     static_assert(kCpl == 8 || kCpl == 4, "chunk ownership sizes");
     const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);
     wsync();
-    chunk_pass(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
+    chunk_pass<LY>(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
     if (outside) chunk_pass_global<LY>(wout, rt, bk, (const lds_u64*)sbase, wlen, kk, lg, lane);
     wsync();
-    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);
+    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane, ra, rb);
     wsync();
     literal_pass<LY>(ea, wout, rt, S, wlen, lane);
 }
@@ -1370,12 +1399,11 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
 // string starts inside the chunk; then the record's literal bytes (session / SBE header, fixed
 // block, u16 lengths), split over the record's two lanes.  No record table, no walk: every lane
 // works from its own record's registers.
-static_assert(kLpr == 2, "record-lane composition splits a record between two lanes");
-
 template <class LY>
 __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, lds_i32* rt,
                                                 const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
                                                 int lane, int ra, int rb, Ph& ph) {
+    SBE_TILE_SHAPE(LY);
     const int q = lane % kLpr, r = lane / kLpr;
     const bool live = S.rec_out != 0 && r >= ra && r < rb;
     const int32_t rw = (int32_t)S.rs - wrel;  // record start in the window
@@ -1402,9 +1430,10 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         for (int f = LY::kNF; f < 5; ++f) zs[f - 1] = zs[4];
     }
     const int32_t z1 = zs[0], z2 = zs[1], z3 = zs[2], z4 = zs[3];
-    // this lane's chunks: the first (q = 0) or second half of the record's own chunks
+    // this lane's chunks: the first (q = 0) or second half of the record's own chunks (kLpr = 1:
+    // all of them)
     const int32_t c0 = (rw + 15) >> 4, nc = live ? ((rw + rl + 15) >> 4) - c0 : 0;
-    const int32_t h = (nc + 1) >> 1;
+    const int32_t h = kLpr == 2 ? (nc + 1) >> 1 : nc;
     int32_t cb = c0 + (q ? h : 0), n_mine = q ? nc - h : h;
     // the record this lane composes chunks of (its own unless rebalanced)
     int32_t brw = rw, bsrc0 = src0, bz1 = z1, bz2 = z2, bz3 = z3, bz4 = z4;
@@ -1419,8 +1448,18 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         const bool lead = q == 0 && nc > 0;
         const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
         const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
-        T = (C + (kWave - nrec) - 1) / (kWave - nrec);  // >= 1: C >= nrec >= 1
-        rebal = kGuard ? T < lane_u32(wave_incl_max((uint32_t)(n_mine > 0 ? n_mine : 0)), kWave - 1) : true;
+        // T chunks per lane: C / (64 - records) rounded up, which always fits (sum of ceil(nc_j / T)
+        // <= C / T + records); one lane a record (64-record tiles): ceil(C / 64) first, when the
+        // records' runs of ceil(nc / T) lanes fit the wave (records of equal lengths: every lane
+        // busy); no spare lane: no rebalance
+        uint32_t U0 = ~0u, T0 = 0;
+        if (kLpr == 1) {
+            T0 = (C + kWave - 1) / kWave;
+            U0 = lane_u32(wave_incl_scan(lead ? ((uint32_t)nc + T0 - 1) / T0 : 0u, lane), kWave - 1);
+        }
+        T = U0 <= (uint32_t)kWave ? T0 : (nrec < (uint32_t)kWave ? (C + (kWave - nrec) - 1) / (kWave - nrec) : 0u);
+        const uint32_t mx = lane_u32(wave_incl_max((uint32_t)(n_mine > 0 ? n_mine : 0)), kWave - 1);
+        rebal = T != 0 && (kGuard ? T < mx : true);
     }
     if (rebal) {
         // records of unequal lengths (variable-length records, or one long record): two lanes per
@@ -1498,7 +1537,7 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     }
     wsync();
     ph.lap(1);
-    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);
+    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane, ra, rb);
     wsync();
     ph.lap(2);
     if (!live) return true;
@@ -1511,38 +1550,39 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     I.sess = ea.sess_id;
     I.tmpl = ea.tmpl;
     // The literal bytes split over the record's two lanes, one instruction stream for both (no
-    // divergent header / lengths branches): lane q writes half of the header's aligned dwords (q = 0
-    // the bytes before the first aligned one, q = 1 those after the last) and the lengths of fields
-    // f = 2k + q, each as one ds_write_b16 where it is 2-aligned.
-    {
-        constexpr int kW = LY::kLit / 4, kH = (kW + 1) / 2;
-        uint32_t w[kW];
+    // divergent header / lengths branches): part p = q writes half of the header's aligned dwords
+    // (p = 0 the bytes before the first aligned one, p = 1 those after the last) and the lengths
+    // of fields f = 2k + p, each as one ds_write_b16 where it is 2-aligned.  kLpr = 1: the
+    // record's lane writes both parts.
+    constexpr int kW = LY::kLit / 4, kH = (kW + 1) / 2;
+    uint32_t w[kW];
 #pragma unroll
-        for (int j = 0; j < kW; ++j) w[j] = lit_word_v<LY>(I, j);
-        const uint32_t a = (uint32_t)(-rw) & 3u;  // header bytes before the first 4-aligned position
-        const int32_t xa = rw + (int32_t)a;
-        const int nA = a ? kW - 1 : kW;            // whole aligned dwords of the header
-        // dword k of the aligned run (k compile-time per unrolled step, lane-dependent by q)
+    for (int j = 0; j < kW; ++j) w[j] = lit_word_v<LY>(I, j);
+    const uint32_t a = (uint32_t)(-rw) & 3u;  // header bytes before the first 4-aligned position
+    const int32_t xa = rw + (int32_t)a;
+    const int nA = a ? kW - 1 : kW;            // whole aligned dwords of the header
+    auto part = [&](int p) {
+        // dword k of the aligned run (k compile-time per unrolled step, lane-dependent by p)
 #pragma unroll
         for (int k = 0; k < kH; ++k) {
-            const int kk = q ? kH + k : k;
+            const int kk = p ? kH + k : k;
             uint32_t v = 0;
 #pragma unroll
             for (int j = 0; j < kW; ++j)
                 if (j == kk) v = a ? __builtin_amdgcn_alignbyte(w[j + 1 < kW ? j + 1 : j], w[j], a) : w[j];
             if (kk < nA) *reinterpret_cast<lds_u32*>(wout + wout_addr(xa + 4 * kk)) = v;
         }
-        if (a) {  // q = 0: the a bytes before the run; q = 1: the 4 - a bytes after it
-            const uint32_t src = q ? w[kW - 1] : w[0];
-            const int32_t x0 = q ? rw + LY::kLit - 4 + (int32_t)a : rw;
-            const uint32_t sh0 = q ? a : 0u, cnt = q ? 4u - a : a;
+        if (a) {  // p = 0: the a bytes before the run; p = 1: the 4 - a bytes after it
+            const uint32_t src = p ? w[kW - 1] : w[0];
+            const int32_t x0 = p ? rw + LY::kLit - 4 + (int32_t)a : rw;
+            const uint32_t sh0 = p ? a : 0u, cnt = p ? 4u - a : a;
 #pragma unroll
             for (uint32_t t = 0; t < 3; ++t)
                 if (t < cnt) wout[wout_addr(x0 + (int32_t)t)] = (uint8_t)(src >> (8 * (sh0 + t)));
         }
 #pragma unroll
         for (int k = 0; k < (LY::kNF + 1) / 2; ++k) {
-            const int f = 2 * k + q;
+            const int f = 2 * k + p;
             if (f >= LY::kNF) continue;
             int32_t P = LY::kLit;
             uint32_t L = S.L[0];
@@ -1560,6 +1600,12 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
                 if (P + 1 < rl) wout[wout_addr(X + 1)] = (uint8_t)(L >> 8);
             }
         }
+    };
+    if (kLpr == 2) {
+        part(q);
+    } else {
+        part(0);
+        part(1);
     }
     return true;
 }
@@ -1577,11 +1623,15 @@ struct Win {
     int32_t nb;
 };
 
+template <class LY>
 __device__ __forceinline__ bool tile_big(const TileSt& S, int lane) {
+    SBE_TILE_SHAPE(LY);
     return __ballot(lane % kLpr == 0 && S.rec_out > (uint32_t)(kEW - 16)) != 0;
 }
 
+template <class LY>
 __device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, uintptr_t sink) {
+    SBE_TILE_SHAPE(LY);
     Win W;
     const int q = lane % kLpr, r = lane / kLpr;
     W.ra = ra;
@@ -1604,6 +1654,7 @@ __device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, ui
 
 template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
+    SBE_TILE_SHAPE(LY);
     __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
     __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
     __shared__ __attribute__((aligned(16))) int32_t rt_arr[kPacked ? kRpt * kRecEnt : 4];
@@ -1627,8 +1678,8 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
     uint4 I[kStageRegs];
     const uintptr_t sink = reinterpret_cast<uintptr_t>(a.sink);
     Win W{0, kRpt, 0, 0, 0, sink, 0};
-    bool fast = kPacked && !S.wrapped && !tile_big(S, lane);
-    if (fast) W = tile_window(S, 0, lane, sink);
+    bool fast = kPacked && !S.wrapped && !tile_big<LY>(S, lane);
+    if (fast) W = tile_window<LY>(S, 0, lane, sink);
     if (kPacked) {
         stage_issue(W.swb, W.nb, lane, I);
         stage_write(win_in, W.nb, lane, I);
@@ -1647,15 +1698,15 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         Win Wn{0, kRpt, 0, 0, 0, sink, 0};
         bool fast_n = false;
         if (more_win) {
-            Wn = tile_window(S, W.rb, lane, sink);
+            Wn = tile_window<LY>(S, W.rb, lane, sink);
             fast_n = true;
         } else if (have_next) {
             Sn = tile_prepare<LY, kPacked, kLen>(a, x, tn, lane, sp_out, sp_in);
             ph.lap(7);
             const uint64_t t2 = tn + G;
             x = tile_load<LY, kPacked>(a, t2 < ntiles ? t2 : ntiles - 1, lane, sb_next);
-            fast_n = kPacked && !Sn.wrapped && !tile_big(Sn, lane);
-            if (fast_n) Wn = tile_window(Sn, 0, lane, sink);
+            fast_n = kPacked && !Sn.wrapped && !tile_big<LY>(Sn, lane);
+            if (fast_n) Wn = tile_window<LY>(Sn, 0, lane, sink);
         }
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         ph.lap(0);
@@ -2983,8 +3034,8 @@ struct EncReq {
     int64_t term_id, sess_id;
 };
 
-size_t enc_workspace_size(uint64_t n) {
-    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
+size_t enc_workspace_size(uint64_t n) {  // the smallest tile shape's (the most tiles)
+    const uint64_t sbs = (n + kSbRecMin - 1) / kSbRecMin;
     const uint64_t tiles = sbs * kTilesPerSb;
     return (size_t)(16 * (tiles + sbs) + kSinkBytes + 16);
 }
@@ -3011,8 +3062,8 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
     if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
     if (!q.str_len || !q.ts || !q.arena || !out) return SBE_EINVAL;
     if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
-    const uint64_t sbs = (n + kSbRec - 1) / kSbRec;
-    const uint64_t tiles = (n + kRpt - 1) / kRpt;
+    const uint64_t sbs = (n + LY::kSbRec - 1) / LY::kSbRec;
+    const uint64_t tiles = (n + LY::kRpt - 1) / LY::kRpt;
     if (tiles > kMaxTiles) return SBE_EINVAL;
     if (!workspace || workspace_bytes < enc_workspace_size(n)) return SBE_ENOSPC;
     if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
