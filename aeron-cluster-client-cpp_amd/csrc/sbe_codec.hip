@@ -2812,16 +2812,24 @@ __global__ __launch_bounds__(kFsThreads) void frag_reduce(FragArgs a, FragScan* 
     const FragScan tot = fs_block(a, b, e, wt, before);
     if (threadIdx.x == 0) agg[b] = tot;
 }
-// exclusive prefixes of the nb block aggregates, in place
-constexpr int kFsbThreads = 1024;  // one workgroup: a million fragments' 977 aggregates in one pass
+// exclusive prefixes of the nb block aggregates, in place: one workgroup of kFsThreads threads,
+// kFsPer consecutive aggregates a thread (a million fragments' 977 aggregates in one pass; at 1024
+// threads a pass the scan's registers spilled: 21 us instead of a few)
+constexpr int kFsbThreads = kFsThreads;
 __global__ __launch_bounds__(kFsbThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb) {
     __shared__ FragScan wt[kFsbThreads / kWave];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
     FragScan carry = fs_identity();
-    for (uint64_t c0 = 0; c0 < nb; c0 += kFsbThreads) {
-        const uint64_t j = c0 + (uint64_t)tid;
-        const FragScan v = j < nb ? agg[j] : fs_identity();
-        const FragScan inc = fs_wave_scan(v, lane);
+    for (uint64_t c0 = 0; c0 < nb; c0 += kFsBlk) {
+        const uint64_t j0 = c0 + (uint64_t)tid * kFsPer;
+        FragScan e[kFsPer];
+#pragma unroll
+        for (int k = 0; k < kFsPer; ++k) e[k] = j0 + k < nb ? agg[j0 + k] : fs_identity();
+        FragScan r[kFsPer];  // thread-inclusive
+        r[0] = e[0];
+#pragma unroll
+        for (int k = 1; k < kFsPer; ++k) r[k] = FragScanOp{}(r[k - 1], e[k]);
+        const FragScan inc = fs_wave_scan(r[kFsPer - 1], lane);
         const FragScan up = fs_shfl_up(inc, 1);
         const FragScan ex = lane ? up : fs_identity();
         __syncthreads();
@@ -2833,7 +2841,10 @@ __global__ __launch_bounds__(kFsbThreads) void frag_scan_blocks(FragScan* agg, u
             if (k < w) wpre = FragScanOp{}(wpre, wt[k]);
             tot = FragScanOp{}(tot, wt[k]);
         }
-        if (j < nb) agg[j] = FragScanOp{}(carry, FragScanOp{}(wpre, ex));
+        const FragScan P = FragScanOp{}(carry, FragScanOp{}(wpre, ex));  // before this thread's first
+#pragma unroll
+        for (int k = 0; k < kFsPer; ++k)
+            if (j0 + k < nb) agg[j0 + k] = k ? FragScanOp{}(P, r[k - 1]) : P;
         carry = FragScanOp{}(carry, tot);
     }
 }

@@ -12,8 +12,10 @@ import sys
 
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
-    name = re.sub(r"Lay<0, 16, 5, true>", "TM", name)
-    name = re.sub(r"Lay<32, 16, 5, true>", "TMS", name)
+    name = re.sub(r"Lay<0, 16, 5, true(, \d+)?>", "TM", name)
+    name = re.sub(r"Lay<32, 16, 5, true(, \d+)?>", "TMS", name)
+    name = re.sub(r"Lay<0, 12, 2, false(, \d+)?>", "L2", name)
+    name = re.sub(r"Lay<0, 12, 3, false(, \d+)?>", "L3", name)
     name = re.sub(r"\(.*\)$", "", name)
     return name.replace("void ", "")
 
