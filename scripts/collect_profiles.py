@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -27,10 +28,13 @@ KERNELS = {"sbe_enc_pack<(anonymous namespace)::Lay<0, 16, 5, true>, true, 0>": 
            "sbe_decode_kernel<0u>": "sbe_decode_kernel<parse_message>",
            "sbe_decode_kernel<0u, 16384u>": "sbe_decode_kernel<parse_message>",
            "sbe_decode_kernel<0u, 12288u>": "sbe_decode_kernel<parse_message,wide>",
+           "sbe_decode_kernel<0u, 14336u>": "sbe_decode_kernel<parse_message,14k>",
+           "sbe_decode_kernel<0u, 8192u>": "sbe_decode_kernel<parse_message,8k>",
            "sbe_seqnum_kernel": "sbe_seqnum_kernel"}
 
 
 def short(name):
+    name = re.sub(r"(Lay<[^>]*?), (32|64)>", r"\1>", name)  # the layout's tile shape argument
     for k, v in KERNELS.items():
         if k in name:
             return v
