@@ -325,6 +325,30 @@ Ctx& ctx() {
 
 inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// n bytes from src to dst for the short strings of a record (topic, type, uuid, headers: tens of
+// bytes): fixed-size, overlapping moves that the compiler inlines, instead of a memcpy call per
+// string (the call, not the bytes, was the cost of staging and of building ParseResults)
+inline void copy_small(void* dst_, const void* src_, size_t n) {
+    uint8_t* dst = static_cast<uint8_t*>(dst_);
+    const uint8_t* src = static_cast<const uint8_t*>(src_);
+    if (n > 64) {
+        std::memcpy(dst, src, n);
+    } else if (n >= 16) {
+        for (size_t k = 0; k + 16 < n; k += 16) std::memcpy(dst + k, src + k, 16);
+        std::memcpy(dst + n - 16, src + n - 16, 16);
+    } else if (n >= 8) {
+        std::memcpy(dst, src, 8);
+        std::memcpy(dst + n - 8, src + n - 8, 8);
+    } else if (n >= 4) {
+        std::memcpy(dst, src, 4);
+        std::memcpy(dst + n - 4, src + n - 4, 4);
+    } else if (n) {
+        dst[0] = src[0];
+        dst[n / 2] = src[n / 2];
+        dst[n - 1] = src[n - 1];
+    }
+}
+
 // AERON_AMD_TRACE=1: one line per batch call on stderr with its phase times (diagnosis only)
 struct Trace {
     using clk = std::chrono::steady_clock;
@@ -675,7 +699,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
                 uint8_t* at = p + (pin[i] - in_lo);
                 for (int k2 = 0; k2 < nf; ++k2) {
                     const std::string_view f = field(i, k2);
-                    if (!f.empty()) std::memcpy(at, f.data(), f.size());
+                    copy_small(at, f.data(), f.size());
                     at += f.size();
                     lp[(size_t)nf * r + k2] = (uint32_t)f.size();
                 }
@@ -735,11 +759,6 @@ inline uint16_t rdu16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8));
 // the strings have grown to the records' sizes)
 void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, size_t i) {
     r.success = false;
-    r.error_message.clear();
-    r.message_type.clear();
-    r.message_id.clear();
-    r.payload.clear();
-    r.headers.clear();
     r.timestamp = 0;
     r.sequence_number = 0;
     r.template_id = r.schema_id = r.version = r.block_length = 0;
@@ -755,7 +774,19 @@ void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, 
         uint32_t n;
     };
     auto view = [&](int k) { return View{reinterpret_cast<const char*>(rec) + off[k], len[k]}; };
-    auto set = [](std::string& s, View v) { s.assign(v.p, v.n); };
+    // strings the status's branch writes (the others are cleared after it): resized only when the
+    // length changes, so a reused ParseResult of the same shape is overwritten in place
+    enum : unsigned { kType = 2, kId = 4, kPay = 8, kHdr = 16 };
+    unsigned written = 0;
+    auto set = [&](std::string& s, View v, unsigned which) {
+        if (s.size() != v.n) s.resize(v.n);
+        copy_small(s.data(), v.p, v.n);
+        written |= which;
+    };
+    auto put = [&](std::string& s, std::string&& v, unsigned which) {
+        s = std::move(v);
+        written |= which;
+    };
     auto take_hdr = [&] {
         r.block_length = h[0];
         r.template_id = h[1];
@@ -766,10 +797,10 @@ void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, 
     switch (st) {
         case SBE_ST_TM:  // src/sbe_encoder.cpp:1021-1135
             r.success = true;
-            set(r.message_type, view(1));
-            set(r.message_id, view(2));
-            set(r.payload, view(3));
-            set(r.headers, view(4));
+            set(r.message_type, view(1), kType);
+            set(r.message_id, view(2), kId);
+            set(r.payload, view(3), kPay);
+            set(r.headers, view(4), kHdr);
             r.timestamp = (int64_t)d.ts(i);
             r.sequence_key_present = (fl & SBE_FL_SEQ_KEY) != 0;
             r.sequence_number = d.seq(i);  // src/sbe_encoder.cpp:1031-1125
@@ -777,28 +808,28 @@ void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, 
             break;
         case SBE_ST_ACK:  // src/sbe_encoder.cpp:916-941
             r.success = true;
-            r.message_type = "Acknowledgment";
+            set(r.message_type, View{"Acknowledgment", 14}, kType);
             r.timestamp = (int64_t)d.ts(i);
             if (fl & SBE_FL_ID_DEFAULT)
-                r.message_id = "ack_" + std::to_string(d.ts(i));
+                put(r.message_id, "ack_" + std::to_string(d.ts(i)), kId);
             else
-                set(r.message_id, view(0));
+                set(r.message_id, view(0), kId);
             if (fl & SBE_FL_PAYLOAD_DEFAULT)
-                r.payload = "SUCCESS";
+                set(r.payload, View{"SUCCESS", 7}, kPay);
             else
-                set(r.payload, view(1));
-            set(r.headers, view(2));
+                set(r.payload, view(1), kPay);
+            set(r.headers, view(2), kHdr);
             take_hdr();
             break;
         case SBE_ST_SESSION_EVENT:  // src/sbe_encoder.cpp:629-644 (SessionEvent layout sbe_messages.hpp:39-50)
             r.success = true;
-            r.message_type = "SessionEvent";
+            set(r.message_type, View{"SessionEvent", 12}, kType);
             r.correlation_id = rdi64(rec + 8);
             r.session_id = rdi64(rec + 16);
             r.leadership_term_id = rdi64(rec + 24);
             r.leader_member_id = rdi32(rec + 32);
             r.event_code = rdi32(rec + 36);
-            set(r.payload, view(3));
+            set(r.payload, view(3), kPay);
             r.timestamp = 0;
             take_hdr();
             break;
@@ -828,6 +859,11 @@ void materialize_into(ParseResult& r, const uint8_t* rec, const Descriptors& d, 
             break;
         default: throw std::runtime_error("sbecodec: unexpected parse status");
     }
+    if (st < SBE_ST_ERR_NULL_EMPTY) r.error_message.clear();  // every error branch above sets it
+    if (!(written & kType)) r.message_type.clear();
+    if (!(written & kId)) r.message_id.clear();
+    if (!(written & kPay)) r.payload.clear();
+    if (!(written & kHdr)) r.headers.clear();
 }
 
 ParseResult materialize(const uint8_t* rec, const Descriptors& d, size_t i) {
