@@ -466,6 +466,45 @@ int main() {
             if (failures > 20) break;
         }
     }
+    // --- every field length 0..80 in every field position, against hand-built wire bytes: covers
+    // each size class of the staging copy (1..3, 4..7, 8..15, 16..64 overlapping moves, >64 memcpy)
+    // independently of the oracle, then parses the same records back into a reused vector
+    {
+        std::vector<TopicMessageFields> fm;
+        std::vector<std::vector<std::string>> fr;
+        for (int f = 0; f < 5; ++f)
+            for (int L = 0; L <= 80; ++L) {
+                std::vector<std::string> r(5);
+                for (int k = 0; k < 5; ++k) {
+                    size_t n = k == f ? (size_t)L : (size_t)((L * 7 + k * 13) % 81);
+                    r[k].resize(n);
+                    for (size_t j = 0; j < n; ++j) r[k][j] = (char)('A' + (j * 31 + k * 7 + L) % 58);
+                }
+                fr.push_back(r);
+                fm.push_back({r[0], r[1], r[2], r[3], r[4], (int64_t)(1700000000000000000LL + 1000003 * L + f)});
+            }
+        EncodedBatch b = SBEEncoder::encode_topic_batch(fm, EncodeLength::Wire);
+        std::vector<uint8_t> want;
+        std::vector<uint64_t> woff{0};
+        auto put = [&](uint64_t v, int nb) { for (int j = 0; j < nb; ++j) want.push_back((uint8_t)(v >> (8 * j))); };
+        for (size_t i = 0; i < fr.size(); ++i) {
+            put(16, 2), put(1, 2), put(1, 2), put(1, 2);
+            put((uint64_t)fm[i].timestamp, 8), put(0, 8);
+            for (int k = 0; k < 5; ++k) {
+                put(fr[i][k].size(), 2);
+                want.insert(want.end(), fr[i][k].begin(), fr[i][k].end());
+            }
+            woff.push_back(want.size());
+        }
+        CHECK(b.offsets == woff);
+        CHECK(b.bytes == want);
+        std::vector<ParseResult> prs(3);  // reused: more records than the vector holds
+        MessageParser::parse_batch(b.bytes.data(), b.offsets.data(), fr.size(), prs);
+        CHECK(prs.size() == fr.size());
+        for (size_t i = 0; i < fr.size() && failures <= 20; ++i)
+            CHECK(prs[i].success && prs[i].message_type == fr[i][1] && prs[i].message_id == fr[i][2] &&
+                  prs[i].payload == fr[i][3] && prs[i].headers == fr[i][4] && prs[i].timestamp == fm[i].timestamp);
+    }
     // ---- session frames (src/session_manager.cpp:936-967, :1050-1144) ----
     {
         SessionFrameEncoder sf;
