@@ -481,8 +481,11 @@ int main() {
                     for (size_t j = 0; j < n; ++j) r[k][j] = (char)('A' + (j * 31 + k * 7 + L) % 58);
                 }
                 fr.push_back(r);
-                fm.push_back({r[0], r[1], r[2], r[3], r[4], (int64_t)(1700000000000000000LL + 1000003 * L + f)});
             }
+        // the fields are views: into fr, once it no longer grows
+        for (size_t i = 0; i < fr.size(); ++i)
+            fm.push_back({fr[i][0], fr[i][1], fr[i][2], fr[i][3], fr[i][4],
+                          (int64_t)(1700000000000000000LL + 1000003 * (int64_t)(i % 81) + (int64_t)(i / 81))});
         EncodedBatch b = SBEEncoder::encode_topic_batch(fm, EncodeLength::Wire);
         std::vector<uint8_t> want;
         std::vector<uint64_t> woff{0};

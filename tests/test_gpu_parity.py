@@ -145,6 +145,30 @@ def test_encode_edges(codec):
         check_encode(codec, arena, L, ts, flags=flags, ts_default=1_760_000_000_123)
 
 
+def field_length_records():
+    """Every field length 0..80 in every field position, the other fields (7L + 13k) mod 81: 405
+    records whose tiles mix empty, 1..3-byte and ~80-byte strings (the C++ host test builds the same
+    records, tests/cpp/test_host_api.cpp)."""
+    recs, ts = [], []
+    for f in range(5):
+        for n in range(81):
+            r = []
+            for k in range(5):
+                m = n if k == f else (n * 7 + k * 13) % 81
+                r.append(bytes(ord("A") + (j * 31 + k * 7 + n) % 58 for j in range(m)))
+            recs.append(r)
+            ts.append(1_700_000_000_000_000_000 + 1_000_003 * n + f)
+    arena = np.frombuffer(b"".join(b"".join(r) for r in recs), np.uint8).copy()
+    L = np.array([[len(s) for s in r] for r in recs], np.uint32)
+    return arena, L, np.array(ts, np.uint64)
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+def test_encode_field_lengths(codec, flags):
+    arena, L, ts = field_length_records()
+    check_encode(codec, arena, L, ts, flags=flags)
+
+
 def _publish_lens(rng, n_small):
     """Lengths of ClusterClient::publish_topic records: the u16 wrap edges on every field, mixed
     into ordinary records so tiles hold both wrapped and plain records."""
