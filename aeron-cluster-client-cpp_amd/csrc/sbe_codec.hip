@@ -112,6 +112,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+// ceil(a / b) for a, b < 2^20, b > 0: a float reciprocal estimate corrected by one step either
+// way (exact), instead of the compiler's ~20-instruction u32 division
+__device__ __forceinline__ uint32_t ceil_div_small(uint32_t a, uint32_t b) {
+    const uint32_t x = a + b - 1;
+    uint32_t q = (uint32_t)((float)x * __builtin_amdgcn_rcpf((float)b));
+    q += (q + 1) * b <= x;
+    q -= q * b > x;
+    return q;
+}
+
 // inclusive max over the 64 lanes of values >= 0 (0 is the identity DPP fills in)
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     v = max(v, dpp0<0x111>(v));
@@ -226,7 +236,10 @@ struct Lay {
     // (~77-B records) are ~2.5 KiB, three of the eight 1-KiB rows
     static constexpr int kStoreRows0 = kNF == 2 ? (kRpt == 64 ? 5 : 3) : 8;
 };
-using LayTM = Lay<0, 16, 5, true, 32>;
+#ifndef SBE_TM_RPT
+#define SBE_TM_RPT 32  // A/B builds only (scripts/abv.py)
+#endif
+using LayTM = Lay<0, 16, 5, true, SBE_TM_RPT>;
 using LayTMS = Lay<32, 16, 5, true, 64>;
 using LayL2 = Lay<0, 12, 2, false, 64>;
 using LayL3 = Lay<0, 12, 3, false, 64>;
@@ -1448,16 +1461,23 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         const bool lead = q == 0 && nc > 0;
         const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
         const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
-        // T chunks per lane: C / (64 - records) rounded up, which always fits (sum of ceil(nc_j / T)
-        // <= C / T + records); one lane a record (64-record tiles): ceil(C / 64) first, when the
-        // records' runs of ceil(nc / T) lanes fit the wave (records of equal lengths: every lane
-        // busy); no spare lane: no rebalance
-        uint32_t U0 = ~0u, T0 = 0;
-        if (kLpr == 1) {
-            T0 = (C + kWave - 1) / kWave;
-            U0 = lane_u32(wave_incl_scan(lead ? ((uint32_t)nc + T0 - 1) / T0 : 0u, lane), kWave - 1);
+        // T chunks per lane: the smallest of T0 .. T0 + 3 (T0 = ceil(C / 64)) whose records' runs
+        // of ceil(nc_j / T) lanes fit the wave, from one scan of the four lane counts packed in
+        // bytes (each sum <= C / T0 + records <= 128, so no byte carries into the next); else
+        // ceil(C / (64 - records)), which always fits (sum of ceil(nc_j / T) <= C / T + records);
+        // no spare lane: no rebalance.  Variable-length TopicMessage windows (~21 records, ~390
+        // chunks) take T0 + 1 where the bound gives 10-12.
+        const uint32_t T0 = (C + kWave - 1) / kWave;
+        uint32_t pk = 0;
+        if (lead) {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) pk |= ceil_div_small((uint32_t)nc, T0 + k) << (8 * k);
         }
-        T = U0 <= (uint32_t)kWave ? T0 : (nrec < (uint32_t)kWave ? (C + (kWave - nrec) - 1) / (kWave - nrec) : 0u);
+        const uint32_t S4 = lane_u32(wave_incl_scan(pk, lane), kWave - 1);
+        T = nrec < (uint32_t)kWave ? (C + (kWave - nrec) - 1) / (kWave - nrec) : 0u;
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (((S4 >> (8 * k)) & 0xffu) <= (uint32_t)kWave) T = T0 + (uint32_t)k;
         const uint32_t mx = lane_u32(wave_incl_max((uint32_t)(n_mine > 0 ? n_mine : 0)), kWave - 1);
         rebal = T != 0 && (kGuard ? T < mx : true);
     }
@@ -1468,7 +1488,7 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         // lanes (at most 64 in all); a lane finds its record by a max-scan of the lanes where the
         // records' runs start, then reads that record's registers from its lead lane.
         const bool lead = q == 0 && nc > 0;
-        const uint32_t L = lead ? ((uint32_t)nc + T - 1) / T : 0u;
+        const uint32_t L = lead ? ceil_div_small((uint32_t)nc, T) : 0u;
         const uint32_t incL = wave_incl_scan(L, lane);
         const uint32_t A = incL - L;  // first lane serving this lane's record (lead lanes)
         const uint32_t used = lane_u32(incL, kWave - 1);
@@ -1497,8 +1517,11 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         n_mine = n_mine > 0 ? n_mine : 0;
     }
     const int32_t imax = (nb + kInSlack) / 4 - 5;
-    constexpr int kG = 4;  // chunks per group: all their LDS reads in flight together
-    for (int32_t i0 = 0; __ballot(i0 < n_mine); i0 += kG) {
+    // groups of kG chunks, all their LDS reads in flight together: 4 while some lane has 4 left,
+    // then a group of 2 and one of 1 as the longest lane needs them (a rebalanced window's T is
+    // rarely a multiple of 4)
+    auto group = [&](auto kGc, int32_t i0) {
+        constexpr int kG = decltype(kGc)::value;
         int32_t u[kG];
         uint32_t d[kG][5];
 #pragma unroll
@@ -1521,7 +1544,14 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
                 *reinterpret_cast<lds_u32x4*>(wout + wout_addr(p)) = v;
             }
         }
+    };
+    int32_t i0 = 0;
+    for (; __ballot(i0 + 3 < n_mine); i0 += 4) group(std::integral_constant<int, 4>{}, i0);
+    if (__ballot(i0 + 1 < n_mine)) {
+        group(std::integral_constant<int, 2>{}, i0);
+        i0 += 2;
     }
+    if (__ballot(i0 < n_mine)) group(std::integral_constant<int, 1>{}, i0);
     if (q == 0) {  // the record table entry zone_fixup reads (RecEnt; no record clipped here)
         i32x4 ea4, eb4;
         ea4.x = rw;
