@@ -383,20 +383,29 @@ struct Trace {
     }
 };
 
-// Bytes of staged work per pipeline chunk (AERON_AMD_CHUNK_BYTES, default 8 MiB).
-size_t chunk_target_bytes() {
-    static const size_t v = [] {
+// Bytes of staged work per pipeline chunk: AERON_AMD_CHUNK_BYTES when set, else a third of the
+// batch's bytes within [8, 32] MiB (and at most 65536 records, chunk_records): every chunk pays its
+// copies' and launches' fixed costs, and a batch of a few chunks still overlaps its copies.
+// host_latency, fixed-256 records, encode + parse_batch, three interleaved repetitions per
+// setting (profiles/r03_host_chunks.log): 8 MiB chunks 46 M rec/s at 262 K records (median) and
+// 39 M at 1 M; 16 MiB chunks (65536 records) 48 / 43 M at 262 K and 53 / 58 M at 1 M.  This
+// rule against fixed 8 MiB chunks, interleaved on one box: 262 K 43.5 vs 41.5 M, 1 M 48.3 vs
+// 47.8 M (medians; the box-to-box and run-to-run spread of these host numbers is ~20 %).
+size_t chunk_target_bytes(size_t total_bytes) {
+    static const size_t env = [] {
         const char* e = std::getenv("AERON_AMD_CHUNK_BYTES");
         const long long x = e ? std::atoll(e) : 0;
-        return x > 0 ? (size_t)x : (size_t(8) << 20);
+        return x > 0 ? (size_t)x : size_t(0);
     }();
-    return v;
+    if (env) return env;
+    return std::min(size_t(32) << 20, std::max(size_t(8) << 20, total_bytes / 3));
 }
 // Records per chunk: a power of two so that a chunk holds about chunk_target_bytes().
 size_t chunk_records(size_t n, size_t total_bytes) {
     const size_t avg = std::max<size_t>(1, total_bytes / std::max<size_t>(n, 1));
+    const size_t target = chunk_target_bytes(total_bytes);
     size_t c = 1;
-    while (c < n && c < 65536 && (c * 2) * avg <= chunk_target_bytes()) c *= 2;
+    while (c < n && c < 65536 && (c * 2) * avg <= target) c *= 2;
     return c;
 }
 
