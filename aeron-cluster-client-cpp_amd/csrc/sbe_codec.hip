@@ -5,9 +5,11 @@
 //
 //  encode  (SBEEncoder::encode_topic_message, src/sbe_encoder.cpp:131-167, and the session / Lite
 //           layouts), two launches:
-//    sbe_enc_sums  one 1024-thread workgroup per 4096-record superblock: each 32-record tile's
-//                  output / packed-input byte prefix inside its superblock, the superblock totals
-//    sbe_enc_pack  persistent, one wave per workgroup, tiles of 32 records (two lanes per record):
+//    sbe_enc_sums  one 1024-thread workgroup per superblock of 128 tiles: each tile's output /
+//                  packed-input byte prefix inside its superblock, the superblock totals
+//    sbe_enc_pack  persistent, one wave per workgroup, tiles of 32 records (two lanes per record;
+//                  the session and Lite layouts 64, a lane per record; Lay::kRpt), windows whose
+//                  chunks would leave some lane more than 8 rebalanced over the lanes:
 //                  record offsets by a DPP wave scan; output windows of <= 8 KiB holding whole
 //                  records; the next window's input strings loaded into registers while the current
 //                  one is composed (b128 chunk composition from the staged input: five LDS dword
@@ -17,8 +19,9 @@
 //  decode  (MessageParser::parse_message :513-551 / MessageHandler::on_egress
 //           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105 /
 //           the Lite flyweights), one launch, one wave per 64-record tile:
-//    1. the tile's bytes are staged window by window (16 KiB windows, 12 KiB for batches of records
-//       over 256 B on average) into an XOR-swizzled LDS window with 16-byte loads; the second
+//    1. the tile's bytes are staged window by window (16 KiB windows; 12 KiB for batches of records
+//       over 256 B on average, 14 KiB up to 204 B, 8 KiB up to 112 B: sbe_decode_batch_sized) into
+//       an XOR-swizzled LDS window with 16-byte loads; the second
 //       window's loads are issued before the first one is parsed
 //    2. each lane parses its record from LDS (template-ID dispatch per lane) and writes the
 //       descriptor SoA; records no window can hold are parsed from HBM.
