@@ -308,6 +308,7 @@ struct Pipeline {
 struct Ctx {
     Pipeline pipe;
     DevBuf d_aux;   // reassembly / Order JSON
+    DevBuf d_ws;    // encode workspace of the zero-copy path
     HostBuf h_aux;
     std::vector<uint64_t> pin, pout;  // encode plan scratch (kept: first-touch costs on every call otherwise)
     Ctx() {
@@ -316,7 +317,52 @@ struct Ctx {
     }
     ~Ctx() { pipe.destroy(); }
     void sync_all() { pipe.drain(); }
+    // After a throw inside a chunk loop: wait for every copy and kernel already queued (their
+    // page-locked sources and destinations must not go back to a pool, or be restaged, while a
+    // DMA still reads or writes them), then forget the slots' event history.  Never throws.
+    void abort_all() noexcept {
+        for (hipStream_t st : {pipe.s_in, pipe.s_comp, pipe.s_out})
+            if (st) (void)hipStreamSynchronize(st);
+        (void)hipGetLastError();
+        for (Pipeline::Slot& sl : pipe.slot) sl.used = false;
+    }
 };
+
+// Drains the pipeline if a chunk loop unwinds (declared after the buffers the queued copies use, so
+// it runs before they are released).
+struct PipeGuard {
+    Ctx& c;
+    bool armed = true;
+    explicit PipeGuard(Ctx& x) : c(x) {}
+    ~PipeGuard() {
+        if (armed) c.abort_all();
+    }
+    void release() { armed = false; }
+};
+
+// The device address of page-locked host memory (hipHostMalloc'd or registered), or nullptr when
+// it has none: kernels of the zero-copy path read their input and write their results there.
+void* device_view(const void* host) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(host), 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
+}
+
+// Batches up to this many staged bytes (one pipeline chunk) take the zero-copy path: the kernels
+// read the page-locked staging buffer and write their results straight into the page-locked result
+// block over PCIe, one launch (encode: two) and one completion wait, no hipMemcpyAsync.  Larger
+// one-chunk batches, and every chunk of a multi-chunk batch, go through the DMA copy engines.
+// AERON_AMD_ZC_BYTES overrides (0: never).
+size_t zero_copy_max_bytes() {
+    static const size_t v = [] {
+        const char* e = std::getenv("AERON_AMD_ZC_BYTES");
+        return e ? (size_t)std::max(0LL, std::atoll(e)) : (size_t(4) << 20);
+    }();
+    return v;
+}
 
 Ctx& ctx() {
     thread_local Ctx c;
@@ -565,6 +611,45 @@ bool page_locked(const void* p, size_t bytes) {
 // soon as its descriptors are on the host, while the later chunks are still being copied and
 // decoded: the host's work on chunk k overlaps the device's on chunk k+1.
 using ChunkFn = std::function<void(const Descriptors&, size_t, size_t)>;
+
+// The zero-copy path of a one-chunk decode: the offsets (and, unless the caller's bytes are
+// page-locked already, the records) staged in the slot's page-locked buffer, which the kernel reads
+// over PCIe; the descriptors written by the kernel straight into d.block.  One launch, one wait.
+// false (nothing launched) when some buffer has no device address.
+bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode, bool direct,
+                      Descriptors& d) {
+    Pipeline& P = c.pipe;
+    Pipeline::Slot& sl = P.slot[0];  // serial use (the pipeline is idle between calls)
+    const uint64_t lo = rec_off[0], bytes = rec_off[n] - lo;
+    const size_t o_data = al16((n + 1) * 8);
+    sl.pin.need((direct ? o_data : o_data + (size_t)bytes) + 16);
+    uint8_t* pin = sl.pin.b();
+    uint64_t* ro = reinterpret_cast<uint64_t*>(pin);
+    uint8_t* dpin = static_cast<uint8_t*>(device_view(pin));
+    uint8_t* dblk = static_cast<uint8_t*>(device_view(d.block.get()));
+    const uint8_t* drec = direct ? static_cast<const uint8_t*>(device_view(data + lo)) : (dpin ? dpin + o_data : nullptr);
+    if (!dpin || !dblk || !drec) return false;
+    for_ranges(n + 1, 8192, [&](size_t x, size_t y) {
+        for (size_t i = x; i < y; ++i) ro[i] = rec_off[i] - lo;
+    });
+    if (!direct && bytes)
+        for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) { copy_small(pin + o_data + x, data + lo + x, y - x); });
+    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
+    sbe_decoded out{dblk,
+                    dblk + d.o_fl,
+                    reinterpret_cast<uint16_t*>(dblk + d.o_hdr),
+                    reinterpret_cast<uint64_t*>(dblk + d.o_ts),
+                    reinterpret_cast<uint32_t*>(dblk + d.o_off),
+                    reinterpret_cast<uint32_t*>(dblk + d.o_len),
+                    parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
+    if (sbe_decode_batch_sized(drec, reinterpret_cast<const uint64_t*>(dpin), n, bytes, mode, &out, P.s_comp) != SBE_OK) {
+        c.abort_all();
+        fail("sbe_decode_batch");
+    }
+    hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
+    return true;
+}
+
 std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec_off, size_t n, uint32_t mode,
                                         const ChunkFn* on_chunk = nullptr) {
     auto d = std::make_shared<Descriptors>();
@@ -583,6 +668,15 @@ std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec
     d->block = PinnedPool::get().take(K * d->chunk_bytes);
     uint8_t* hblk = static_cast<uint8_t*>(d->block.get());
     tr.lap(tr.plan);
+    if (K == 1 && al16((n + 1) * 8) + (direct ? 0 : (size_t)total) <= zero_copy_max_bytes() &&
+        decode_zero_copy(c, data, rec_off, n, mode, direct, *d)) {
+        tr.lap(tr.sync);
+        if (on_chunk) (*on_chunk)(*d, 0, n);
+        tr.lap(tr.finish);
+        tr.done(n, 0);
+        return d;
+    }
+    PipeGuard guard(c);
     for (size_t k = 0; k < K; ++k) {
         const size_t a = k * C, m = std::min(n, a + C) - a;
         const uint64_t lo = rec_off[a], bytes = rec_off[a + m] - lo;
@@ -631,6 +725,7 @@ std::shared_ptr<Descriptors> run_decode(const uint8_t* data, const uint64_t* rec
         }
     }
     c.sync_all();
+    guard.release();
     tr.lap(tr.sync);
     if (on_chunk) {
         (*on_chunk)(*d, (K - 1) * C, n - (K - 1) * C);
@@ -682,26 +777,24 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
     const size_t K = (n + C - 1) / C;
     P.serial = K == 1;
     b.bytes = HostBytesAccess::make((size_t)pout[n]);
-    // per-chunk device offsets (C + 1) and status (C), copied back beside each other
-    const size_t meta_stride = al16((C + 1) * 8 + C);
-    std::shared_ptr<void> meta = PinnedPool::get().take(K * meta_stride);
-    uint8_t* hmeta = static_cast<uint8_t*>(meta.get());
-    const size_t ws_bytes = sbe_encode_workspace_size(C);
-    tr.lap(tr.plan);
-    for (size_t k = 0; k < K; ++k) {
-        const size_t a = k * C, m = std::min(n, a + C) - a;
-        const uint64_t in_lo = pin[a], in_bytes = pin[a + m] - in_lo;
-        const uint64_t out_lo = pout[a], out_bytes = pout[a + m] - out_lo;
-        // staging layout: arena | u32 lengths [m][nf] | u64 [m] | u32 [m]
-        const size_t o_len = al16((size_t)in_bytes), o_u64 = o_len + al16((size_t)m * 4 * nf),
-                     o_u32 = o_u64 + al16(m * 8), stage = o_u32 + al16(m * 4);
-        Pipeline::Slot& sl = P.begin(k);
-        tr.lap(tr.wait);
-        sl.pin.need(stage);
-        uint8_t* p = sl.pin.b();
-        uint32_t* lp = reinterpret_cast<uint32_t*>(p + o_len);
-        uint64_t* up = reinterpret_cast<uint64_t*>(p + o_u64);
-        uint32_t* wp = reinterpret_cast<uint32_t*>(p + o_u32);
+    // staging layout of records [a, a + m): arena | u32 lengths [m][nf] | u64 [m] | u32 [m]
+    struct Stage {
+        size_t o_len, o_u64, o_u32, bytes;
+    };
+    auto stage_layout = [&](size_t a, size_t m) {
+        const uint64_t in_bytes = pin[a + m] - pin[a];
+        Stage s;
+        s.o_len = al16((size_t)in_bytes);
+        s.o_u64 = s.o_len + al16((size_t)m * 4 * nf);
+        s.o_u32 = s.o_u64 + al16(m * 8);
+        s.bytes = s.o_u32 + al16(m * 4);
+        return s;
+    };
+    auto stage_fill = [&](uint8_t* p, const Stage& s, size_t a, size_t m) {
+        const uint64_t in_lo = pin[a];
+        uint32_t* lp = reinterpret_cast<uint32_t*>(p + s.o_len);
+        uint64_t* up = reinterpret_cast<uint64_t*>(p + s.o_u64);
+        uint32_t* wp = reinterpret_cast<uint32_t*>(p + s.o_u32);
         for_ranges(m, 2048, [&](size_t x, size_t y) {
             for (size_t r = x; r < y; ++r) {
                 const size_t i = a + r;
@@ -716,6 +809,55 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
                 wp[r] = u32(i);
             }
         });
+    };
+    tr.lap(tr.plan);
+    if (K == 1) {
+        // zero-copy: the kernels read the page-locked staging buffer and write the stream, the
+        // offsets and the status straight into the caller's page-locked result arrays
+        const Stage s = stage_layout(0, n);
+        Pipeline::Slot& sl = P.slot[0];
+        if (s.bytes <= zero_copy_max_bytes()) {
+            sl.pin.need(s.bytes);
+            uint8_t* dp = static_cast<uint8_t*>(device_view(sl.pin.p));
+            uint8_t* dbytes = n && pout[n] ? static_cast<uint8_t*>(device_view(b.bytes.data())) : nullptr;
+            uint64_t* doff = static_cast<uint64_t*>(device_view(b.offsets.data()));
+            uint8_t* dst = static_cast<uint8_t*>(device_view(b.status.data()));
+            if (dp && doff && dst && (dbytes || pout[n] == 0)) {
+                stage_fill(sl.pin.b(), s, 0, n);
+                tr.lap(tr.stage);
+                PipeGuard zguard(c);
+                const size_t ws_bytes = sbe_encode_workspace_size(n);
+                c.d_ws.need(ws_bytes);
+                // a batch whose records all fail (E109) has no bytes: the kernels still want a
+                // 16-B aligned output pointer, which they never write at capacity 0
+                launch(dp, reinterpret_cast<const uint32_t*>(dp + s.o_len), reinterpret_cast<const uint64_t*>(dp + s.o_u64),
+                       reinterpret_cast<const uint32_t*>(dp + s.o_u32), n, dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst,
+                       c.d_ws.b(), ws_bytes, P.s_comp);
+                tr.lap(tr.enqueue);
+                hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
+                zguard.release();
+                tr.lap(tr.sync);
+                if (b.offsets[n] != pout[n]) throw std::logic_error("sbecodec: encoded batch size differs from its plan");
+                tr.done(n, 0);
+                return b;
+            }
+        }
+    }
+    // per-chunk device offsets (C + 1) and status (C), copied back beside each other
+    const size_t meta_stride = al16((C + 1) * 8 + C);
+    std::shared_ptr<void> meta = PinnedPool::get().take(K * meta_stride);
+    uint8_t* hmeta = static_cast<uint8_t*>(meta.get());
+    const size_t ws_bytes = sbe_encode_workspace_size(C);
+    PipeGuard guard(c);
+    for (size_t k = 0; k < K; ++k) {
+        const size_t a = k * C, m = std::min(n, a + C) - a;
+        const uint64_t out_lo = pout[a], out_bytes = pout[a + m] - out_lo;
+        const Stage s = stage_layout(a, m);
+        const size_t o_len = s.o_len, o_u64 = s.o_u64, o_u32 = s.o_u32, stage = s.bytes;
+        Pipeline::Slot& sl = P.begin(k);
+        tr.lap(tr.wait);
+        sl.pin.need(stage);
+        stage_fill(sl.pin.b(), s, a, m);
         tr.lap(tr.stage);
         // device: out bytes | out_off [m+1] | status [m] | workspace
         const size_t d_off = al16((size_t)out_bytes), d_ws = d_off + meta_stride;
@@ -734,6 +876,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         tr.lap(tr.enqueue);
     }
     c.sync_all();
+    guard.release();
     tr.lap(tr.sync);
     for (size_t k = 0; k < K; ++k) {
         const size_t a = k * C, m = std::min(n, a + C) - a;
@@ -1077,6 +1220,101 @@ std::string ParseResult::get_description() const {
         ss << "Parse Error: " << error_message;
     }
     return ss.str();
+}
+
+// ======================================================================================
+// SBEDecoder (src/sbe_encoder.cpp:174-323): one-record struct readers, host code (see the header)
+// ======================================================================================
+namespace {
+// SBEDecoder::extract_variable_string (:285-318): a u32 length prefix at offset, the string after
+// it; 0 (output untouched) when the prefix or the string does not fit or the length is over 10 MiB
+size_t extract_variable_string(const uint8_t* data, size_t offset, size_t remaining, std::string& output) {
+    if (offset + sizeof(uint32_t) > remaining) {
+        debug_log("[ERROR] Not enough data for length prefix at offset ", offset, ", remaining: ", remaining);
+        return 0;
+    }
+    uint32_t length;
+    std::memcpy(&length, data + offset, sizeof(uint32_t));
+    debug_log("[DEBUG] Extracting string at offset ", offset, ", length prefix: ", length, ", remaining: ", remaining);
+    offset += sizeof(uint32_t);
+    if (length > remaining - sizeof(uint32_t) || length > 10u * 1024u * 1024u) {
+        debug_log("[ERROR] Invalid string length: ", length, ", remaining data: ", (remaining - sizeof(uint32_t)));
+        return 0;
+    }
+    if (length > 0) {
+        output.assign(reinterpret_cast<const char*>(data + offset), length);
+        offset += length;
+        debug_log("[DEBUG] Extracted string: \"", output, "\"");
+    } else {
+        output.clear();
+        debug_log("[DEBUG] Extracted empty string");
+    }
+    return offset;
+}
+}  // namespace
+
+bool SBEDecoder::decode_message_header(const std::uint8_t* data, std::size_t length, MessageHeader& header) {
+    if (!data || length < sizeof(MessageHeader)) return false;
+    std::memcpy(&header, data, sizeof(MessageHeader));
+    return true;
+}
+
+bool SBEDecoder::decode_session_event(const std::uint8_t* data, std::size_t length, SessionEvent& event,
+                                      std::string& detail) {
+    if (!data || length < sizeof(MessageHeader) + SessionEvent::sbe_block_length()) return false;
+    if (debug_enabled()) {  // the reference's raw-data diagnostics (:189-214)
+        debug_log("Raw data analysis (", length, " bytes)");
+        debug_log("Hex dump: ");
+        for (size_t i = 0; i < length && i < 64; ++i) {
+            debug_log("0x", static_cast<unsigned>(data[i]), " ");
+            if ((i + 1) % 16 == 0) debug_log("\n          ");
+        }
+        debug_log("Readable content: ");
+        std::string readable;
+        for (size_t i = 0; i < length && i < 256; ++i) {
+            const char ch = static_cast<char>(data[i]);
+            if (ch >= 32 && ch <= 126) {
+                readable += ch;
+            } else if (!readable.empty()) {
+                if (readable.length() >= 3) debug_log("\"", readable, "\" ");
+                readable.clear();
+            }
+        }
+        if (readable.length() >= 3) debug_log("\"", readable, "\"");
+    }
+    MessageHeader header;
+    if (!decode_message_header(data, length, header)) return false;
+    if (!(header.template_id == SessionEvent::sbe_template_id() && header.schema_id == SessionEvent::sbe_schema_id()))
+        return false;
+    std::memcpy(&event, data + sizeof(MessageHeader), SessionEvent::sbe_block_length());
+    const size_t remaining = length - sizeof(MessageHeader) - SessionEvent::sbe_block_length();
+    if (remaining > 0)
+        extract_variable_string(data + sizeof(MessageHeader) + SessionEvent::sbe_block_length(), 0, remaining, detail);
+    return true;
+}
+
+bool SBEDecoder::decode_acknowledgment(const std::uint8_t* data, std::size_t length, std::string& message_id,
+                                       std::string& status, std::string& error, std::int64_t& timestamp) {
+    constexpr size_t kAckBlock = 8;  // Acknowledgment::sbe_block_length() (sbe_messages.hpp:106-118)
+    if (!data || length < sizeof(MessageHeader) + kAckBlock) return false;
+    MessageHeader header;
+    if (!decode_message_header(data, length, header)) return false;
+    if (!(header.template_id == SBEConstants::ACKNOWLEDGMENT_TEMPLATE_ID && header.schema_id == SBEConstants::TOPIC_SCHEMA_ID))
+        return false;
+    const uint8_t* ptr = data + sizeof(MessageHeader);
+    std::memcpy(&timestamp, ptr, sizeof(int64_t));
+    ptr += kAckBlock;
+    const size_t remaining = length - sizeof(MessageHeader) - kAckBlock;
+    size_t offset = extract_variable_string(ptr, 0, remaining, message_id);
+    if (offset == 0) return false;
+    offset = extract_variable_string(ptr, offset, remaining, status);
+    if (offset == 0) return false;
+    if (offset < remaining) extract_variable_string(ptr, offset, remaining, error);
+    return true;
+}
+
+std::int64_t SBEEncoder::get_current_timestamp() {
+    return (std::int64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count();
 }
 
 bool gpu_codec_available() { return sbe_device_ready() == 1; }

@@ -60,6 +60,54 @@ constexpr std::int32_t SESSION_EVENT_CLOSED = 4;
 constexpr std::size_t SBE_HEADER_LENGTH = 8;
 }  // namespace SBEConstants
 
+// include/aeron_cluster/sbe_messages.hpp:14-20: the 8-byte SBE message header, packed
+struct MessageHeader {
+    std::uint16_t block_length;
+    std::uint16_t template_id;
+    std::uint16_t schema_id;
+    std::uint16_t version;
+} __attribute__((packed));
+static_assert(sizeof(MessageHeader) == 8, "MessageHeader must be exactly 8 bytes");
+
+// include/aeron_cluster/sbe_messages.hpp:39-54: SessionEvent's 32-byte fixed block (template 2,
+// schema 111), packed
+struct SessionEvent {
+    std::int64_t correlation_id;
+    std::int64_t cluster_session_id;
+    std::int64_t leadership_term_id;
+    std::int32_t leader_member_id;
+    std::int32_t code;
+    static constexpr std::uint16_t sbe_block_length() { return 32; }
+    static constexpr std::uint16_t sbe_template_id() { return 2; }
+    static constexpr std::uint16_t sbe_schema_id() { return 111; }
+    static constexpr std::uint16_t sbe_schema_version() { return 8; }
+} __attribute__((packed));
+static_assert(sizeof(SessionEvent) == 32, "SessionEvent must be exactly 32 bytes");
+
+// include/aeron_cluster/sbe_messages.hpp:189-247, bodies src/sbe_encoder.cpp:174-323: the
+// reference's one-record struct readers.  Host code: each is a header / fixed-block copy plus at
+// most three u32-length-prefixed strings, and none is on the batch decode path (parse_message
+// reaches SessionEvent through the GPU decode, whose fields these return for the same record; the
+// u32-prefixed Acknowledgment layout of decode_acknowledgment is unreachable from parse_message,
+// whose is_topic_message() claims template 2 / schema 1 first, src/sbe_encoder.cpp:536-544).
+// decode_topic_message is declared by the reference but never defined (no definition in src/), so
+// it is not provided here either.
+class SBEDecoder {
+public:
+    // :174-181: false for null data or fewer than 8 bytes, else the header bytes
+    static bool decode_message_header(const std::uint8_t* data, std::size_t length, MessageHeader& header);
+    // :183-238: false below 40 bytes or unless template 2 / schema 111; event = the 32-B block;
+    // detail = the u32-prefixed string after it when one fits (<= 10 MiB; empty when its length is
+    // 0; left as the caller had it when the prefix or the string does not fit)
+    static bool decode_session_event(const std::uint8_t* data, std::size_t length, SessionEvent& event,
+                                     std::string& detail);
+    // :240-282: false below 16 bytes, unless template 2 / schema 1, or when message_id or status (u32
+    // prefixes after the 8-B block) do not fit; error is read when bytes remain after status;
+    // timestamp = the i64 after the header (written whenever the header checks pass)
+    static bool decode_acknowledgment(const std::uint8_t* data, std::size_t length, std::string& message_id,
+                                      std::string& status, std::string& error, std::int64_t& timestamp);
+};
+
 // The reference's debug helpers (include/aeron_cluster/sbe_messages.hpp:252-301, bodies
 // src/sbe_encoder.cpp:328-485).  Host-side formatting only: ParseResult::get_description and the
 // reference's tools (tools/message_inspector.cpp) call them; none of them is on the codec path.
@@ -195,6 +243,8 @@ public:
     // Batch encode: one GPU launch; records with E109 get status != 0 and zero bytes.
     static EncodedBatch encode_topic_batch(const std::vector<TopicMessageFields>& msgs,
                                            EncodeLength length = EncodeLength::Wire);
+    // src/sbe_encoder.cpp:169-172: high_resolution_clock ticks since its epoch (nanoseconds)
+    static std::int64_t get_current_timestamp();
 };
 
 class ParsedBatch;

@@ -73,9 +73,11 @@ def parse_args():
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
     p.add_argument("--settle-ms", type=float, default=500.0,
                    help="untimed round trips before the warmup steps, until the GPU has run this long")
-    p.add_argument("--event-every", type=int, default=10,
-                   help="HIP events on the pack / decode dispatches of every k-th timed step (0: none, "
-                        "diagnosis only: kernel times then come from an extra untimed pass)")
+    p.add_argument("--event-every", type=int, default=-1,
+                   help="HIP events on the pack / decode dispatches of every k-th timed step (-1: "
+                        "max(1, min(10, steps // 20)), so that at least 20 launches are sampled whenever "
+                        "steps >= 20 (every launch below 200 steps); 0: none, diagnosis only: kernel "
+                        "times then come from an extra untimed pass)")
     return p.parse_args()
 
 
@@ -320,6 +322,8 @@ def verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 22):
 
 def main():
     args = parse_args()
+    if args.event_every < 0:
+        args.event_every = max(1, min(10, args.steps // 20))
     if args.gpus > 1 and not launched_distributed():
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local = setup_dist(args)
@@ -398,8 +402,10 @@ def main():
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-    pack_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_PACK)))
-    deck_ms = float(np.mean(sbecodec.profile_read(sbecodec.PROF_DECODE)))
+    pack_samples = sbecodec.profile_read(sbecodec.PROF_PACK)
+    deck_samples = sbecodec.profile_read(sbecodec.PROF_DECODE)
+    pack_ms = float(np.mean(pack_samples))
+    deck_ms = float(np.mean(deck_samples))
     sbecodec.profile_enable(0)
 
     # informational, untimed: whole-call encode (sums + pack) and decode times
@@ -426,10 +432,10 @@ def main():
 
         if pack_ms >= deck_ms:
             dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, bytes_all=ENC_BYTES_ALL,
-                       ms=pack_ms)
+                       ms=pack_ms, samples=pack_samples)
         else:
             dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES,
-                       bytes_all=DEC_BYTES_ALL, ms=deck_ms)
+                       bytes_all=DEC_BYTES_ALL, ms=deck_ms, samples=deck_samples)
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
@@ -449,8 +455,13 @@ def main():
                          "bytes_source": "SURVEY §8(d) algorithmic bytes per 256-B record",
                          "achieved_incl_offsets": gbs(dom["bytes_all"], dom["ms"]),
                          "bytes_per_record_incl_offsets": dom["bytes_all"],
-                         "timing": (f"HIP events on the kernel's dispatch in every {args.event_every}th timed step"
-                                    if args.event_every else "HIP events, untimed pass (diagnosis run)")},
+                         "timing": (f"HIP events on the kernel's dispatch in every {args.event_every}th timed step: "
+                                    f"{len(dom['samples'])} samples"
+                                    if args.event_every else "HIP events, untimed pass (diagnosis run)"),
+                         "samples": len(dom["samples"]),
+                         "kernel_ms_min": float(np.min(dom["samples"])),
+                         "kernel_ms_median": float(np.median(dom["samples"])),
+                         "kernel_ms_max": float(np.max(dom["samples"]))},
             "kernels": {"encode_ms": enc_ms, "decode_ms": dec_ms, "pack_ms": pack_ms,
                         "pack_gbs": gbs(ENC_BYTES, pack_ms), "decode_kernel_ms": deck_ms,
                         "decode_kernel_gbs": gbs(DEC_BYTES, deck_ms),

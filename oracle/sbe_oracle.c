@@ -1227,3 +1227,58 @@ int orc_order_json_batch(const uint8_t* arena, const uint32_t* str_off, const ui
     free(base);
     return 0;
 }
+
+/* ---- SBEDecoder's one-record struct readers (src/sbe_encoder.cpp:174-323) ---------------- */
+
+/* SBEDecoder::extract_variable_string, src/sbe_encoder.cpp:285-318: u32 length prefix at `off`
+ * of a region of `rem` bytes; returns the end offset, 0 when nothing was assigned (prefix past the
+ * region, length past the region or above 10 MiB).  *s_off / *s_len: the string assigned. */
+static uint64_t sbedec_extract(const uint8_t* p, uint64_t off, uint64_t rem, uint32_t* s_off, uint32_t* s_len) {
+    if (off + 4 > rem) return 0;                                   /* :287-290 */
+    uint64_t L = rd32(p + off);                                    /* :295-296 */
+    off += 4;
+    if (L > rem - 4 || L > 10u * 1024u * 1024u) return 0;          /* :302-305 */
+    *s_off = (uint32_t)off;
+    *s_len = (uint32_t)L;                                          /* :308-315 (0: clear) */
+    return off + L;
+}
+
+/* SBEDecoder::decode_session_event, src/sbe_encoder.cpp:183-238 */
+int orc_sbedecoder_session_event(const uint8_t* rec, uint64_t len, uint32_t* d_off, uint32_t* d_len, uint32_t* got) {
+    *got = 0;
+    if (!rec || len < 8 + 32) return 0;                            /* :185-187 */
+    if (!(rd16(rec + 2) == 2 && rd16(rec + 4) == SBE_CLUSTER_SCHEMA_ID)) return 0; /* :216-223, :320-323 */
+    uint64_t rem = len - 40;                                       /* :232 */
+    if (rem > 0) {
+        uint32_t o = 0, l = 0;
+        if (sbedec_extract(rec + 40, 0, rem, &o, &l)) {            /* :233-235 */
+            *d_off = 40 + o;
+            *d_len = l;
+            *got = 1;
+        }
+    }
+    return 1;
+}
+
+/* SBEDecoder::decode_acknowledgment, src/sbe_encoder.cpp:240-282.  got: bit k = string k
+ * (messageId, status, error) assigned at rec[off[k] .. off[k] + slen[k]); bit 3 = *ts written. */
+int orc_sbedecoder_ack(const uint8_t* rec, uint64_t len, uint32_t off[3], uint32_t slen[3], uint32_t* got, int64_t* ts) {
+    *got = 0;
+    if (!rec || len < 8 + 8) return 0;                             /* :243-245 */
+    if (!(rd16(rec + 2) == 2 && rd16(rec + 4) == 1)) return 0;     /* :253-256 */
+    *ts = (int64_t)rd64(rec + 8);                                  /* :259-260 */
+    *got |= 8;
+    const uint8_t* p = rec + 16;
+    uint64_t rem = len - 16, o = 0;                                /* :264-265 */
+    uint32_t so, sl;
+    o = sbedec_extract(p, o, rem, &so, &sl);                       /* :268-270 */
+    if (o == 0) return 0;
+    off[0] = 16 + so, slen[0] = sl, *got |= 1;
+    o = sbedec_extract(p, o, rem, &so, &sl);                       /* :272-274 */
+    if (o == 0) return 0;
+    off[1] = 16 + so, slen[1] = sl, *got |= 2;
+    if (o < rem && sbedec_extract(p, o, rem, &so, &sl)) {          /* :277-279 */
+        off[2] = 16 + so, slen[2] = sl, *got |= 4;
+    }
+    return 1;
+}

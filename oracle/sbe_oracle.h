@@ -85,6 +85,13 @@ int orc_order_json_batch(const uint8_t* arena, const uint32_t* str_off, const ui
                          const int64_t* customer_id, const int64_t* timestamp, const double* quantity,
                          uint64_t n, uint32_t what, uint8_t* out, uint64_t* out_off, int nthreads);
 
+/* SBEDecoder::decode_session_event (src/sbe_encoder.cpp:183-238): 1 (true) / 0 (false); *got = 1
+ * when the u32-prefixed detail was assigned, its bytes at rec[*off .. *off + *len). */
+int orc_sbedecoder_session_event(const uint8_t* rec, uint64_t len, uint32_t* off, uint32_t* len_out, uint32_t* got);
+/* SBEDecoder::decode_acknowledgment (:240-282): 1 / 0; *got bit k = string k (messageId, status,
+ * error) assigned at rec[off[k] .. off[k] + slen[k]), bit 3 = *ts written. */
+int orc_sbedecoder_ack(const uint8_t* rec, uint64_t len, uint32_t off[3], uint32_t slen[3], uint32_t* got, int64_t* ts);
+
 /* protocol.hpp:37-42 */
 uint64_t orc_to_nanos_auto(uint64_t ts);
 
