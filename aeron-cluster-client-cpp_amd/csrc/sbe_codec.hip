@@ -979,6 +979,31 @@ __device__ __forceinline__ RecEnt rec_load(lds_i32* rt, int32_t r) {
     return E;
 }
 
+// The five dwords i .. i+4 of the staged input (a 16-byte chunk at any byte alignment inside them).
+// SBE_CHUNK_B64: as three ds_read_b64 at the 8-byte aligned dword i & ~1 and one select per dword
+// (banks (a/4) mod 64 for ds_read_b64, against (a/4) mod 32 for ds_read_b32: lanes whose chunks lie
+// 128 B apart, the two lanes of a 256-B record, or a rebalanced window's runs of 16 T bytes, stop
+// sharing banks); else five ds_read_b32.  i <= imax - 1 (the b64 form reads one dword further).
+#ifndef SBE_CHUNK_B64
+#define SBE_CHUNK_B64 0
+#endif
+__device__ __forceinline__ void lds_dw5(lds_cu8* inb, int32_t i, uint32_t (&d)[5]) {
+    if (SBE_CHUNK_B64) {
+        const lds_cu32x2* q = reinterpret_cast<lds_cu32x2*>(reinterpret_cast<lds_cu32*>(inb) + (i & ~1));
+        const u32x2 a = q[0], b = q[1], c = q[2];
+        const bool odd = (i & 1) != 0;
+        d[0] = odd ? a.y : a.x;
+        d[1] = odd ? b.x : a.y;
+        d[2] = odd ? b.y : b.x;
+        d[3] = odd ? c.x : b.y;
+        d[4] = odd ? c.y : c.x;
+    } else {
+        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) d[j] = q[j];
+    }
+}
+
 // the 16 bytes at staged-input position u (any alignment); the base is clamped into the array
 // (a clamped read only ever feeds don't-care bytes)
 __device__ __forceinline__ u32x4 chunk_lds(lds_cu8* inb, int32_t u, int32_t imax) {
@@ -1155,10 +1180,8 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
         int32_t i = u[k] >> 2;
-        i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
-        lds_cu32* q = reinterpret_cast<lds_cu32*>(inb) + i;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) d[k][j] = q[j];
+        i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax - 1 ? imax - 1 : i);
+        lds_dw5(inb, i, d[k]);
     }
     lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;  // padded rows never split a lane
 #pragma unroll
@@ -1533,10 +1556,8 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
             const int32_t f = (X >= bz1) + (X >= bz2) + (X >= bz3) + (X >= bz4);
             u[k] = bsrc0 + X - 2 * f;
             int32_t i = u[k] >> 2;
-            i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
-            lds_cu32* qd = reinterpret_cast<lds_cu32*>(inb) + i;
-#pragma unroll
-            for (int j = 0; j < 5; ++j) d[k][j] = qd[j];
+            i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax - 1 ? imax - 1 : i);
+            lds_dw5(inb, i, d[k]);
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
@@ -2172,6 +2193,9 @@ __device__ __forceinline__ uint64_t printable_mask64<LdsRec>(const LdsRec& R, ui
     return nbytes >= 64 ? m : m & ((1ull << nbytes) - 1);
 }
 
+#ifndef SBE_ACK_FAST
+#define SBE_ACK_FAST 1
+#endif
 // decode_acknowledgment_with_sbe (src/sbe_encoder.cpp:833-954)
 template <typename R_t>
 __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& d) {
@@ -2181,9 +2205,38 @@ __device__ void dec_ack_heuristic(const R_t& R, uint32_t b, uint32_t len, Desc& 
     d.status = SBE_ST_ACK;
     d.ts = R.u64(b + 8);
     if (b) d.flags |= SBE_FL_WRAPPED;
+    // Fast path (the common, well-formed Ack: u16-length-prefixed messageId, topic, correlationId
+    // from byte 16, src/ack_decoder.cpp's layout): when every field byte is printable, every length
+    // byte is not, each field is >= 3 bytes and the byte after the third field is not printable (or
+    // is past the record), the first three maximal runs of the scan below are exactly the three
+    // fields.  One 64-byte printable mask checks that for fields ending by byte 79; anything else
+    // takes the general run scan.
+    uint32_t nruns = 0;
+#if SBE_ACK_FAST
+    if (len >= 22) {
+        const uint32_t L1 = R.u16(b + 16);
+        const uint32_t p2 = 18 + L1;
+        const uint32_t L2 = p2 + 2 <= len ? R.u16(b + p2) : 0u;
+        const uint32_t p3 = p2 + 2 + L2;
+        const uint32_t L3 = p3 + 2 <= len ? R.u16(b + p3) : 0u;
+        const uint32_t end3 = p3 + 2 + L3;  // record offset after the third field
+        const uint32_t span = (end3 < len ? end3 + 1 : end3) - 16;  // bytes [16, 16 + span) decide
+        if (L1 >= 3 && L2 >= 3 && L3 >= 3 && end3 <= len && span <= 64) {
+            const uint64_t m = printable_mask64(R, b + 16, span);
+            auto ones = [](uint32_t n) { return n >= 64 ? ~0ull : (1ull << n) - 1; };
+            // field bits: [2, 2 + L1), [4 + L1, 4 + L1 + L2), [6 + L1 + L2, 6 + L1 + L2 + L3) of the span
+            const uint64_t want = (ones(L1) << 2) | (ones(L2) << (4 + L1)) | (ones(L3) << (6 + L1 + L2));
+            if ((m & ones(span)) == want) {
+                d.set_view(0, b + 18, L1);
+                d.set_view(1, b + p2 + 2, L2);
+                d.set_view(2, b + p3 + 2, L3);
+                return;
+            }
+        }
+    }
+#endif
     // maximal runs of printable bytes over [16, len), 64 bytes per block as a bitmask; a run may
     // continue into the next block
-    uint32_t nruns = 0;
     uint64_t run_start = 0, run_len = 0;
     for (uint32_t s0 = 16; s0 < len && nruns < 3; s0 += 64) {
         const uint32_t nb = len - s0 < 64u ? len - s0 : 64u;
@@ -3404,6 +3457,15 @@ static RcclApi& rccl_api() {
     static std::once_flag once;
     std::call_once(once, [] {
         void* h = nullptr;
+        // test only: SBE_RCCL_LIB names a stand-in with RCCL's symbols (tests/mock_rccl: the ranks
+        // of a communicator as threads of one process), so the multi-rank gather runs on one GPU
+        if (const char* alt = std::getenv("SBE_RCCL_LIB"); alt && *alt) {
+            h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+            if (!h) {
+                std::snprintf(api.err, sizeof(api.err), "SBE_RCCL_LIB not loadable: %s", dlerror());
+                return;
+            }
+        }
         for (const char* name : {"librccl.so.1", "librccl.so"})
             if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);  // the process's own RCCL first
         for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
