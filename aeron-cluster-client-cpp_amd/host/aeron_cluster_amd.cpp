@@ -143,8 +143,10 @@ void for_ranges(size_t n, size_t grain, F&& fn) {
     w.parallel_for(ntasks, [&](size_t t) { fn(n * t / ntasks, n * (t + 1) / ntasks); });
 }
 
-// Page-locked host blocks recycled by size class (powers of two from 64 KiB); hipHostMalloc costs
-// milliseconds per call for large blocks, so a block is allocated once and reused.
+// Page-locked host blocks recycled by size class (powers of two from 4 KiB); hipHostMalloc costs
+// milliseconds per call for large blocks, so a block is allocated once and reused.  Free blocks are
+// kept up to AERON_AMD_PINNED_CACHE_BYTES (default 4 GiB) in all; a block returned beyond that is
+// freed.  Blocks held by callers (EncodedBatch, ParsedBatch) do not count against the cap.
 class PinnedPool {
 public:
     static PinnedPool& get() {
@@ -152,7 +154,7 @@ public:
         return *p;
     }
     std::shared_ptr<void> take(size_t bytes) {
-        size_t cls = size_t(1) << 16;
+        size_t cls = size_t(1) << 12;
         while (cls < bytes) cls <<= 1;
         void* p = nullptr;
         {
@@ -172,7 +174,7 @@ private:
     void give(void* p, size_t cls) {
         {
             std::lock_guard<std::mutex> g(m_);
-            if (cached_ + cls <= kMaxCached) {
+            if (cached_ + cls <= max_cached_) {
                 free_[cls].push_back(p);
                 cached_ += cls;
                 return;
@@ -180,7 +182,10 @@ private:
         }
         (void)hipHostFree(p);
     }
-    static constexpr size_t kMaxCached = size_t(4) << 30;
+    PinnedPool() {
+        if (const char* e = std::getenv("AERON_AMD_PINNED_CACHE_BYTES")) max_cached_ = (size_t)std::max(0LL, std::atoll(e));
+    }
+    size_t max_cached_ = size_t(4) << 30;
     std::mutex m_;
     std::map<size_t, std::vector<void*>> free_;
     size_t cached_ = 0;
@@ -342,13 +347,20 @@ struct PipeGuard {
 
 // The device address of page-locked host memory (hipHostMalloc'd or registered), or nullptr when
 // it has none: kernels of the zero-copy path read their input and write their results there.
+// An interior pointer resolves through the start of its allocation.
 void* device_view(const void* host) {
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, const_cast<void*>(host), 0) != hipSuccess) {
+    void* start = nullptr;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                               (hipDeviceptr_t)const_cast<void*>(host)) != hipSuccess || !start) {
         (void)hipGetLastError();
         return nullptr;
     }
-    return d;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, start, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(d) + (static_cast<const uint8_t*>(host) - static_cast<const uint8_t*>(start));
 }
 
 // Batches up to this many staged bytes (one pipeline chunk) take the zero-copy path: the kernels
@@ -527,6 +539,15 @@ struct HostBytesAccess {
             h.block_ = PinnedPool::get().take(n * sizeof(T));
             h.p_ = static_cast<T*>(h.block_.get());
         }
+        h.n_ = n;
+        return h;
+    }
+    // n elements at p inside `block` (several arrays of one result share a block)
+    template <class T>
+    static HostArray<T> view(const std::shared_ptr<void>& block, void* p, size_t n) {
+        HostArray<T> h;
+        h.block_ = block;
+        h.p_ = n ? static_cast<T*>(p) : nullptr;
         h.n_ = n;
         return h;
     }
@@ -750,9 +771,8 @@ template <class Field, class U64, class U32, class Launch>
 EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, EncodePlan plan, Launch&& launch) {
     EncodedBatch b;
     Trace tr("encode");
-    b.offsets = HostBytesAccess::make<uint64_t>(n + 1);
-    b.status = HostBytesAccess::make<uint8_t>(n);
     if (n == 0) {
+        b.offsets = HostBytesAccess::make<uint64_t>(1);
         b.offsets[0] = 0;
         return b;
     }
@@ -776,7 +796,14 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
     const size_t C = chunk_records(n, (size_t)(pin[n] + pout[n]) / 2);
     const size_t K = (n + C - 1) / C;
     P.serial = K == 1;
-    b.bytes = HostBytesAccess::make((size_t)pout[n]);
+    {  // offsets | status | stream in one page-locked block (16-B aligned parts)
+        const size_t o_st = al16((n + 1) * 8), o_by = o_st + al16(n);
+        std::shared_ptr<void> blk = PinnedPool::get().take(o_by + (size_t)pout[n]);
+        uint8_t* base = static_cast<uint8_t*>(blk.get());
+        b.offsets = HostBytesAccess::view<uint64_t>(blk, base, n + 1);
+        b.status = HostBytesAccess::view<uint8_t>(blk, base + o_st, n);
+        b.bytes = HostBytesAccess::view<uint8_t>(blk, base + o_by, (size_t)pout[n]);
+    }
     // staging layout of records [a, a + m): arena | u32 lengths [m][nf] | u64 [m] | u32 [m]
     struct Stage {
         size_t o_len, o_u64, o_u32, bytes;
@@ -819,9 +846,12 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         if (s.bytes <= zero_copy_max_bytes()) {
             sl.pin.need(s.bytes);
             uint8_t* dp = static_cast<uint8_t*>(device_view(sl.pin.p));
-            uint8_t* dbytes = n && pout[n] ? static_cast<uint8_t*>(device_view(b.bytes.data())) : nullptr;
-            uint64_t* doff = static_cast<uint64_t*>(device_view(b.offsets.data()));
-            uint8_t* dst = static_cast<uint8_t*>(device_view(b.status.data()));
+            // offsets, status and stream share one block (above): one lookup for all three
+            uint8_t* const hb = reinterpret_cast<uint8_t*>(b.offsets.data());
+            uint8_t* const db = static_cast<uint8_t*>(device_view(hb));
+            uint8_t* dbytes = db && pout[n] ? db + (b.bytes.data() - hb) : nullptr;
+            uint64_t* doff = reinterpret_cast<uint64_t*>(db);
+            uint8_t* dst = db ? db + (b.status.data() - hb) : nullptr;
             if (dp && doff && dst && (dbytes || pout[n] == 0)) {
                 stage_fill(sl.pin.b(), s, 0, n);
                 tr.lap(tr.stage);

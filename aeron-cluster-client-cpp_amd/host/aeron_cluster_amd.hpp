@@ -20,10 +20,16 @@
 // plus batched overloads, which are the point of the GPU path: one launch per batch.
 //
 // Everything computes on the GPU.  There is no CPU codec here: without a gfx950 device every
-// entry point throws std::runtime_error("sbecodec: ...").  Host work is staging and result
-// building only: batches move through a two-stream pipeline (host threads stage chunk k+1 in
-// page-locked memory while chunk k is copied, coded and copied back), on min(16, cores) host
-// threads (AERON_AMD_HOST_THREADS).
+// codec entry point throws std::runtime_error("sbecodec: ...") (SBEUtils, SBEDecoder and the
+// header-only MessageParser helpers are host struct readers, as in the reference).  Host work is
+// staging and result building only, on min(16, cores) host threads (AERON_AMD_HOST_THREADS):
+//  - a batch of at most 65536 records and 8-32 MiB (AERON_AMD_CHUNK_BYTES) is one chunk; up to
+//    4 MiB staged (AERON_AMD_ZC_BYTES) it takes the zero-copy path: the kernels read the
+//    page-locked staging buffer and write the results straight into the page-locked result
+//    block over PCIe, one launch (encode: two) and one wait, no copy step;
+//  - larger batches are cut into chunks that flow through three HIP streams (copy-in, kernels,
+//    copy-out) three slots deep, so chunk k+1's H2D, chunk k's kernels and chunk k-1's D2H
+//    overlap while the host threads stage the next chunk.
 #pragma once
 
 #include <cstdint>
@@ -183,9 +189,15 @@ struct HostBytesAccess;
 struct Descriptors;
 }  // namespace detail
 
-// An array in page-locked host memory taken from a recycled pool: the device's DMA engines copy
-// results straight into it (no staging copy, no zero fill, no page faults on reuse), and the caller
-// reads it in place.  Copies share the block; the block returns to the pool with the last copy.
+// An array in page-locked host memory taken from a recycled pool: the device writes results
+// straight into it (DMA, or the kernels themselves on the zero-copy path: no staging copy, no zero
+// fill, no page faults on reuse), and the caller reads it in place.
+// Aliasing: copying a HostArray (or an EncodedBatch) copies a reference, not the bytes: the copies
+// share one block, and the arrays of one EncodedBatch (offsets, status, bytes) share one block.
+// to_vector() makes an independent copy.  Retention: the block (a power of two of at least 4 KiB)
+// stays page-locked while any copy lives, then returns to the pool, which keeps up to
+// AERON_AMD_PINNED_CACHE_BYTES (default 4 GiB) of free blocks for reuse; a caller that holds many
+// small results pins at least 4 KiB per result.
 template <class T>
 class HostArray {
 public:
