@@ -1483,7 +1483,10 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     constexpr bool kGuard = !(LY::kTM && LY::kPre == 0);
     bool rebal = false;
     uint32_t T = 0;
-    if (__ballot(n_mine > kCpl)) {
+#ifndef SBE_REBAL_MIN  // A/B: chunks per lane above which a window is rebalanced
+#define SBE_REBAL_MIN kCpl
+#endif
+    if (__ballot(n_mine > SBE_REBAL_MIN)) {
         const bool lead = q == 0 && nc > 0;
         const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
         const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));

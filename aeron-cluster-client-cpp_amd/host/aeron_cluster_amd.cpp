@@ -643,15 +643,18 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
     Pipeline::Slot& sl = P.slot[0];  // serial use (the pipeline is idle between calls)
     const uint64_t lo = rec_off[0], bytes = rec_off[n] - lo;
     const size_t o_data = al16((n + 1) * 8);
+    // the kernel reads its records from a 16-B aligned base: page-locked caller bytes are read from
+    // the 16-B boundary below the first record (offsets rebased to it); staged bytes start aligned
+    const uint64_t base = direct ? (lo & ~(uint64_t)15) : lo;
     sl.pin.need((direct ? o_data : o_data + (size_t)bytes) + 16);
     uint8_t* pin = sl.pin.b();
     uint64_t* ro = reinterpret_cast<uint64_t*>(pin);
     uint8_t* dpin = static_cast<uint8_t*>(device_view(pin));
     uint8_t* dblk = static_cast<uint8_t*>(device_view(d.block.get()));
-    const uint8_t* drec = direct ? static_cast<const uint8_t*>(device_view(data + lo)) : (dpin ? dpin + o_data : nullptr);
-    if (!dpin || !dblk || !drec) return false;
+    const uint8_t* drec = direct ? static_cast<const uint8_t*>(device_view(data + base)) : (dpin ? dpin + o_data : nullptr);
+    if (!dpin || !dblk || !drec || (reinterpret_cast<uintptr_t>(drec) & 15u)) return false;
     for_ranges(n + 1, 8192, [&](size_t x, size_t y) {
-        for (size_t i = x; i < y; ++i) ro[i] = rec_off[i] - lo;
+        for (size_t i = x; i < y; ++i) ro[i] = rec_off[i] - base;
     });
     if (!direct && bytes)
         for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) { copy_small(pin + o_data + x, data + lo + x, y - x); });
