@@ -60,8 +60,14 @@ constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWin
 // the workgroups (and so the bytes in flight) per CU: batches of records up to kMidAvg / kSmallAvg
 // bytes on average take a 14 / 8 KiB window (64 records of 204 B average fill 12.8 KiB; a tile past
 // the window takes a second one, as any tile does).
+#ifndef SBE_DEC_SMALL_AVG  // A/B builds only
+#define SBE_DEC_SMALL_AVG 112
+#endif
+#ifndef SBE_DEC_MID_AVG
+#define SBE_DEC_MID_AVG 204
+#endif
 constexpr uint32_t kWinMid = 14336, kWinSmall = 8192;
-constexpr uint64_t kMidAvg = 204, kSmallAvg = 112;
+constexpr uint64_t kMidAvg = SBE_DEC_MID_AVG, kSmallAvg = SBE_DEC_SMALL_AVG;
 
 // ------------------------------------------------------------------------------------------
 // LDS window.  Dword i of the window lives at i ^ ((i >> 6) & 28): within each 256-B row (64

@@ -73,11 +73,13 @@ def parse_args():
     p.add_argument("--verify", action="store_true", help="check one step against the oracle (small n)")
     p.add_argument("--settle-ms", type=float, default=500.0,
                    help="untimed round trips before the warmup steps, until the GPU has run this long")
-    p.add_argument("--event-every", type=int, default=-1,
-                   help="HIP events on the pack / decode dispatches of every k-th timed step (-1: "
-                        "max(1, min(10, steps // 20)), so that at least 20 launches are sampled whenever "
-                        "steps >= 20 (every launch below 200 steps); 0: none, diagnosis only: kernel "
-                        "times then come from an extra untimed pass)")
+    p.add_argument("--event-every", type=int, default=10,
+                   help="HIP events on the pack / decode dispatches of every k-th timed step (0: none).  "
+                        "A timed dispatch costs the GPU ~5 us, so the timed region samples sparsely; the "
+                        "roofline comes from the sampled pass that follows it (--sample-steps)")
+    p.add_argument("--sample-steps", type=int, default=0,
+                   help="steps of the sampled pass right after the timed region, HIP events on every pack / "
+                        "decode dispatch (0: max(steps, 20), at most 256)")
     return p.parse_args()
 
 
@@ -322,8 +324,8 @@ def verify_gathered(dst, dst_off, N, dev, ws, chunk=1 << 22):
 
 def main():
     args = parse_args()
-    if args.event_every < 0:
-        args.event_every = max(1, min(10, args.steps // 20))
+    if args.sample_steps <= 0:
+        args.sample_steps = min(256, max(args.steps, 20))
     if args.gpus > 1 and not launched_distributed():
         sys.exit(spawn_ranks(args.gpus))
     world, rank, local = setup_dist(args)
@@ -395,13 +397,15 @@ def main():
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
-    # the dominant kernels' durations, from the events the library recorded around them on the
-    # launch stream inside the timed region
-    if args.event_every == 0:  # diagnosis: kernel times from an extra, untimed pass
-        sbecodec.profile_enable(1)
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
+    # the in-region samples (every event_every-th step), then the sampled pass: the same steps on
+    # the same stream right after the timed region, HIP events on every pack / decode dispatch
+    # (hipExtLaunchKernel timestamps of the kernel itself); its mean is the roofline's duration
+    inreg_pack = sbecodec.profile_read(sbecodec.PROF_PACK) if args.event_every else []
+    inreg_deck = sbecodec.profile_read(sbecodec.PROF_DECODE) if args.event_every else []
+    sbecodec.profile_enable(1)
+    for _ in range(args.sample_steps):
+        step()
+    torch.cuda.synchronize()
     pack_samples = sbecodec.profile_read(sbecodec.PROF_PACK)
     deck_samples = sbecodec.profile_read(sbecodec.PROF_DECODE)
     pack_ms = float(np.mean(pack_samples))
@@ -432,10 +436,10 @@ def main():
 
         if pack_ms >= deck_ms:
             dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, bytes_all=ENC_BYTES_ALL,
-                       ms=pack_ms, samples=pack_samples)
+                       ms=pack_ms, samples=pack_samples, inreg=inreg_pack)
         else:
             dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES,
-                       bytes_all=DEC_BYTES_ALL, ms=deck_ms, samples=deck_samples)
+                       bytes_all=DEC_BYTES_ALL, ms=deck_ms, samples=deck_samples, inreg=inreg_deck)
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
@@ -455,10 +459,13 @@ def main():
                          "bytes_source": "SURVEY §8(d) algorithmic bytes per 256-B record",
                          "achieved_incl_offsets": gbs(dom["bytes_all"], dom["ms"]),
                          "bytes_per_record_incl_offsets": dom["bytes_all"],
-                         "timing": (f"HIP events on the kernel's dispatch in every {args.event_every}th timed step: "
-                                    f"{len(dom['samples'])} samples"
-                                    if args.event_every else "HIP events, untimed pass (diagnosis run)"),
+                         "timing": (f"HIP events on every dispatch of the kernel in {args.sample_steps} steps run right "
+                                    f"after the timed region (same stream, inputs and clocks): {len(dom['samples'])} "
+                                    f"samples; the timed region itself samples every {args.event_every}th step "
+                                    f"(kernel_ms_in_region, {len(dom['inreg'])} samples), since a timed dispatch "
+                                    f"costs the GPU ~5 us"),
                          "samples": len(dom["samples"]),
+                         "kernel_ms_in_region": float(np.mean(dom["inreg"])) if dom["inreg"] else None,
                          "kernel_ms_min": float(np.min(dom["samples"])),
                          "kernel_ms_median": float(np.median(dom["samples"])),
                          "kernel_ms_max": float(np.max(dom["samples"]))},

@@ -15,10 +15,13 @@ OUT = os.path.join(ROOT, "abl")
 VARIANTS = {
     "base": [],
     # record-lane composition: skip the literal bytes / the zone merges / everything after the gate
-    "nolit": [("    wsync();\n    if (!live) return true;\n    // literal bytes: q = 0",
-               "    wsync();\n    return true;\n    // literal bytes: q = 0")],
-    "nofix": [("    wsync();\n    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane);\n    wsync();\n    if (!live) return true;",
-               "    wsync();\n    if (!live) return true;")],
+    "nolit": [("    ph.lap(2);\n    if (!live) return true;\n    // literal bytes: q = 0",
+               "    ph.lap(2);\n    return true;\n    // literal bytes: q = 0")],
+    "nofix": [("    ph.lap(1);\n    zone_fixup<LY>(wout, inb, rt, wlen, nb, lane, ra, rb);\n", "    ph.lap(1);\n")],
+    # record-lane composition: the chunk groups left out (the rebalance still runs)
+    "nogroups": [("    int32_t i0 = 0;\n    for (; __ballot(i0 + 3 < n_mine); i0 += 4)", "    int32_t i0 = 0;\n    for (; __ballot(i0 + 3 < n_mine && n_mine < 0); i0 += 4)"),
+                 ("    if (__ballot(i0 + 1 < n_mine)) {\n        group(", "    if (__ballot(i0 + 1 < n_mine && n_mine < 0)) {\n        group("),
+                 ("    if (__ballot(i0 < n_mine)) group(", "    if (__ballot(i0 < n_mine && n_mine < 0)) group(")],
     "nocompose": [("    if (__ballot(!ok)) return false;\n", "    if (__ballot(!ok)) return false;\n    return true;\n")],
     # decode tiles of 48 / 32 records (lanes past the tile idle) in 12 / 8 KiB windows: more
     # workgroups per CU (LDS-bound at 16 KiB) against idle parse lanes
