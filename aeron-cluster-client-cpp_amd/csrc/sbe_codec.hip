@@ -31,7 +31,9 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>  // types only: the library is dlopen-ed (rccl_api)
 
+#include <chrono>
 #include <mutex>
+#include <new>
 #include <type_traits>
 
 #include <cstdint>
@@ -588,6 +590,8 @@ struct TileSt {  // prepared per-lane state of one tile; offsets are bytes from 
     uintptr_t gsrc[5];             // gather mode (and kLenPub packed): absolute string addresses
     bool wrapped;                  // kLenPub packed: some record's input strings are longer than its
                                    // output ones (a length >= 65536): compose from gsrc (uniform)
+    uint32_t agg_out;              // output bytes of the tile's records (uniform)
+    uint64_t tot_in;               // packed: input bytes of the tile's records, 64-bit (uniform)
 };
 
 // sb_next: the first superblock whose total this workgroup has not loaded yet (tiles come in
@@ -620,15 +624,32 @@ __device__ __forceinline__ TileIn tile_load(const EncArgs& a, uint64_t tile, int
     return x;
 }
 
+// The tile of kRpt records from record r_first (records at or past rend are not part of it), its
+// output starting at base_out and its packed input at arena + base_in.
+template <class LY, bool kPacked, int kLen>
+__device__ __forceinline__ TileSt tile_prepare_at(const EncArgs& a, const TileIn& x, uint64_t r_first, uint64_t rend,
+                                                  int lane, uint64_t base_out, uint64_t base_in);
+
 // sp_out / sp_in: running totals of the superblocks before this workgroup's current tile
 template <class LY, bool kPacked, int kLen>
 __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x, uint64_t tile, int lane,
                                                uint64_t& sp_out, uint64_t& sp_in) {
     SBE_TILE_SHAPE(LY);
+    sp_out += wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull);
+    if (kPacked) sp_in += wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull);
+    const uint64_t base_out = uniform64(sp_out + x.to);
+    const uint64_t base_in = kPacked ? uniform64(sp_in + x.ti) : 0ull;
+    return tile_prepare_at<LY, kPacked, kLen>(a, x, tile * kRpt, a.n, lane, base_out, base_in);
+}
+
+template <class LY, bool kPacked, int kLen>
+__device__ __forceinline__ TileSt tile_prepare_at(const EncArgs& a, const TileIn& x, uint64_t r_first, uint64_t rend,
+                                                  int lane, uint64_t base_out, uint64_t base_in) {
+    SBE_TILE_SHAPE(LY);
     TileSt S;
     const int q = lane % kLpr;
-    const uint64_t r = tile * kRpt + lane / kLpr;
-    const bool valid = r < a.n;
+    const uint64_t r = r_first + lane / kLpr;
+    const bool valid = r < rend;
     uint64_t sum = 0, sum_in = 0;
     uint8_t st = SBE_ENC_OK;
 #pragma unroll
@@ -647,16 +668,14 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
     const uint32_t rec_out = (valid && st == SBE_ENC_OK) ? ovh + (uint32_t)sum : 0u;
     const uint64_t rec_in = (kPacked && valid) ? sum_in : 0ull;
     S.wrapped = kLen == kLenPub && kPacked && __ballot(sum_in != sum) != 0;
-    sp_out += wave_sum64((uint32_t)lane < x.pcount ? x.po : 0ull);
-    if (kPacked) sp_in += wave_sum64((uint32_t)lane < x.pcount ? x.pi : 0ull);
-    const uint64_t base_out = uniform64(sp_out + x.to);
-    const uint64_t base_in = kPacked ? uniform64(sp_in + x.ti) : 0ull;
     const uint32_t lo_out = q == 0 ? rec_out : 0u;
     const uint32_t inc_out = wave_incl_scan(lo_out, lane);
     const uint32_t agg_out = lane_u32(inc_out, kWave - 1);
     // the record's lead lane's value (kLpr = 2: quad_perm [0,0,2,2])
     S.rs = kLpr == 2 ? dpp0<0xa0>(inc_out - lo_out) : inc_out - lo_out;
     S.rec_out = rec_out;
+    S.agg_out = agg_out;
+    S.tot_in = 0;
     if (kPacked) {
         // every record of the tile encodable: input offsets follow the output ones (34 B apart
         // per record); otherwise (E109 / past the end) a 64-bit scan of the input sizes
@@ -665,11 +684,13 @@ __device__ __forceinline__ TileSt tile_prepare(const EncArgs& a, const TileIn& x
             S.in0 = S.rs - ovh0 * (uint32_t)(lane / kLpr);
             const uint64_t agg_in = agg_out - (uint64_t)ovh0 * kRpt;
             S.agg_in = (uint32_t)agg_in;
+            S.tot_in = agg_in;
         } else {
             const uint64_t lo_in = q == 0 ? rec_in : 0ull;
             const uint64_t inc_in = wave_incl_scan64(lo_in, lane);
             const uint64_t agg_in = lane_u64(inc_in, kWave - 1);
             S.agg_in = agg_in < 0x7fffffffull ? (uint32_t)agg_in : 0x7fffffffu;
+            S.tot_in = agg_in;
             const uint64_t ex = inc_in - lo_in;
             S.in0 = kLpr == 2 ? ((uint64_t)dpp0<0xa0>((uint32_t)(ex >> 32)) << 32) | dpp0<0xa0>((uint32_t)ex) : ex;
         }
@@ -1715,22 +1736,29 @@ __device__ __forceinline__ Win tile_window(const TileSt& S, int ra, int lane, ui
     return W;
 }
 
+// The pack loop's LDS (one workgroup): output window, staged input, record / bucket tables.
+template <class LY, bool kPacked>
+struct PackLds {
+    __attribute__((aligned(16))) uint8_t wout[kWoutBytes];
+    __attribute__((aligned(16))) uint8_t win[kPacked ? kWinBytes : 16];
+    __attribute__((aligned(16))) int32_t rt[kPacked ? LY::kRpt * kRecEnt : 4];
+    int32_t bk[kPacked ? kWave : 1];
+    uint64_t sbase[kPacked ? LY::kRpt : 1];
+};
+
+// Tiles first, first + G, ... of the batch (the pack kernel: first = blockIdx.x, G = gridDim.x;
+// the serve kernel: 0, 1 for a one-tile batch).
 template <class LY, bool kPacked, int kLen>
-__global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
+__device__ __forceinline__ void enc_pack_run(const EncArgs& a, uint64_t first, uint64_t G, PackLds<LY, kPacked>& L) {
     SBE_TILE_SHAPE(LY);
-    __shared__ __attribute__((aligned(16))) uint8_t wout_arr[kWoutBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t win_raw[kPacked ? kWinBytes : 16];
-    __shared__ __attribute__((aligned(16))) int32_t rt_arr[kPacked ? kRpt * kRecEnt : 4];
-    __shared__ int32_t bk_arr[kPacked ? kWave : 1];
-    __shared__ uint64_t sbase[kPacked ? kRpt : 1];
-    lds_u8* const wout = (lds_u8*)wout_arr;
-    lds_u8* const win_in = (lds_u8*)win_raw + kInSlack;
-    lds_i32* const rt = (lds_i32*)rt_arr;
-    lds_i32* const bk = (lds_i32*)bk_arr;
+    lds_u8* const wout = (lds_u8*)L.wout;
+    lds_u8* const win_in = (lds_u8*)L.win + kInSlack;
+    lds_i32* const rt = (lds_i32*)L.rt;
+    lds_i32* const bk = (lds_i32*)L.bk;
+    uint64_t* const sbase = L.sbase;
     const int lane = threadIdx.x;
     const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
-    const uint64_t G = gridDim.x;
-    uint64_t t = blockIdx.x;
+    uint64_t t = first;
     if (t >= ntiles) return;
     Ph ph;
     ph.start();
@@ -1833,6 +1861,174 @@ __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArg
         fast = fast_n;
     }
     ph.put(lane);
+}
+
+// ---- virtual tiles: every window full -----------------------------------------------------
+// Workgroup w owns the contiguous tiles [w T / G, (w + 1) T / G) and walks their records in order
+// with running output / input offsets.  Each step takes the kRpt records from the first one not
+// yet written (a "virtual tile", at any record index) and writes ONE output window: the records
+// from its first that fit kEW bytes, so every window but a workgroup's last is full.  (Tile-aligned
+// steps leave a tile's last window part full: a 32-record tile of ~380-B records is a full 8 KiB
+// window and a ~4 KiB one, and a window costs about the same whatever it holds.)  The records
+// after the window start the next step; their lengths are loaded one step ahead, like the tiles'.
+// A virtual tile the fast path cannot take (a record longer than a window, gather mode, a
+// PUBLISH_TOPIC length wrap) is written whole, window by window, as before.
+template <class LY, bool kPacked>
+__device__ __forceinline__ TileIn vt_load(const EncArgs& a, uint64_t r0, int lane) {
+    SBE_TILE_SHAPE(LY);
+    TileIn x;
+    uint64_t r = r0 + (uint64_t)(lane / kLpr);
+    r = r < a.n ? r : a.n - 1;  // unconditional loads at a clamped index (tile_load)
+#pragma unroll
+    for (int f = 0; f < 5; ++f) x.L[f] = f < LY::kNF ? a.str_len[LY::kNF * r + f] : 0u;
+    x.ts = a.timestamp[r];
+    x.tid = LY::kTM ? 0u : a.topic_id[r];
+    x.to = x.ti = x.po = x.pi = 0;
+    x.pcount = 0;
+    return x;
+}
+
+// bytes before the first record of tile t0 (output, packed input): the superblock totals before it
+// plus the tile's prefix inside its superblock (sbe_enc_sums)
+__device__ __forceinline__ void vt_base(const EncArgs& a, uint64_t t0, bool packed, int lane, uint64_t& bo, uint64_t& bi) {
+    const uint64_t nsb = t0 / kTilesPerSb;
+    uint64_t so = 0, si = 0;
+    for (uint64_t j = (uint64_t)lane; j < nsb; j += kWave) {
+        so += a.bsum[2 * j];
+        if (packed) si += a.bsum[2 * j + 1];
+    }
+    bo = uniform64(wave_sum64(so) + a.tsum[2 * t0]);
+    bi = packed ? uniform64(wave_sum64(si) + a.tsum[2 * t0 + 1]) : 0ull;
+}
+
+template <class LY, bool kPacked, int kLen>
+__device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first, uint64_t G, PackLds<LY, kPacked>& L) {
+    SBE_TILE_SHAPE(LY);
+    lds_u8* const wout = (lds_u8*)L.wout;
+    lds_u8* const win_in = (lds_u8*)L.win + kInSlack;
+    lds_i32* const rt = (lds_i32*)L.rt;
+    lds_i32* const bk = (lds_i32*)L.bk;
+    uint64_t* const sbase = L.sbase;
+    const int lane = threadIdx.x;
+    const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
+    const uint64_t t_lo = first * ntiles / G, t_hi = (first + 1) * ntiles / G;
+    if (t_lo >= t_hi) return;
+    const uint64_t r_hi = t_hi * kRpt < a.n ? t_hi * kRpt : a.n;  // this workgroup's records end here
+    uint64_t r = t_lo * kRpt;
+    Ph ph;
+    ph.start();
+    uint64_t bo, bi;
+    vt_base(a, t_lo, kPacked, lane, bo, bi);
+    const uintptr_t sink = reinterpret_cast<uintptr_t>(a.sink);
+    // records written by the step of tile S with window W, and the offsets after them
+    auto advance = [&](const TileSt& S_, const Win& W_, bool fast_, uint64_t& bo_, uint64_t& bi_) -> uint32_t {
+        const uint32_t k = fast_ ? (uint32_t)W_.rb : (uint32_t)kRpt;
+        if (k < (uint32_t)kRpt) {
+            bo_ += lane_u32(S_.rs, (int)k * kLpr);
+            if (kPacked) bi_ += lane_u64(S_.in0, (int)k * kLpr);
+        } else {
+            bo_ += S_.agg_out;
+            if (kPacked) bi_ += S_.tot_in;
+        }
+        return k;
+    };
+    TileIn x = vt_load<LY, kPacked>(a, r, lane);
+    TileSt S = tile_prepare_at<LY, kPacked, kLen>(a, x, r, r_hi, lane, bo, bi);
+    uint4 I[kStageRegs];
+    Win W{0, kRpt, 0, 0, 0, sink, 0};
+    bool fast = kPacked && !S.wrapped && !tile_big<LY>(S, lane);
+    if (fast) W = tile_window<LY>(S, 0, lane, sink);
+    uint64_t rn = r + advance(S, W, fast, bo, bi);  // bo / bi: the next step's offsets
+    if (kPacked) {
+        stage_issue(W.swb, W.nb, lane, I);
+        stage_write(win_in, W.nb, lane, I);
+    }
+    x = vt_load<LY, kPacked>(a, rn, lane);
+
+    for (;;) {
+        const bool have_next = rn < r_hi;
+        TileSt Sn;
+        Win Wn{0, kRpt, 0, 0, 0, sink, 0};
+        bool fast_n = false;
+        uint64_t rnn = rn;
+        if (have_next) {
+            Sn = tile_prepare_at<LY, kPacked, kLen>(a, x, rn, r_hi, lane, bo, bi);
+            ph.lap(7);
+            fast_n = kPacked && !Sn.wrapped && !tile_big<LY>(Sn, lane);
+            if (fast_n) Wn = tile_window<LY>(Sn, 0, lane, sink);
+            rnn = rn + advance(Sn, Wn, fast_n, bo, bi);
+            x = vt_load<LY, kPacked>(a, rnn, lane);
+        }
+        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
+        ph.lap(0);
+        if (fast) {
+            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb, ph)) {
+                pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
+                ph.lap(6);
+            } else {
+                ph.lap(3);
+            }
+            wsync();
+            store_window<(LY::kStoreRows0 < kStoreRows ? LY::kStoreRows0 : kStoreRows)>(a.out, wout, S.T0 + W.A, S.T0 + (int64_t)W.wrel,
+                                          S.T0 + (int64_t)(W.wrel + W.wlen), lane);
+            wsync();
+            ph.lap(4);
+        } else {  // the whole virtual tile, window by window (records longer than a window, gather mode)
+            const int32_t wrel0 = -(int32_t)(S.T0 & 15);
+            for (int32_t wrel = wrel0; wrel < (int32_t)S.len; wrel += kEW) {
+                const int32_t we_rel = wrel + kEW < (int32_t)S.len ? wrel + kEW : (int32_t)S.len;
+                uintptr_t sw = 0;
+                int32_t nbw = 0;
+                if (kPacked && !S.wrapped) {
+                    stage_range<LY>(S, wrel, lane, sw, nbw);
+                    for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
+                        uint4 J[3];
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const uint32_t ch = lane + kWave * (k0 + k);
+                            J[k] = (int32_t)(16 * ch) < nbw ? gload128(sw + 16u * ch) : make_uint4(0, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            const uint32_t ch = lane + kWave * (k0 + k);
+                            if ((int32_t)(16 * ch) < nbw) lds_store16(win_in + 16 * ch, J[k]);
+                        }
+                    }
+                }
+                if (kPacked && !S.wrapped) {
+                    pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, wrel, we_rel - wrel, sw, nbw, lane);
+                } else {
+                    wsync();
+                    compose<LY, false>(a, wout, win_in, S, wrel, we_rel, sw, nbw);
+                }
+                wsync();
+                store_window(a.out, wout, S.T0, S.T0 + (int64_t)wrel, S.T0 + (uint64_t)we_rel, lane);
+                wsync();
+            }
+            ph.lap(6);
+        }
+        if (!have_next) break;
+        if (kPacked) stage_write(win_in, Wn.nb, lane, I);  // after the compose above read win_in
+        wsync();
+        ph.lap(5);
+        S = Sn;
+        W = Wn;
+        fast = fast_n;
+        rn = rnn;
+    }
+    ph.put(lane);
+}
+
+#ifndef SBE_PACK_VT
+#define SBE_PACK_VT 1
+#endif
+template <class LY, bool kPacked, int kLen>
+__global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
+    __shared__ PackLds<LY, kPacked> lds;
+    if (SBE_PACK_VT)
+        enc_pack_run_vt<LY, kPacked, kLen>(a, blockIdx.x, gridDim.x, lds);
+    else
+        enc_pack_run<LY, kPacked, kLen>(a, blockIdx.x, gridDim.x, lds);
 }
 
 #include "seqnum.hpp"
@@ -2574,11 +2770,12 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
 #ifndef SBE_DEC_MINW
 #define SBE_DEC_MINW 3
 #endif
-template <uint32_t kMode, uint32_t kWin>
-__global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
-    __shared__ uint32_t win[kWin / 4];
+// One 64-record tile (the decode kernel: tile = blockIdx.x; the serve kernel: tile 0 of a one-tile
+// batch); win is the workgroup's LDS window of kWin bytes.
+template <uint32_t kMode, uint32_t kWin, bool kServe = false>
+__device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32_t* win) {
     const int lane = threadIdx.x;
-    const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t t0 = tile * kTile;
     const uint64_t r = t0 + (uint64_t)lane;
     const bool valid = r < a.n;
     const uint64_t last = t0 + kTile < a.n ? t0 + kTile : a.n;
@@ -2685,8 +2882,16 @@ __global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs
     // backslash), evaluated from HBM by the lanes that hold one
     if (kMode == SBE_DEC_PARSE_MESSAGE && a.seq) {
         const bool cand = valid && d.status == SBE_ST_TM && (d.flags & kSeqCand);
-        if (__ballot(cand) && cand) a.seq[r] = json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
+        if (__ballot(cand) && cand)
+            a.seq[r] = kServe ? json_seq_eval_call_serve(a.in + rs + d.off[3], d.len[3])
+                              : json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
     }
+}
+
+template <uint32_t kMode, uint32_t kWin>
+__global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
+    __shared__ uint32_t win[kWin / 4];
+    dec_tile<kMode, kWin>(a, blockIdx.x, win);
 }
 
 thread_local char g_last_error[256] = "";
@@ -3156,21 +3361,33 @@ void enc_launch_k(const EncArgs& a, uint64_t sbs, uint64_t tiles, hipStream_t s)
     prof_commit(0, e0);
 }
 
-// Argument checks, workspace carving and the two launches (sums, pack) of one encode call.
+// Argument checks shared by the batch and serve entry points (the workspace aside).
 template <class LY>
-int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out, uint64_t out_capacity,
-               uint64_t* out_off, uint8_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+int enc_check(const EncReq& q, uint64_t n, uint32_t flags, const uint8_t* out, const uint64_t* out_off) {
     if (!out_off) return SBE_EINVAL;
     if (flags & ~(SBE_ENC_REF_TRUNCATE8 | SBE_ENC_PUBLISH_TOPIC)) return SBE_EINVAL;
     if (!LY::kTM && flags) return SBE_EINVAL;
     if ((flags & SBE_ENC_PUBLISH_TOPIC) && ((flags & SBE_ENC_REF_TRUNCATE8) || LY::kPre)) return SBE_EINVAL;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
+    if (n == 0) return SBE_OK;
     if (!q.str_len || !q.ts || !q.arena || !out) return SBE_EINVAL;
     if ((reinterpret_cast<uintptr_t>(out) & 15u) || (reinterpret_cast<uintptr_t>(out_off) & 7u)) return SBE_EINVAL;
+    if ((n + LY::kRpt - 1) / LY::kRpt > kMaxTiles) return SBE_EINVAL;
+    return SBE_OK;
+}
+
+inline int enc_len_mode(uint32_t flags) {
+    return (flags & SBE_ENC_REF_TRUNCATE8) ? kLenRef : (flags & SBE_ENC_PUBLISH_TOPIC) ? kLenPub : kLenWire;
+}
+
+// Argument checks, workspace carving and the two launches (sums, pack) of one encode call.
+template <class LY>
+int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out, uint64_t out_capacity,
+               uint64_t* out_off, uint8_t* status, void* workspace, size_t workspace_bytes, void* stream) {
+    if (const int rc = enc_check<LY>(q, n, flags, out, out_off)) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (n == 0) return record_hip(hipMemsetAsync(out_off, 0, sizeof(uint64_t), s));
     const uint64_t sbs = (n + LY::kSbRec - 1) / LY::kSbRec;
     const uint64_t tiles = (n + LY::kRpt - 1) / LY::kRpt;
-    if (tiles > kMaxTiles) return SBE_EINVAL;
     if (!workspace || workspace_bytes < enc_workspace_size(n)) return SBE_ENOSPC;
     if (reinterpret_cast<uintptr_t>(workspace) & 15u) return SBE_EINVAL;
     uint64_t* ws = static_cast<uint64_t*>(workspace);
@@ -3178,7 +3395,7 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
               out,     out_capacity, out_off, status, ws, ws + 2 * sbs * kTilesPerSb,
               reinterpret_cast<uint8_t*>(ws + 2 * sbs * (kTilesPerSb + 1))};
     const bool packed = q.str_off == nullptr;
-    const int len = (flags & SBE_ENC_REF_TRUNCATE8) ? kLenRef : (flags & SBE_ENC_PUBLISH_TOPIC) ? kLenPub : kLenWire;
+    const int len = enc_len_mode(flags);
     if constexpr (LY::kTM) {
         if (packed) {
             if (len == kLenWire) enc_launch_k<LY, true, kLenWire>(a, sbs, tiles, s);
@@ -3194,6 +3411,198 @@ int enc_launch(const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
         else enc_launch_k<LY, false, kLenWire>(a, sbs, tiles, s);
     }
     return record_hip(hipGetLastError());
+}
+
+// Argument checks of a decode call (batch and serve entry points).
+int dec_check(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode, const sbe_decoded* out) {
+    if (mode != SBE_DEC_PARSE_MESSAGE && mode != SBE_DEC_ON_EGRESS && mode != SBE_DEC_LITE) return SBE_EINVAL;
+    if (n == 0) return SBE_OK;
+    if (!in || !rec_off || !out || !out->status || !out->flags || !out->hdr || !out->ts || !out->view_off ||
+        !out->view_len)
+        return SBE_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(in) & 15u) || (reinterpret_cast<uintptr_t>(rec_off) & 7u) ||
+        (reinterpret_cast<uintptr_t>(out->hdr) & 7u) || (reinterpret_cast<uintptr_t>(out->ts) & 7u) ||
+        (reinterpret_cast<uintptr_t>(out->view_off) & 3u) || (reinterpret_cast<uintptr_t>(out->view_len) & 3u))
+        return SBE_EINVAL;
+    if ((n + kTile - 1) / kTile > kMaxTiles) return SBE_EINVAL;
+    if (mode == SBE_DEC_PARSE_MESSAGE && out->seq && (reinterpret_cast<uintptr_t>(out->seq) & 7u)) return SBE_EINVAL;
+    return SBE_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Serve kernel: one resident wave that polls a page-locked request slot (sbecodec.h, "small-batch
+// serve kernel").  A request is one EncArgs or DecArgs; the wave runs the same device code as the
+// batch kernels over the whole batch (decode: dec_tile over its tiles; encode: the pack loop as
+// workgroup 0 of 1, whose running offsets make the tile sums unnecessary), then publishes done_seq.
+// ------------------------------------------------------------------------------------------
+enum : uint32_t {
+    kSvShutdown = 1,
+    kSvDecParse, kSvDecEgress, kSvDecLite,
+    kSvTmWire, kSvTmRef, kSvTmPub, kSvTmsWire, kSvTmsRef, kSvLite2, kSvLite3
+};
+
+struct ServeReq {
+    uint32_t op, pad;
+    EncArgs e;
+    DecArgs d;
+};
+constexpr int kReqWords = (int)(sizeof(ServeReq) / 4);
+static_assert(sizeof(ServeReq) % 4 == 0 && kReqWords <= kWave, "a request is read one dword per lane");
+
+// Host-written words and device-written words on separate 64-B lines.
+struct ServeSlot {
+    alignas(64) uint32_t req_seq;  // host → device: sequence number of the posted request
+    alignas(64) uint32_t done_seq; // device → host: the last request completed
+    uint32_t alive;                // 1 from the host's launch until the kernel's exit
+    alignas(64) ServeReq req;
+};
+
+union ServeLds {
+    PackLds<LayTM, true> tm;
+    PackLds<LayTMS, true> tms;
+    PackLds<LayL2, true> l2;
+    PackLds<LayL3, true> l3;
+    uint32_t win[kWin / 4];
+};
+
+__device__ __forceinline__ uint32_t sys_acquire(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_release(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <uint32_t kMode>
+__device__ __forceinline__ void serve_decode(const DecArgs& a, uint32_t* win) {
+    for (uint64_t t = 0; t * kTile < a.n; ++t) {
+        dec_tile<kMode, kWin, true>(a, t, win);
+        wsync();
+    }
+}
+
+template <class LY, int kLen>
+__device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>& L) {
+    if (a.n == 0) {
+        if (threadIdx.x == 0) a.out_off[0] = 0;
+        return;
+    }
+    enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L);
+}
+
+// idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits.
+__global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks) {
+    __shared__ ServeLds lds;
+    const int lane = threadIdx.x;
+    uint32_t last = __builtin_amdgcn_readfirstlane(sys_acquire(&slot->done_seq));
+    uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t seq = __builtin_amdgcn_readfirstlane(sys_acquire(&slot->req_seq));
+        if (seq == last) {
+            if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) break;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        // the request, one dword per lane (after the acquire: fresh from host memory)
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&slot->req);
+        const uint32_t v = lane < kReqWords ? __builtin_nontemporal_load(w + lane) : 0u;
+        union {
+            ServeReq r;
+            uint32_t u[kReqWords];
+        } q;
+#pragma unroll
+        for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
+        switch (q.r.op) {
+            case kSvDecParse: serve_decode<SBE_DEC_PARSE_MESSAGE>(q.r.d, lds.win); break;
+            case kSvDecEgress: serve_decode<SBE_DEC_ON_EGRESS>(q.r.d, lds.win); break;
+            case kSvDecLite: serve_decode<SBE_DEC_LITE>(q.r.d, lds.win); break;
+            case kSvTmWire: serve_encode<LayTM, kLenWire>(q.r.e, lds.tm); break;
+            case kSvTmRef: serve_encode<LayTM, kLenRef>(q.r.e, lds.tm); break;
+            case kSvTmPub: serve_encode<LayTM, kLenPub>(q.r.e, lds.tm); break;
+            case kSvTmsWire: serve_encode<LayTMS, kLenWire>(q.r.e, lds.tms); break;
+            case kSvTmsRef: serve_encode<LayTMS, kLenRef>(q.r.e, lds.tms); break;
+            case kSvLite2: serve_encode<LayL2, kLenWire>(q.r.e, lds.l2); break;
+            case kSvLite3: serve_encode<LayL3, kLenWire>(q.r.e, lds.l3); break;
+            default: break;
+        }
+        wsync();
+        __threadfence_system();  // every lane's result stores reach memory before done_seq
+        if (lane == 0) sys_release(&slot->done_seq, seq);
+        last = seq;
+        if (q.r.op == kSvShutdown) break;
+        t_idle = __builtin_amdgcn_s_memrealtime();
+    }
+    __threadfence_system();
+    if (lane == 0) sys_release(&slot->alive, 0u);
+}
+
+}  // namespace
+
+struct sbe_server {
+    ServeSlot* h = nullptr;  // page-locked slot, host address
+    ServeSlot* d = nullptr;  // its device address
+    uint64_t* ws = nullptr;  // device: zero tile sums (2 u64, never written) + the pack's sink
+    hipStream_t stream = nullptr;
+    uint32_t seq = 0;
+    uint64_t idle_ticks = 0;
+    uint64_t requests = 0, launches = 0;
+};
+
+namespace {
+
+constexpr size_t kServeWsBytes = 16 + kSinkBytes + 16;
+
+int serve_launch(sbe_server* s) {
+    __atomic_store_n(&s->h->alive, 1u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(sbe_serve_kernel, dim3(1), dim3(kWave), 0, s->stream, s->d, s->idle_ticks);
+    ++s->launches;
+    return record_hip(hipGetLastError());
+}
+
+// Post one request and wait for its completion (relaunching the kernel whenever it is not running).
+int serve_call(sbe_server* s, const ServeReq& r) {
+    if (!s || !s->h) return SBE_EINVAL;
+    ServeSlot* h = s->h;
+    std::memcpy(&h->req, &r, sizeof r);
+    const uint32_t seq = ++s->seq;
+    __atomic_store_n(&h->req_seq, seq, __ATOMIC_RELEASE);
+    ++s->requests;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&h->done_seq, __ATOMIC_ACQUIRE) == seq) return SBE_OK;
+        if (__atomic_load_n(&h->alive, __ATOMIC_ACQUIRE) == 0) {
+            // exited (idle): it may have answered just before, else start one
+            if (__atomic_load_n(&h->done_seq, __ATOMIC_ACQUIRE) == seq) return SBE_OK;
+            if (const int rc = serve_launch(s)) return rc;
+        }
+        if ((spin & 4095) == 4095) {
+            const hipError_t e = hipStreamQuery(s->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return record_hip(e);
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                std::snprintf(g_last_error, sizeof g_last_error, "serve request %u timed out", seq);
+                return SBE_EHIP;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+template <class LY>
+int serve_encode_req(sbe_server* s, const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out,
+                     uint64_t out_capacity, uint64_t* out_off, uint8_t* status, uint32_t op) {
+    if (!s) return SBE_EINVAL;
+    if (const int rc = enc_check<LY>(q, n, flags, out, out_off)) return rc;
+    if (n > SBE_SERVE_MAX_RECORDS || (n && q.str_off)) return SBE_EINVAL;
+    ServeReq r{};
+    r.op = op;
+    r.e = EncArgs{q.arena, nullptr, q.str_len, q.ts, q.tid, q.tmpl, q.term_id, q.sess_id, n, ts_default,
+                  out, out_capacity, out_off, status, s->ws, s->ws, reinterpret_cast<uint8_t*>(s->ws + 2)};
+    return serve_call(s, r);
+}
+
+uint32_t serve_tm_op(bool session, uint32_t flags) {
+    const int len = enc_len_mode(flags);
+    if (session) return len == kLenRef ? kSvTmsRef : kSvTmsWire;
+    return len == kLenRef ? kSvTmRef : len == kLenPub ? kSvTmPub : kSvTmWire;
 }
 
 }  // namespace
@@ -3278,18 +3687,9 @@ int sbe_encode_lite_batch(const sbe_lite_batch* in, uint64_t n, uint32_t templat
 
 int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint64_t in_bytes, uint32_t mode,
                            const sbe_decoded* out, void* stream) {
-    if (mode != SBE_DEC_PARSE_MESSAGE && mode != SBE_DEC_ON_EGRESS && mode != SBE_DEC_LITE) return SBE_EINVAL;
+    if (const int rc = dec_check(in, rec_off, n, mode, out)) return rc;
     if (n == 0) return SBE_OK;
-    if (!in || !rec_off || !out || !out->status || !out->flags || !out->hdr || !out->ts || !out->view_off ||
-        !out->view_len)
-        return SBE_EINVAL;
-    if ((reinterpret_cast<uintptr_t>(in) & 15u) || (reinterpret_cast<uintptr_t>(rec_off) & 7u) ||
-        (reinterpret_cast<uintptr_t>(out->hdr) & 7u) || (reinterpret_cast<uintptr_t>(out->ts) & 7u) ||
-        (reinterpret_cast<uintptr_t>(out->view_off) & 3u) || (reinterpret_cast<uintptr_t>(out->view_len) & 3u))
-        return SBE_EINVAL;
     const uint64_t tiles = (n + kTile - 1) / kTile;
-    if (tiles > kMaxTiles) return SBE_EINVAL;
-    if (mode == SBE_DEC_PARSE_MESSAGE && out->seq && (reinterpret_cast<uintptr_t>(out->seq) & 7u)) return SBE_EINVAL;
     DecArgs a{in,           rec_off,       n,
               out->status,  out->flags,    out->hdr,
               out->ts,      out->view_off, out->view_len,
@@ -3329,6 +3729,102 @@ int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t 
 int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out, void* stream) {
     return sbe_decode_batch_sized(in, rec_off, n, 0, mode, out, stream);
+}
+
+int sbe_server_create(sbe_server** srv, uint32_t idle_us) {
+    if (!srv) return SBE_EINVAL;
+    *srv = nullptr;
+    sbe_server* s = new (std::nothrow) sbe_server;
+    if (!s) return SBE_EINVAL;
+    s->idle_ticks = 100ull * (idle_us ? idle_us : 20000u);
+    void* h = nullptr;
+    void* d = nullptr;
+    hipError_t e = hipHostMalloc(&h, sizeof(ServeSlot), hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) {
+        std::memset(h, 0, sizeof(ServeSlot));
+        e = hipHostGetDevicePointer(&d, h, 0);
+    }
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->ws), kServeWsBytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemsetAsync(s->ws, 0, kServeWsBytes, s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    s->h = static_cast<ServeSlot*>(h);
+    s->d = static_cast<ServeSlot*>(d);
+    if (e != hipSuccess) {
+        const int rc = record_hip(e);
+        sbe_server_destroy(s);
+        return rc;
+    }
+    *srv = s;
+    return SBE_OK;
+}
+
+int sbe_server_destroy(sbe_server* s) {
+    if (!s) return SBE_OK;
+    int rc = SBE_OK;
+    if (s->h && s->stream && __atomic_load_n(&s->h->alive, __ATOMIC_ACQUIRE)) {
+        ServeReq r{};
+        r.op = kSvShutdown;
+        rc = serve_call(s, r);
+    }
+    if (s->stream) {
+        const hipError_t e = hipStreamSynchronize(s->stream);
+        if (rc == SBE_OK && e != hipSuccess) rc = record_hip(e);
+        (void)hipStreamDestroy(s->stream);
+    }
+    if (s->ws) (void)hipFree(s->ws);
+    if (s->h) (void)hipHostFree(s->h);
+    delete s;
+    return rc;
+}
+
+int sbe_server_stats(const sbe_server* s, uint64_t* requests, uint64_t* launches) {
+    if (!s) return SBE_EINVAL;
+    if (requests) *requests = s->requests;
+    if (launches) *launches = s->launches;
+    return SBE_OK;
+}
+
+int sbe_serve_encode_topic(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
+                           uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, 0, 0};
+    return serve_encode_req<LayTM>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status,
+                                   serve_tm_op(false, flags));
+}
+
+int sbe_serve_encode_session(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                             uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, leadership_term_id, cluster_session_id};
+    return serve_encode_req<LayTMS>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status,
+                                    serve_tm_op(true, flags));
+}
+
+int sbe_serve_encode_lite(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id, uint8_t* out,
+                          uint64_t out_capacity, uint64_t* out_off, uint8_t* status) {
+    const uint32_t nf = sbe_lite_fields(template_id);
+    if (!in || nf == 0) return SBE_EINVAL;
+    if (n && !in->topic_id) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->sequence, in->topic_id, template_id, 0, 0};
+    if (nf == 2)
+        return serve_encode_req<LayL2>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite2);
+    return serve_encode_req<LayL3>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite3);
+}
+
+int sbe_serve_decode(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     const sbe_decoded* out) {
+    if (!srv) return SBE_EINVAL;
+    if (const int rc = dec_check(in, rec_off, n, mode, out)) return rc;
+    if (n > SBE_SERVE_MAX_RECORDS) return SBE_EINVAL;
+    if (n == 0) return SBE_OK;
+    ServeReq r{};
+    r.op = mode == SBE_DEC_ON_EGRESS ? kSvDecEgress : mode == SBE_DEC_LITE ? kSvDecLite : kSvDecParse;
+    r.d = DecArgs{in,          rec_off,      n,           out->status,
+                  out->flags,  out->hdr,     out->ts,     out->view_off,
+                  out->view_len, mode == SBE_DEC_PARSE_MESSAGE ? out->seq : nullptr};
+    return serve_call(srv, r);
 }
 
 int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,

@@ -515,6 +515,9 @@ __device__ uint64_t json_seq_eval(const uint8_t* p, uint32_t n) {
 // the decode kernel's call (parse mode with sbe_decoded.seq): kept out of line so the rare
 // evaluation does not widen the decode kernel's register allocation
 __device__ __noinline__ uint64_t json_seq_eval_call(const uint8_t* p, uint32_t n) { return json_seq_eval(p, n); }
+// the serve kernel's own copy: a callee shared with that one-wave kernel would be compiled for its
+// occupancy (more registers) and lower the decode kernels' occupancy with it
+__device__ __noinline__ uint64_t json_seq_eval_call_serve(const uint8_t* p, uint32_t n) { return json_seq_eval(p, n); }
 
 struct SeqArgs {
     const uint8_t* in;

@@ -143,6 +143,49 @@ void for_ranges(size_t n, size_t grain, F&& fn) {
     w.parallel_for(ntasks, [&](size_t t) { fn(n * t / ntasks, n * (t + 1) / ntasks); });
 }
 
+// The page-locked ranges this library knows: its own pool blocks and staging buffers and the
+// ranges the caller registered with host_register, each with its device address (looked up once,
+// when the range is added).  A per-call lookup here replaces the HIP pointer queries, which cost
+// microseconds per call.
+class PinnedRegistry {
+public:
+    static PinnedRegistry& get() {
+        static PinnedRegistry* r = new PinnedRegistry();  // never destroyed
+        return *r;
+    }
+    void add(const void* p, size_t bytes) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess) {
+            (void)hipGetLastError();
+            d = nullptr;
+        }
+        std::lock_guard<std::mutex> g(m_);
+        ranges_[reinterpret_cast<uintptr_t>(p)] = Range{reinterpret_cast<uintptr_t>(p) + bytes, reinterpret_cast<uintptr_t>(d)};
+    }
+    void remove(const void* p) {
+        std::lock_guard<std::mutex> g(m_);
+        ranges_.erase(reinterpret_cast<uintptr_t>(p));
+    }
+    // [p, p + bytes) inside one known range: its device address (nullptr when it has none), true
+    bool find(const void* p, size_t bytes, uint8_t** dev) const {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        std::lock_guard<std::mutex> g(m_);
+        auto it = ranges_.upper_bound(a);
+        if (it == ranges_.begin()) return false;
+        --it;
+        if (a + bytes > it->second.end) return false;
+        *dev = it->second.dev ? reinterpret_cast<uint8_t*>(it->second.dev + (a - it->first)) : nullptr;
+        return true;
+    }
+
+private:
+    struct Range {
+        uintptr_t end, dev;
+    };
+    mutable std::mutex m_;
+    std::map<uintptr_t, Range> ranges_;
+};
+
 // Page-locked host blocks recycled by size class (powers of two from 4 KiB); hipHostMalloc costs
 // milliseconds per call for large blocks, so a block is allocated once and reused.  Free blocks are
 // kept up to AERON_AMD_PINNED_CACHE_BYTES (default 4 GiB) in all; a block returned beyond that is
@@ -166,7 +209,10 @@ public:
                 cached_ -= cls;
             }
         }
-        if (!p) hip_check(hipHostMalloc(&p, cls, hipHostMallocDefault), "hipHostMalloc");
+        if (!p) {
+            hip_check(hipHostMalloc(&p, cls, hipHostMallocDefault), "hipHostMalloc");
+            PinnedRegistry::get().add(p, cls);
+        }
         return std::shared_ptr<void>(p, [this, cls](void* q) { give(q, cls); });
     }
 
@@ -180,6 +226,7 @@ private:
                 return;
             }
         }
+        PinnedRegistry::get().remove(p);
         (void)hipHostFree(p);
     }
     PinnedPool() {
@@ -211,20 +258,30 @@ struct DevBuf {
 };
 struct HostBuf {
     void* p = nullptr;
+    uint8_t* dev = nullptr;  // its device address (the zero-copy kernels read it there)
     size_t cap = 0;
     void need(size_t n) {
         if (n <= cap) return;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         const size_t c = n < 4096 ? 4096 : n + n / 4;
         hip_check(hipHostMalloc(&p, c, hipHostMallocDefault), "hipHostMalloc");
         cap = c;
+        PinnedRegistry::get().add(p, c);
+        uint8_t* d = nullptr;
+        PinnedRegistry::get().find(p, 1, &d);
+        dev = d;
     }
     uint8_t* b() const { return static_cast<uint8_t*>(p); }
-    ~HostBuf() {
-        if (p) (void)hipHostFree(p);
+    void release() {
+        if (p) {
+            PinnedRegistry::get().remove(p);
+            (void)hipHostFree(p);
+        }
+        p = nullptr;
+        dev = nullptr;
+        cap = 0;
     }
+    ~HostBuf() { release(); }
 };
 
 // Three-stream chunk pipeline: host→device copies, kernels and device→host copies each on a
@@ -309,6 +366,28 @@ struct Pipeline {
     }
 };
 
+// Batches of at most this many records (and within the zero-copy size) go to the thread's serve
+// kernel (sbe_server_*: a resident wave polling a page-locked request slot, no launch per call);
+// larger ones to the batch kernels.  AERON_AMD_SERVE_RECORDS overrides (0: never serve).
+size_t serve_max_records() {
+    static const size_t v = [] {
+        const char* e = std::getenv("AERON_AMD_SERVE_RECORDS");
+        const long long x = e ? std::atoll(e) : 256;
+        return (size_t)std::min<long long>(std::max(0LL, x), SBE_SERVE_MAX_RECORDS);
+    }();
+    return v;
+}
+
+// How long an idle serve kernel keeps polling before it exits (AERON_AMD_SERVE_IDLE_US, default
+// 20 ms); the next small call relaunches it.
+uint32_t serve_idle_us() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("AERON_AMD_SERVE_IDLE_US");
+        return e ? (uint32_t)std::max(1LL, std::atoll(e)) : 20000u;
+    }();
+    return v;
+}
+
 // Per-thread device context (the reference's codec functions are reentrant statics).
 struct Ctx {
     Pipeline pipe;
@@ -316,11 +395,27 @@ struct Ctx {
     DevBuf d_ws;    // encode workspace of the zero-copy path
     HostBuf h_aux;
     std::vector<uint64_t> pin, pout;  // encode plan scratch (kept: first-touch costs on every call otherwise)
+    sbe_server* srv = nullptr;
+    bool srv_failed = false;
     Ctx() {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");
         pipe.create();
     }
-    ~Ctx() { pipe.destroy(); }
+    ~Ctx() {
+        if (srv) (void)sbe_server_destroy(srv);
+        pipe.destroy();
+    }
+    // The serve kernel for a batch of n records, or nullptr (too large, disabled, or unavailable:
+    // the batch kernels take it).
+    sbe_server* server(size_t n) {
+        if (n == 0 || n > serve_max_records() || srv_failed) return nullptr;
+        if (!srv && sbe_server_create(&srv, serve_idle_us()) != SBE_OK) {
+            srv = nullptr;
+            srv_failed = true;
+            (void)hipGetLastError();
+        }
+        return srv;
+    }
     void sync_all() { pipe.drain(); }
     // After a throw inside a chunk loop: wait for every copy and kernel already queued (their
     // page-locked sources and destinations must not go back to a pool, or be restaged, while a
@@ -347,8 +442,11 @@ struct PipeGuard {
 
 // The device address of page-locked host memory (hipHostMalloc'd or registered), or nullptr when
 // it has none: kernels of the zero-copy path read their input and write their results there.
-// An interior pointer resolves through the start of its allocation.
+// An interior pointer resolves through the start of its allocation; ranges this library knows
+// (PinnedRegistry) need no HIP query.
 void* device_view(const void* host) {
+    uint8_t* d0 = nullptr;
+    if (PinnedRegistry::get().find(host, 1, &d0)) return d0;
     void* start = nullptr;
     if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
                                (hipDeviceptr_t)const_cast<void*>(host)) != hipSuccess || !start) {
@@ -608,6 +706,11 @@ namespace {
 // it in place, with no staging copy.
 bool page_locked(const void* p, size_t bytes) {
     if (!p || bytes == 0) return false;
+    uint8_t* dev = nullptr;
+    if (PinnedRegistry::get().find(p, bytes, &dev)) return true;
+    // memory page-locked outside this library (the caller's own hipHostMalloc) is found by the HIP
+    // pointer query, which costs microseconds: asked only where that is small against the copy
+    if (bytes < (size_t(1) << 20)) return false;
     hipPointerAttribute_t a{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -649,7 +752,7 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
     sl.pin.need((direct ? o_data : o_data + (size_t)bytes) + 16);
     uint8_t* pin = sl.pin.b();
     uint64_t* ro = reinterpret_cast<uint64_t*>(pin);
-    uint8_t* dpin = static_cast<uint8_t*>(device_view(pin));
+    uint8_t* dpin = sl.pin.dev;
     uint8_t* dblk = static_cast<uint8_t*>(device_view(d.block.get()));
     const uint8_t* drec = direct ? static_cast<const uint8_t*>(device_view(data + base)) : (dpin ? dpin + o_data : nullptr);
     if (!dpin || !dblk || !drec || (reinterpret_cast<uintptr_t>(drec) & 15u)) return false;
@@ -666,6 +769,11 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
                     reinterpret_cast<uint32_t*>(dblk + d.o_off),
                     reinterpret_cast<uint32_t*>(dblk + d.o_len),
                     parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
+    if (sbe_server* srv = c.server(n)) {
+        if (sbe_serve_decode(srv, drec, reinterpret_cast<const uint64_t*>(dpin), n, mode, &out) != SBE_OK)
+            fail("sbe_serve_decode");
+        return true;
+    }
     if (sbe_decode_batch_sized(drec, reinterpret_cast<const uint64_t*>(dpin), n, bytes, mode, &out, P.s_comp) != SBE_OK) {
         c.abort_all();
         fail("sbe_decode_batch");
@@ -769,7 +877,8 @@ struct EncodePlan {
 };
 
 // Encode n records (nf strings, a u64 and a u32 each) through the chunk pipeline.  launch(...)
-// issues one sbe_encode_*_batch call for a chunk on the given stream.
+// issues one sbe_encode_*_batch call for a chunk on the given stream, or (server non-null: a small
+// zero-copy batch) the synchronous sbe_serve_encode_* call.
 template <class Field, class U64, class U32, class Launch>
 EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, EncodePlan plan, Launch&& launch) {
     EncodedBatch b;
@@ -848,7 +957,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         Pipeline::Slot& sl = P.slot[0];
         if (s.bytes <= zero_copy_max_bytes()) {
             sl.pin.need(s.bytes);
-            uint8_t* dp = static_cast<uint8_t*>(device_view(sl.pin.p));
+            uint8_t* dp = sl.pin.dev;
             // offsets, status and stream share one block (above): one lookup for all three
             uint8_t* const hb = reinterpret_cast<uint8_t*>(b.offsets.data());
             uint8_t* const db = static_cast<uint8_t*>(device_view(hb));
@@ -859,15 +968,16 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
                 stage_fill(sl.pin.b(), s, 0, n);
                 tr.lap(tr.stage);
                 PipeGuard zguard(c);
-                const size_t ws_bytes = sbe_encode_workspace_size(n);
+                sbe_server* srv = c.server(n);
+                const size_t ws_bytes = srv ? 16 : sbe_encode_workspace_size(n);
                 c.d_ws.need(ws_bytes);
                 // a batch whose records all fail (E109) has no bytes: the kernels still want a
                 // 16-B aligned output pointer, which they never write at capacity 0
-                launch(dp, reinterpret_cast<const uint32_t*>(dp + s.o_len), reinterpret_cast<const uint64_t*>(dp + s.o_u64),
-                       reinterpret_cast<const uint32_t*>(dp + s.o_u32), n, dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst,
-                       c.d_ws.b(), ws_bytes, P.s_comp);
+                launch(srv, dp, reinterpret_cast<const uint32_t*>(dp + s.o_len),
+                       reinterpret_cast<const uint64_t*>(dp + s.o_u64), reinterpret_cast<const uint32_t*>(dp + s.o_u32), n,
+                       dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst, c.d_ws.b(), ws_bytes, P.s_comp);
                 tr.lap(tr.enqueue);
-                hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
+                if (!srv) hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
                 zguard.release();
                 tr.lap(tr.sync);
                 if (b.offsets[n] != pout[n]) throw std::logic_error("sbecodec: encoded batch size differs from its plan");
@@ -899,7 +1009,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         hipStream_t st = P.compute(sl);
         const uint8_t* di = sl.d_in.b();
         uint8_t* dout = sl.d_out.b();
-        launch(di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
+        launch(nullptr, di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
                reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
                reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st);
         st = P.copy_out(sl);
@@ -1100,12 +1210,17 @@ EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength
     return run_encode(
         msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
         [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; }, plan,
-        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, size_t m, uint8_t* out,
-            uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+        [&](sbe_server* srv, const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, size_t m,
+            uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
             sbe_tm_batch in{arena, nullptr, len, ts};
-            const int rc = session ? sbe_encode_session_batch(&in, m, ts_default, flags, term, sess, out, cap, off, st,
-                                                              ws, wsb, s)
-                                   : sbe_encode_topic_batch(&in, m, ts_default, flags, out, cap, off, st, ws, wsb, s);
+            int rc;
+            if (srv)
+                rc = session ? sbe_serve_encode_session(srv, &in, m, ts_default, flags, term, sess, out, cap, off, st)
+                             : sbe_serve_encode_topic(srv, &in, m, ts_default, flags, out, cap, off, st);
+            else
+                rc = session ? sbe_encode_session_batch(&in, m, ts_default, flags, term, sess, out, cap, off, st, ws,
+                                                        wsb, s)
+                             : sbe_encode_topic_batch(&in, m, ts_default, flags, out, cap, off, st, ws, wsb, s);
             if (rc != SBE_OK) fail(session ? "sbe_encode_session_batch" : "sbe_encode_topic_batch");
         });
 }
@@ -1355,8 +1470,12 @@ unsigned host_threads() { return Workers::get().size(); }
 
 void host_register(const void* p, std::size_t len) {
     hip_check(hipHostRegister(const_cast<void*>(p), len, hipHostRegisterDefault), "hipHostRegister");
+    PinnedRegistry::get().add(p, len);
 }
-void host_unregister(const void* p) { hip_check(hipHostUnregister(const_cast<void*>(p)), "hipHostUnregister"); }
+void host_unregister(const void* p) {
+    PinnedRegistry::get().remove(p);
+    hip_check(hipHostUnregister(const_cast<void*>(p)), "hipHostUnregister");
+}
 
 // ======================================================================================
 // encode
@@ -1441,11 +1560,13 @@ EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOf
         offsets.size(), 2,
         [&](size_t i, int k) { return std::string_view(k == 0 ? offsets[i].message_id : offsets[i].message_identifier); },
         [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; }, plan,
-        [&](const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid, size_t m, uint8_t* out,
-            uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+        [&](sbe_server* srv, const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid,
+            size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
             sbe_lite_batch in{arena, nullptr, len, tid, seq};
-            if (sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws, wsb, s) != SBE_OK)
-                fail("sbe_encode_lite_batch");
+            const int rc = srv ? sbe_serve_encode_lite(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
+                               : sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
+                                                       wsb, s);
+            if (rc != SBE_OK) fail("sbe_encode_lite_batch");
         });
 }
 

@@ -30,7 +30,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 6
+ABI_VERSION = 7
 ENC_REF_TRUNCATE8 = 0x1
 ENC_PUBLISH_TOPIC = 0x2
 ENC_OK, ENC_OVERFLOW = 0, 6
@@ -157,6 +157,27 @@ def _load():
     lib.sbe_gather_plan.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                     ctypes.POINTER(ctypes.c_uint64)]
+    lib.sbe_server_create.restype = ctypes.c_int
+    lib.sbe_server_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32]
+    lib.sbe_server_destroy.restype = ctypes.c_int
+    lib.sbe_server_destroy.argtypes = [ctypes.c_void_p]
+    lib.sbe_server_stats.restype = ctypes.c_int
+    lib.sbe_server_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.sbe_serve_encode_topic.restype = ctypes.c_int
+    lib.sbe_serve_encode_topic.argtypes = [ctypes.c_void_p, ctypes.POINTER(_TmBatch), ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+    lib.sbe_serve_encode_session.restype = ctypes.c_int
+    lib.sbe_serve_encode_session.argtypes = [ctypes.c_void_p, ctypes.POINTER(_TmBatch), ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    lib.sbe_serve_encode_lite.restype = ctypes.c_int
+    lib.sbe_serve_encode_lite.argtypes = [ctypes.c_void_p, ctypes.POINTER(_LiteBatch), ctypes.c_uint64,
+                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                          ctypes.c_void_p]
+    lib.sbe_serve_decode.restype = ctypes.c_int
+    lib.sbe_serve_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_uint32, ctypes.POINTER(_Decoded)]
     if lib.sbe_abi_version() != ABI_VERSION:
         _abi_mismatch()
     return lib
@@ -597,3 +618,125 @@ def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, ds
     if am_root:
         return dst[:nbytes], dst_off[: nrec + 1], nbytes, nrec
     return None, None, nbytes, nrec
+
+
+SERVE_MAX_RECORDS = 4096
+
+
+class Server:
+    """The small-batch serve kernel (sbe_server_* in include/sbecodec.h): one resident wave on its
+    own HIP stream that polls a page-locked request slot, so a one-record call costs no kernel
+    launch.  Every method is synchronous and returns the batch entry point's outputs for the same
+    inputs.  Inputs must be complete when a method is called (it synchronises torch's current
+    stream first); encodes take packed input (no str_off); n <= SERVE_MAX_RECORDS."""
+
+    def __init__(self, idle_us: int = 0):
+        require_device()
+        h = ctypes.c_void_p()
+        _check(lib().sbe_server_create(ctypes.byref(h), int(idle_us)), "sbe_server_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            _check(lib().sbe_server_destroy(h), "sbe_server_destroy")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self):
+        """(requests served, kernel launches) so far."""
+        r, l = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().sbe_server_stats(self._h, ctypes.byref(r), ctypes.byref(l)), "sbe_server_stats")
+        return int(r.value), int(l.value)
+
+    def encode_topic(self, arena, str_len, timestamp, flags=0, ts_default=0, out=None, out_off=None,
+                     status=None) -> Encoded:
+        arena = _dev(arena, torch.uint8, "arena")
+        str_len = _dev(str_len, torch.int32, "str_len")
+        timestamp = _dev(timestamp, torch.int64, "timestamp")
+        n = int(timestamp.numel())
+        if str_len.numel() != 5 * n:
+            raise SbeError("str_len must have 5 entries per record")
+        out, out_off, status = self._outputs(n, output_bound(n, int(arena.numel()), flags), arena.device,
+                                             out, out_off, status)
+        batch = _TmBatch(arena.data_ptr(), None, str_len.data_ptr(), timestamp.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        rc = lib().sbe_serve_encode_topic(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                          _ptr(out), out.numel(), _ptr(out_off), _ptr(status))
+        _check(rc, "sbe_serve_encode_topic")
+        return Encoded(out, out_off, None if status is None else status[:n])
+
+    def encode_session(self, arena, str_len, timestamp, leadership_term_id, cluster_session_id,
+                       flags=ENC_REF_TRUNCATE8, ts_default=0, out=None, out_off=None, status=None) -> Encoded:
+        arena = _dev(arena, torch.uint8, "arena")
+        str_len = _dev(str_len, torch.int32, "str_len")
+        timestamp = _dev(timestamp, torch.int64, "timestamp")
+        n = int(timestamp.numel())
+        if str_len.numel() != 5 * n:
+            raise SbeError("str_len must have 5 entries per record")
+        out, out_off, status = self._outputs(n, output_bound(n, int(arena.numel()), flags), arena.device,
+                                             out, out_off, status)
+        batch = _TmBatch(arena.data_ptr(), None, str_len.data_ptr(), timestamp.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        rc = lib().sbe_serve_encode_session(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                            int(leadership_term_id), int(cluster_session_id), _ptr(out),
+                                            out.numel(), _ptr(out_off), _ptr(status))
+        _check(rc, "sbe_serve_encode_session")
+        return Encoded(out, out_off, None if status is None else status[:n])
+
+    def encode_lite(self, template_id, arena, str_len, topic_id, sequence, out=None, out_off=None,
+                    status=None) -> Encoded:
+        nf = LITE_FIELDS.get(int(template_id))
+        if nf is None:
+            raise SbeError(f"not a Lite template: {template_id}")
+        arena = _dev(arena, torch.uint8, "arena")
+        str_len = _dev(str_len, torch.int32, "str_len")
+        topic_id = _dev(topic_id, torch.int32, "topic_id")
+        sequence = _dev(sequence, torch.int64, "sequence")
+        n = int(sequence.numel())
+        if str_len.numel() != nf * n or topic_id.numel() != n:
+            raise SbeError(f"str_len must have {nf} entries and topic_id one per record")
+        cap = int(lib().sbe_lite_output_bound(n, int(arena.numel()), int(template_id)))
+        out, out_off, status = self._outputs(n, cap, arena.device, out, out_off, status)
+        batch = _LiteBatch(arena.data_ptr(), None, str_len.data_ptr(), topic_id.data_ptr(), sequence.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        rc = lib().sbe_serve_encode_lite(self._h, ctypes.byref(batch), n, int(template_id), _ptr(out), out.numel(),
+                                         _ptr(out_off), _ptr(status))
+        _check(rc, "sbe_serve_encode_lite")
+        return Encoded(out, out_off, None if status is None else status[:n])
+
+    def decode(self, data, rec_off, mode=DEC_PARSE_MESSAGE, out: Decoded | None = None, seq=None) -> Decoded:
+        data = _dev(data, torch.uint8, "data")
+        rec_off = _dev(rec_off, torch.int64, "rec_off")
+        n = int(rec_off.numel()) - 1
+        if out is None:
+            out = alloc_decoded(n, data.device)
+        if seq is True:
+            seq = torch.zeros(max(n, 1), dtype=torch.int64, device=data.device)
+        if seq is not None:
+            seq = _dev(seq, torch.int64, "seq")
+        d = _Decoded(*(getattr(out, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")),
+                     None if seq is None else seq.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        _check(lib().sbe_serve_decode(self._h, _ptr(data), _ptr(rec_off), n, mode, ctypes.byref(d)),
+               "sbe_serve_decode")
+        keys = ("status", "flags", "hdr", "ts", "view_off", "view_len")
+        out = Decoded(*(getattr(out, k)[:n] for k in keys))
+        out.seq = None if seq is None else seq[:n]
+        return out
+
+    @staticmethod
+    def _outputs(n, cap, dev, out, out_off, status):
+        if out is None:
+            out = torch.empty(max(cap, 16), dtype=torch.uint8, device=dev)
+        if out_off is None:
+            out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        if status is None:
+            status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        elif status is False:
+            status = None
+        return out, out_off, status

@@ -43,6 +43,10 @@
  * sbe_order_to_json_batch()       Order::to_json src/order_types.cpp:122-181 and publish_order's
  *                                  headers JSON src/cluster_client.cpp:308-323 (the strings that
  *                                  become the TopicMessage payload / headers)
+ * sbe_serve_*()                   the same encoders / decoders for small batches (one record per
+ *                                  call, as the reference's per-message API is used: parse_message per
+ *                                  fragment src/cluster_client.cpp:1185, publish_topic per message)
+ *                                  through a resident serve kernel instead of a launch per call
  * sbe_gather_encoded()            no reference counterpart (its transport is Aeron,
  *                                  src/session_manager.cpp:1180): the RCCL gather of encoded shards
  *                                  to one ingress rank
@@ -57,7 +61,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 6
+#define SBECODEC_ABI_VERSION 7
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -388,6 +392,40 @@ int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint6
  * Σ records + 1 entries; SBE_EINVAL on a bad world / root. */
 int sbe_gather_plan(const uint64_t* ranks, int world, int root, uint64_t* byte_base, uint64_t* rec_base,
                     uint64_t* totals);
+
+/* ============================ small-batch serve kernel ============================ */
+/* A one-record call through the batch entry points pays a kernel launch and a completion wait
+ * (≈12 us round trip on MI355X, profiles/r04_launch_probe.log) on top of its few microseconds of
+ * work: the reference's per-message calls (SBEEncoder::encode_topic_message,
+ * src/sbe_encoder.cpp:131-181; SBEDecoder/parse_message, src/sbe_encoder.cpp:183-318 and
+ * 915-1029; ClusterClient::publish_topic, src/cluster_client.cpp:1850-1857) cost well under that
+ * on a CPU.  A server is one resident workgroup on its own HIP stream that polls a page-locked
+ * request slot and runs each small batch as it arrives (no launch per request, ≈3 us round
+ * trip), then exits after `idle_us` without a request; the next request relaunches it.
+ * Every sbe_serve_* call is synchronous: it returns when the outputs are written (or with the
+ * error the batch entry point would return, checked on the host before posting).  Outputs are
+ * byte-identical to the batch entry points'.  Pointers are device-visible addresses (device
+ * memory, or page-locked host memory's device pointer); encodes take packed input only
+ * (str_off == NULL); n <= SBE_SERVE_MAX_RECORDS (one workgroup walks the batch tile by tile, so
+ * large batches belong on the batch entry points).  A server is used by one host thread at a time. */
+#define SBE_SERVE_MAX_RECORDS 4096u
+typedef struct sbe_server sbe_server;
+/* idle_us: how long the resident kernel waits for a request before it exits (0: 20000). */
+int sbe_server_create(sbe_server** srv, uint32_t idle_us);
+/* Stops the kernel (a shutdown request, then the stream is synchronised) and frees the server. */
+int sbe_server_destroy(sbe_server* srv);
+int sbe_serve_encode_topic(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
+                           uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
+int sbe_serve_encode_session(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                             uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id, uint8_t* out,
+                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
+int sbe_serve_encode_lite(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id, uint8_t* out,
+                          uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
+/* sbe_decode_batch's modes and outputs (seq evaluated in the same request when non-NULL). */
+int sbe_serve_decode(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                     const sbe_decoded* out);
+/* Requests this server ran and kernel launches it took (a launch per idle exit). */
+int sbe_server_stats(const sbe_server* srv, uint64_t* requests, uint64_t* launches);
 
 /* ================================== profiling ================================== */
 /* Optional (off by default; thread-local): sbe_profile_enable(every) with every >= 1 makes every
