@@ -165,8 +165,12 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, int lane) {
 
 // lane-uniform value of lane `l` (l uniform)
 __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// (the builtin returns int: each half goes through uint32_t, or the low word would sign-extend
+// into the high one whenever its bit 31 is set)
 __device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
-    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // sum over the 64 lanes, uniform
@@ -1864,15 +1868,22 @@ __device__ __forceinline__ void enc_pack_run(const EncArgs& a, uint64_t first, u
 }
 
 // ---- virtual tiles: every window full -----------------------------------------------------
-// Workgroup w owns the contiguous tiles [w T / G, (w + 1) T / G) and walks their records in order
-// with running output / input offsets.  Each step takes the kRpt records from the first one not
-// yet written (a "virtual tile", at any record index) and writes ONE output window: the records
-// from its first that fit kEW bytes, so every window but a workgroup's last is full.  (Tile-aligned
-// steps leave a tile's last window part full: a 32-record tile of ~380-B records is a full 8 KiB
-// window and a ~4 KiB one, and a window costs about the same whatever it holds.)  The records
-// after the window start the next step; their lengths are loaded one step ahead, like the tiles'.
-// A virtual tile the fast path cannot take (a record longer than a window, gather mode, a
-// PUBLISH_TOPIC length wrap) is written whole, window by window, as before.
+// The tiles are cut into chunks of CT consecutive tiles, dealt to the workgroups round robin
+// (chunk c to workgroup c mod G, as the tile loop deals tiles).  A workgroup walks its chunk's
+// records in order with running output / input offsets: each step takes the kRpt records from the
+// first one not yet written (a "virtual tile", at any record index) and writes ONE output window,
+// the records from its first that fit kEW bytes, so every window but a chunk's last is full.
+// (Tile-aligned steps leave a tile's last window part full: a 32-record tile of ~380-B records is
+// a full 8 KiB window and a ~4 KiB one, and a window costs about the same whatever it holds.)  The
+// records after the window start the next step; their lengths are loaded one step ahead, like the
+// tiles'.  Chunks rather than one contiguous range per workgroup: the windows in flight at once
+// then lie CT tiles apart, not n / G records (contiguous ranges measured the fixed-256 pack 10 %
+// slower, profiles/r04_ab_vt.log; chunks did not recover it, see SBE_PACK_VT).  A virtual tile
+// the fast path cannot take (a record longer than a window, gather mode, a PUBLISH_TOPIC length
+// wrap) is written whole, window by window.
+#ifndef SBE_VT_CHUNK  // tiles per chunk (0: one contiguous range per workgroup)
+#define SBE_VT_CHUNK 4
+#endif
 template <class LY, bool kPacked>
 __device__ __forceinline__ TileIn vt_load(const EncArgs& a, uint64_t r0, int lane) {
     SBE_TILE_SHAPE(LY);
@@ -1888,21 +1899,37 @@ __device__ __forceinline__ TileIn vt_load(const EncArgs& a, uint64_t r0, int lan
     return x;
 }
 
-// bytes before the first record of tile t0 (output, packed input): the superblock totals before it
-// plus the tile's prefix inside its superblock (sbe_enc_sums)
-__device__ __forceinline__ void vt_base(const EncArgs& a, uint64_t t0, bool packed, int lane, uint64_t& bo, uint64_t& bi) {
-    const uint64_t nsb = t0 / kTilesPerSb;
-    uint64_t so = 0, si = 0;
-    for (uint64_t j = (uint64_t)lane; j < nsb; j += kWave) {
-        so += a.bsum[2 * j];
-        if (packed) si += a.bsum[2 * j + 1];
+// The lengths of chunk start tile t's first records plus the terms of its base: the tile's prefix
+// inside its superblock (sbe_enc_sums) and, per lane, its share of the superblock totals from
+// sb_next up to the tile's superblock (a workgroup's chunks come in increasing order, so each
+// superblock total is loaded once).
+template <class LY, bool kPacked>
+__device__ __forceinline__ TileIn vt_chunk_load(const EncArgs& a, uint64_t t, int lane, uint64_t& sb_next) {
+    SBE_TILE_SHAPE(LY);
+    TileIn x = vt_load<LY, kPacked>(a, t * kRpt, lane);
+    x.to = a.tsum[2 * t];
+    x.ti = kPacked ? a.tsum[2 * t + 1] : 0ull;
+    const uint64_t sbt = t / kTilesPerSb;
+    uint64_t po = 0, pi = 0;
+    for (uint64_t s = sb_next + (uint64_t)lane; s < sbt; s += kWave) {
+        po += a.bsum[2 * s];
+        if (kPacked) pi += a.bsum[2 * s + 1];
     }
-    bo = uniform64(wave_sum64(so) + a.tsum[2 * t0]);
-    bi = packed ? uniform64(wave_sum64(si) + a.tsum[2 * t0 + 1]) : 0ull;
+    x.po = po;
+    x.pi = pi;
+    sb_next = sbt > sb_next ? sbt : sb_next;
+    return x;
 }
 
+#ifdef SBE_VT_GUARD
+// Debug build only: the first out-of-range window of the virtual-tile loop, recorded instead of
+// stored (read with sbe_debug_vt_guard).
+__device__ uint64_t g_vt_guard[16];
+#endif
+
 template <class LY, bool kPacked, int kLen>
-__device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first, uint64_t G, PackLds<LY, kPacked>& L) {
+__device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first, uint64_t G, PackLds<LY, kPacked>& L,
+                                                uint64_t chunk_tiles = SBE_VT_CHUNK) {
     SBE_TILE_SHAPE(LY);
     lds_u8* const wout = (lds_u8*)L.wout;
     lds_u8* const win_in = (lds_u8*)L.win + kInSlack;
@@ -1911,53 +1938,126 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
     uint64_t* const sbase = L.sbase;
     const int lane = threadIdx.x;
     const uint64_t ntiles = (a.n + kRpt - 1) / kRpt;
-    const uint64_t t_lo = first * ntiles / G, t_hi = (first + 1) * ntiles / G;
-    if (t_lo >= t_hi) return;
-    const uint64_t r_hi = t_hi * kRpt < a.n ? t_hi * kRpt : a.n;  // this workgroup's records end here
-    uint64_t r = t_lo * kRpt;
+    const uint64_t CT = chunk_tiles > 0 ? chunk_tiles : (ntiles + G - 1) / G;
+    const uint64_t nch = (ntiles + CT - 1) / CT;
+    uint64_t c = first;
+    if (c >= nch) return;
+    const uint64_t CR = CT * kRpt;  // records per chunk
+    auto chunk_end = [&](uint64_t cc) { return cc * CR + CR < a.n ? cc * CR + CR : a.n; };
     Ph ph;
     ph.start();
-    uint64_t bo, bi;
-    vt_base(a, t_lo, kPacked, lane, bo, bi);
+    uint64_t sb_next = 0, sp_out = 0, sp_in = 0;
+    uint64_t bo = 0, bi = 0;
+    // a new chunk's base: the superblock totals loaded with its lengths, then its tile prefix
+    auto chunk_base = [&](const TileIn& x_) {
+        sp_out += wave_sum64(x_.po);
+        if (kPacked) sp_in += wave_sum64(x_.pi);
+        bo = uniform64(sp_out + x_.to);
+        bi = kPacked ? uniform64(sp_in + x_.ti) : 0ull;
+    };
     const uintptr_t sink = reinterpret_cast<uintptr_t>(a.sink);
-    // records written by the step of tile S with window W, and the offsets after them
-    auto advance = [&](const TileSt& S_, const Win& W_, bool fast_, uint64_t& bo_, uint64_t& bi_) -> uint32_t {
+    // records written by the step of tile S with window W; bo / bi move past them
+    auto advance = [&](const TileSt& S_, const Win& W_, bool fast_) -> uint32_t {
         const uint32_t k = fast_ ? (uint32_t)W_.rb : (uint32_t)kRpt;
         if (k < (uint32_t)kRpt) {
-            bo_ += lane_u32(S_.rs, (int)k * kLpr);
-            if (kPacked) bi_ += lane_u64(S_.in0, (int)k * kLpr);
+            bo += lane_u32(S_.rs, (int)k * kLpr);
+            if (kPacked) bi += lane_u64(S_.in0, (int)k * kLpr);
         } else {
-            bo_ += S_.agg_out;
-            if (kPacked) bi_ += S_.tot_in;
+            bo += S_.agg_out;
+            if (kPacked) bi += S_.tot_in;
         }
         return k;
     };
-    TileIn x = vt_load<LY, kPacked>(a, r, lane);
-    TileSt S = tile_prepare_at<LY, kPacked, kLen>(a, x, r, r_hi, lane, bo, bi);
+    uint64_t r_hi = chunk_end(c);
+#ifdef SBE_VT_GUARD
+    uint64_t tot_in_all = 0;
+    {
+        const uint64_t nsb_all = (a.n + kSbRec - 1) / kSbRec;
+        uint64_t si = 0;
+        for (uint64_t j = (uint64_t)lane; j < nsb_all; j += kWave) si += a.bsum[2 * j + 1];
+        tot_in_all = uniform64(wave_sum64(si));
+    }
+    // true (and the first such window recorded) when a window would store past the capacity or
+    // stage outside the packed arena
+    auto bad = [&](uint64_t code, const TileSt& S_, int64_t wrel_, int64_t wlen_, uintptr_t swb_, int64_t nb_,
+                   uint64_t r_) -> bool {
+        const uintptr_t a0 = reinterpret_cast<uintptr_t>(a.arena);
+        bool b = wlen_ < 0 || wlen_ > kEW + 16 || (int64_t)S_.T0 + wrel_ + wlen_ > (int64_t)a.cap ||
+                 (int64_t)S_.T0 + wrel_ < -16 || nb_ < 0 || nb_ > kEWIn;
+        if (kPacked && nb_ > 0 && (swb_ + 16 < a0 || swb_ + (uintptr_t)nb_ > a0 + tot_in_all + 16)) b = true;
+        if (!b) return false;
+        if (lane == 0 && atomicCAS((unsigned long long*)&g_vt_guard[0], 0ull, code) == 0ull) {
+            g_vt_guard[1] = first;
+            g_vt_guard[2] = r_;
+            g_vt_guard[3] = S_.T0;
+            g_vt_guard[4] = (uint64_t)wrel_;
+            g_vt_guard[5] = (uint64_t)wlen_;
+            g_vt_guard[6] = swb_ - a0;
+            g_vt_guard[7] = (uint64_t)nb_;
+            g_vt_guard[8] = tot_in_all;
+            g_vt_guard[9] = r_hi;
+            g_vt_guard[10] = S_.agg_out;
+            g_vt_guard[11] = S_.in_tile - a0;
+            g_vt_guard[12] = a.n;
+        }
+        return true;
+    };
+#endif
+    TileIn x = vt_chunk_load<LY, kPacked>(a, c * CT, lane, sb_next);
+    chunk_base(x);
+    uint64_t rn = c * CR;
+    TileSt S = tile_prepare_at<LY, kPacked, kLen>(a, x, rn, r_hi, lane, bo, bi);
     uint4 I[kStageRegs];
     Win W{0, kRpt, 0, 0, 0, sink, 0};
     bool fast = kPacked && !S.wrapped && !tile_big<LY>(S, lane);
     if (fast) W = tile_window<LY>(S, 0, lane, sink);
-    uint64_t rn = r + advance(S, W, fast, bo, bi);  // bo / bi: the next step's offsets
+#ifdef SBE_VT_GUARD
+    if (fast && bad(1, S, W.wrel, W.wlen, W.swb, W.nb, rn)) return;
+#endif
+    rn += advance(S, W, fast);
     if (kPacked) {
         stage_issue(W.swb, W.nb, lane, I);
         stage_write(win_in, W.nb, lane, I);
     }
-    x = vt_load<LY, kPacked>(a, rn, lane);
+    // the next step: the rest of this chunk, or the workgroup's next chunk (its base from the
+    // superblock totals loaded with its lengths)
+    uint64_t cn = c + G;
+    bool nxt_new = rn >= r_hi;
+    if (nxt_new) {
+        rn = cn * CR;
+        x = vt_chunk_load<LY, kPacked>(a, (cn < nch ? cn : nch - 1) * CT, lane, sb_next);
+    } else {
+        x = vt_load<LY, kPacked>(a, rn, lane);
+    }
 
     for (;;) {
-        const bool have_next = rn < r_hi;
+        const bool have_next = !nxt_new || cn < nch;
         TileSt Sn;
         Win Wn{0, kRpt, 0, 0, 0, sink, 0};
-        bool fast_n = false;
+        bool fast_n = false, nxt_new_n = false;
         uint64_t rnn = rn;
         if (have_next) {
+            if (nxt_new) {
+                c = cn;
+                cn = c + G;
+                r_hi = chunk_end(c);
+                chunk_base(x);
+            }
             Sn = tile_prepare_at<LY, kPacked, kLen>(a, x, rn, r_hi, lane, bo, bi);
             ph.lap(7);
             fast_n = kPacked && !Sn.wrapped && !tile_big<LY>(Sn, lane);
             if (fast_n) Wn = tile_window<LY>(Sn, 0, lane, sink);
-            rnn = rn + advance(Sn, Wn, fast_n, bo, bi);
-            x = vt_load<LY, kPacked>(a, rnn, lane);
+#ifdef SBE_VT_GUARD
+            if (fast_n && bad(2, Sn, Wn.wrel, Wn.wlen, Wn.swb, Wn.nb, rn)) return;
+#endif
+            rnn = rn + advance(Sn, Wn, fast_n);
+            nxt_new_n = rnn >= r_hi;
+            if (nxt_new_n) {
+                rnn = cn * CR;
+                x = vt_chunk_load<LY, kPacked>(a, (cn < nch ? cn : nch - 1) * CT, lane, sb_next);
+            } else {
+                x = vt_load<LY, kPacked>(a, rnn, lane);
+            }
         }
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         ph.lap(0);
@@ -1981,6 +2081,9 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
                 int32_t nbw = 0;
                 if (kPacked && !S.wrapped) {
                     stage_range<LY>(S, wrel, lane, sw, nbw);
+#ifdef SBE_VT_GUARD
+                    if (bad(4, S, wrel, we_rel - wrel, sw, nbw, rn)) return;
+#endif
                     for (int k0 = 0; k0 < kStageRegs; k0 += 3) {
                         uint4 J[3];
 #pragma unroll
@@ -2015,12 +2118,20 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
         W = Wn;
         fast = fast_n;
         rn = rnn;
+        nxt_new = nxt_new_n;
     }
     ph.put(lane);
 }
 
+// The batch pack kernel keeps the tile loop: per window, the virtual-tile loop re-prepares a tile
+// (lengths, scans, offsets) where the tile loop reuses the tile's state for its second window, and
+// that costs about what the full windows save (A/B in one process, pack µs tile → virtual tiles:
+// fixed-256 97 → 103-114, config 4 728 → 722-827, session 135 → 134-151, OrderRequestLite 145 →
+// 160, CommitOffsetLite 41 → 40-44 over chunk sizes 1-8 and contiguous ranges;
+// profiles/r04_ab_vt_chunks.log).  The serve kernel uses the virtual-tile loop (running offsets,
+// no tile sums).  SBE_PACK_VT=1 selects it for the batch kernel (A/B).
 #ifndef SBE_PACK_VT
-#define SBE_PACK_VT 1
+#define SBE_PACK_VT 0
 #endif
 template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
@@ -3433,7 +3544,8 @@ int dec_check(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t m
 // Serve kernel: one resident wave that polls a page-locked request slot (sbecodec.h, "small-batch
 // serve kernel").  A request is one EncArgs or DecArgs; the wave runs the same device code as the
 // batch kernels over the whole batch (decode: dec_tile over its tiles; encode: the pack loop as
-// workgroup 0 of 1, whose running offsets make the tile sums unnecessary), then publishes done_seq.
+// workgroup 0 of 1 over one chunk, whose running offsets make the tile sums unnecessary), then
+// publishes done_seq.
 // ------------------------------------------------------------------------------------------
 enum : uint32_t {
     kSvShutdown = 1,
@@ -3486,7 +3598,7 @@ __device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>
         if (threadIdx.x == 0) a.out_off[0] = 0;
         return;
     }
-    enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L);
+    enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L, 0);  // one chunk: the zero prefix of tile 0 is the only base
 }
 
 // idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits.
@@ -3777,6 +3889,18 @@ int sbe_server_destroy(sbe_server* s) {
     delete s;
     return rc;
 }
+
+#ifdef SBE_VT_GUARD
+// debug builds: the virtual-tile guard record (16 u64; [0] = 0 when nothing was caught), then cleared
+int sbe_debug_vt_guard(uint64_t* out16) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_vt_guard), 16 * sizeof(uint64_t));
+    if (e == hipSuccess) {
+        const uint64_t z[16] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_vt_guard), z, sizeof z);
+    }
+    return record_hip(e);
+}
+#endif
 
 int sbe_server_stats(const sbe_server* s, uint64_t* requests, uint64_t* launches) {
     if (!s) return SBE_EINVAL;

@@ -426,3 +426,26 @@ def test_encode_capacity_overflow(codec, kind):
         assert (got[cap:] == 0xAB).all(), "write past out_capacity"
         last = int(eoff[1:][fits][-1]) if fits.any() else 0
         np.testing.assert_array_equal(got[:last], eo[:last])
+
+
+def test_encode_input_offsets_past_2gib(codec):
+    """E109 records whose strings total more than 2 GiB inside one tile, then valid records: the
+    valid records' input offsets come from 64-bit tile sums (a lane read of a sum with bit 31 set
+    once sign-extended into the high word)."""
+    n_bad, big = 32, 70_000_000
+    arena_v, L_v, ts_v = T.fixed256_orders(40)
+    dev = torch.device("cuda")
+    arena = torch.zeros(n_bad * big + arena_v.size, dtype=torch.uint8, device=dev)
+    arena[n_bad * big:] = torch.from_numpy(arena_v).to(dev)
+    L = np.concatenate([np.tile(np.array([[big, 0, 0, 0, 0]], np.uint32), (n_bad, 1)), L_v.reshape(-1, 5)])
+    ts = np.concatenate([np.arange(1, n_bad + 1, dtype=np.uint64), ts_v])
+    enc = codec.encode_topic_batch(arena, to_dev(L, torch.int32), to_dev(ts, torch.int64))
+    torch.cuda.synchronize()
+    n = n_bad + 40
+    off = enc.out_off.cpu().numpy().view(np.uint64)
+    st = enc.status.cpu().numpy()
+    eo, eoff, est = T.oracle_encode(arena_v, L_v, ts_v)
+    assert (st[:n_bad] == 1).all() and np.array_equal(st[n_bad:], est)
+    assert (off[: n_bad + 1] == 0).all() and np.array_equal(off[n_bad:], eoff)
+    assert np.array_equal(enc.out[: int(off[n])].cpu().numpy(), eo)
+    del arena
