@@ -3554,7 +3554,8 @@ enum : uint32_t {
 };
 
 struct ServeReq {
-    uint32_t op, pad;
+    uint32_t op;
+    uint32_t inl;  // bytes of the slot's inline area to copy to the device scratch before running
     EncArgs e;
     DecArgs d;
 };
@@ -3562,11 +3563,18 @@ constexpr int kReqWords = (int)(sizeof(ServeReq) / 4);
 static_assert(sizeof(ServeReq) % 4 == 0 && kReqWords <= kWave, "a request is read one dword per lane");
 
 // Host-written words and device-written words on separate 64-B lines.
+// Inline inputs (sbe_serve_*_host): the host copies a request's inputs into the slot, the wave
+// copies them to device scratch (the first KiB in the same round trip as the request) and runs
+// from there, so the kernel's dependent reads (offsets, then records; lengths, then strings) hit
+// the L2 instead of crossing PCIe.
+constexpr uint32_t kServeInline = SBE_SERVE_INLINE_BYTES;
+static_assert(kServeInline % 1024 == 0, "inline area: whole 1 KiB wave loads");
 struct ServeSlot {
     alignas(64) uint32_t req_seq;  // host → device: sequence number of the posted request
     alignas(64) uint32_t done_seq; // device → host: the last request completed
     uint32_t alive;                // 1 from the host's launch until the kernel's exit
     alignas(64) ServeReq req;
+    alignas(64) uint8_t inl[kServeInline];
 };
 
 union ServeLds {
@@ -3601,8 +3609,9 @@ __device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>
     enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L, 0);  // one chunk: the zero prefix of tile 0 is the only base
 }
 
-// idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits.
-__global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks) {
+// idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits; scratch:
+// the device copy of the inline area.
+__global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks, uint8_t* scratch) {
     __shared__ ServeLds lds;
     const int lane = threadIdx.x;
     uint32_t last = __builtin_amdgcn_readfirstlane(sys_acquire(&slot->done_seq));
@@ -3617,12 +3626,23 @@ __global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, ui
         // the request, one dword per lane (after the acquire: fresh from host memory)
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&slot->req);
         const uint32_t v = lane < kReqWords ? __builtin_nontemporal_load(w + lane) : 0u;
+        typedef __attribute__((address_space(1))) u32x4 g_v4;
+        const g_v4* inl = reinterpret_cast<const g_v4*>(reinterpret_cast<uintptr_t>(slot->inl));
+        const u32x4 i0 = inl[lane];  // the first KiB of inline input, with the request (unused if none)
         union {
             ServeReq r;
             uint32_t u[kReqWords];
         } q;
 #pragma unroll
         for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
+        if (q.r.inl) {
+            g_v4* dst = reinterpret_cast<g_v4*>(reinterpret_cast<uintptr_t>(scratch));
+            if (16u * (uint32_t)lane < q.r.inl) dst[lane] = i0;
+            for (uint32_t o = 1024u + 16u * (uint32_t)lane; o < q.r.inl; o += 1024u) dst[o >> 4] = inl[o >> 4];
+            // the wave's stores complete (and no stale line of an earlier request stays cached)
+            // before its reads of the scratch
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        }
         switch (q.r.op) {
             case kSvDecParse: serve_decode<SBE_DEC_PARSE_MESSAGE>(q.r.d, lds.win); break;
             case kSvDecEgress: serve_decode<SBE_DEC_ON_EGRESS>(q.r.d, lds.win); break;
@@ -3661,11 +3681,14 @@ struct sbe_server {
 
 namespace {
 
-constexpr size_t kServeWsBytes = 16 + kSinkBytes + 16;
+// device workspace: zero tile sums (16 B), the pack's sink, then the inline scratch
+constexpr size_t kServeScratchOff = 16 + kSinkBytes + 16;
+constexpr size_t kServeWsBytes = kServeScratchOff + kServeInline;
 
 int serve_launch(sbe_server* s) {
     __atomic_store_n(&s->h->alive, 1u, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sbe_serve_kernel, dim3(1), dim3(kWave), 0, s->stream, s->d, s->idle_ticks);
+    hipLaunchKernelGGL(sbe_serve_kernel, dim3(1), dim3(kWave), 0, s->stream, s->d, s->idle_ticks,
+                       reinterpret_cast<uint8_t*>(s->ws) + kServeScratchOff);
     ++s->launches;
     return record_hip(hipGetLastError());
 }
@@ -3711,10 +3734,60 @@ int serve_encode_req(sbe_server* s, const EncReq& q, uint64_t n, uint64_t ts_def
     return serve_call(s, r);
 }
 
+// Inline inputs: place `bytes` from host memory at offset `at` of the slot's inline area and
+// return the device address they will have in the scratch.
+struct Inline {
+    sbe_server* s;
+    uint32_t at = 0;
+    bool ok = true;
+    template <class T>
+    const T* put(const T* src, size_t count) {
+        const size_t bytes = count * sizeof(T);
+        const uint32_t o = at;
+        if (bytes > kServeInline || o + bytes > kServeInline) {
+            ok = false;
+            return nullptr;
+        }
+        if (bytes) std::memcpy(s->h->inl + o, src, bytes);
+        at = (uint32_t)((o + bytes + 15) & ~(size_t)15);
+        return reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(s->ws) + kServeScratchOff + o);
+    }
+};
+
 uint32_t serve_tm_op(bool session, uint32_t flags) {
     const int len = enc_len_mode(flags);
     if (session) return len == kLenRef ? kSvTmsRef : kSvTmsWire;
     return len == kLenRef ? kSvTmRef : len == kLenPub ? kSvTmPub : kSvTmWire;
+}
+
+// host-input encode: the packed strings, lengths, timestamps / sequences (and Lite topicIds) into
+// the inline area, then the device-pointer request on the scratch copies
+template <class LY>
+int serve_encode_host(sbe_server* s, const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags, uint8_t* out,
+                      uint64_t out_capacity, uint64_t* out_off, uint8_t* status, uint32_t op) {
+    if (!s || !s->h) return SBE_EINVAL;
+    if (n > SBE_SERVE_MAX_RECORDS || (n && q.str_off)) return SBE_EINVAL;
+    if (n && (!q.str_len || !q.ts)) return SBE_EINVAL;
+    uint64_t sum = 0;
+    for (uint64_t i = 0; i < (uint64_t)LY::kNF * n; ++i) sum += q.str_len[i];
+    if (sum > kServeInline) return SBE_EINVAL;
+    Inline I{s};
+    EncReq d = q;
+    if (n) {
+        d.arena = I.put(q.arena, (size_t)sum);
+        d.str_len = I.put(q.str_len, (size_t)(LY::kNF * n));
+        d.ts = I.put(q.ts, (size_t)n);
+        if (!LY::kTM) d.tid = I.put(q.tid, (size_t)n);
+        if (!I.ok) return SBE_EINVAL;
+        if (!d.arena) d.arena = reinterpret_cast<const uint8_t*>(s->ws) + kServeScratchOff;  // Σlen = 0
+    }
+    if (const int rc = enc_check<LY>(d, n, flags, out, out_off)) return rc;
+    ServeReq r{};
+    r.op = op;
+    r.inl = I.at;
+    r.e = EncArgs{d.arena, nullptr, d.str_len, d.ts, d.tid, d.tmpl, d.term_id, d.sess_id, n, ts_default,
+                  out, out_capacity, out_off, status, s->ws, s->ws, reinterpret_cast<uint8_t*>(s->ws + 2)};
+    return serve_call(s, r);
 }
 
 }  // namespace
@@ -3935,6 +4008,57 @@ int sbe_serve_encode_lite(sbe_server* srv, const sbe_lite_batch* in, uint64_t n,
     if (nf == 2)
         return serve_encode_req<LayL2>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite2);
     return serve_encode_req<LayL3>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite3);
+}
+
+
+int sbe_serve_encode_topic_host(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                uint32_t flags, uint8_t* out, uint64_t out_capacity, uint64_t* out_off,
+                                uint8_t* status) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, 0, 0};
+    return serve_encode_host<LayTM>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status,
+                                    serve_tm_op(false, flags));
+}
+
+int sbe_serve_encode_session_host(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                  uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id,
+                                  uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, leadership_term_id, cluster_session_id};
+    return serve_encode_host<LayTMS>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status,
+                                     serve_tm_op(true, flags));
+}
+
+int sbe_serve_encode_lite_host(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id,
+                               uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status) {
+    const uint32_t nf = sbe_lite_fields(template_id);
+    if (!in || nf == 0) return SBE_EINVAL;
+    if (n && !in->topic_id) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->sequence, in->topic_id, template_id, 0, 0};
+    if (nf == 2) return serve_encode_host<LayL2>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite2);
+    return serve_encode_host<LayL3>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite3);
+}
+
+int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                          const sbe_decoded* out) {
+    if (!srv || !srv->h) return SBE_EINVAL;
+    if (n > SBE_SERVE_MAX_RECORDS) return SBE_EINVAL;
+    if (n == 0) return mode <= SBE_DEC_LITE ? SBE_OK : SBE_EINVAL;
+    if (!in || !rec_off) return SBE_EINVAL;
+    const uint64_t lo = rec_off[0], bytes = rec_off[n] - lo;
+    const uint64_t o_data = (8 * (n + 1) + 15) & ~15ull;
+    if (rec_off[n] < lo || o_data + bytes > kServeInline) return SBE_EINVAL;
+    uint64_t* ro = reinterpret_cast<uint64_t*>(srv->h->inl);
+    for (uint64_t i = 0; i <= n; ++i) ro[i] = rec_off[i] - lo;
+    if (bytes) std::memcpy(srv->h->inl + o_data, in + lo, (size_t)bytes);
+    const uint8_t* scr = reinterpret_cast<const uint8_t*>(srv->ws) + kServeScratchOff;
+    if (const int rc = dec_check(scr + o_data, reinterpret_cast<const uint64_t*>(scr), n, mode, out)) return rc;
+    ServeReq r{};
+    r.op = mode == SBE_DEC_ON_EGRESS ? kSvDecEgress : mode == SBE_DEC_LITE ? kSvDecLite : kSvDecParse;
+    r.inl = (uint32_t)(o_data + bytes);
+    r.d = DecArgs{scr + o_data, reinterpret_cast<const uint64_t*>(scr), n, out->status, out->flags, out->hdr,
+                  out->ts, out->view_off, out->view_len, mode == SBE_DEC_PARSE_MESSAGE ? out->seq : nullptr};
+    return serve_call(srv, r);
 }
 
 int sbe_serve_decode(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,

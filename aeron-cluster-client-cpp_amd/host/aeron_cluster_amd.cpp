@@ -746,6 +746,22 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
     Pipeline::Slot& sl = P.slot[0];  // serial use (the pipeline is idle between calls)
     const uint64_t lo = rec_off[0], bytes = rec_off[n] - lo;
     const size_t o_data = al16((n + 1) * 8);
+    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
+    // small batches: the serve kernel, inputs straight from the caller's memory into its request slot
+    if (sbe_server* srv = c.server(n); srv && o_data + bytes <= SBE_SERVE_INLINE_BYTES) {
+        uint8_t* dblk = static_cast<uint8_t*>(device_view(d.block.get()));
+        if (dblk) {
+            sbe_decoded out{dblk,
+                            dblk + d.o_fl,
+                            reinterpret_cast<uint16_t*>(dblk + d.o_hdr),
+                            reinterpret_cast<uint64_t*>(dblk + d.o_ts),
+                            reinterpret_cast<uint32_t*>(dblk + d.o_off),
+                            reinterpret_cast<uint32_t*>(dblk + d.o_len),
+                            parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
+            if (sbe_serve_decode_host(srv, data, rec_off, n, mode, &out) != SBE_OK) fail("sbe_serve_decode_host");
+            return true;
+        }
+    }
     // the kernel reads its records from a 16-B aligned base: page-locked caller bytes are read from
     // the 16-B boundary below the first record (offsets rebased to it); staged bytes start aligned
     const uint64_t base = direct ? (lo & ~(uint64_t)15) : lo;
@@ -761,7 +777,6 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
     });
     if (!direct && bytes)
         for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) { copy_small(pin + o_data + x, data + lo + x, y - x); });
-    const bool parse = mode == SBE_DEC_PARSE_MESSAGE;
     sbe_decoded out{dblk,
                     dblk + d.o_fl,
                     reinterpret_cast<uint16_t*>(dblk + d.o_hdr),
@@ -769,7 +784,7 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
                     reinterpret_cast<uint32_t*>(dblk + d.o_off),
                     reinterpret_cast<uint32_t*>(dblk + d.o_len),
                     parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
-    if (sbe_server* srv = c.server(n)) {
+    if (sbe_server* srv = c.server(n)) {  // larger than the inline area: inputs through the staging buffer
         if (sbe_serve_decode(srv, drec, reinterpret_cast<const uint64_t*>(dpin), n, mode, &out) != SBE_OK)
             fail("sbe_serve_decode");
         return true;
@@ -878,7 +893,8 @@ struct EncodePlan {
 
 // Encode n records (nf strings, a u64 and a u32 each) through the chunk pipeline.  launch(...)
 // issues one sbe_encode_*_batch call for a chunk on the given stream, or (server non-null: a small
-// zero-copy batch) the synchronous sbe_serve_encode_* call.
+// zero-copy batch) the synchronous sbe_serve_encode_* call (host_in: the inputs by their host
+// addresses, the *_host form).
 template <class Field, class U64, class U32, class Launch>
 EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, EncodePlan plan, Launch&& launch) {
     EncodedBatch b;
@@ -971,10 +987,13 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
                 sbe_server* srv = c.server(n);
                 const size_t ws_bytes = srv ? 16 : sbe_encode_workspace_size(n);
                 c.d_ws.need(ws_bytes);
+                // the serve kernel takes the staged inputs by their host addresses (copied into its
+                // request slot when they fit, else read through their device addresses)
+                const uint8_t* ip = srv && s.bytes <= SBE_SERVE_INLINE_BYTES ? sl.pin.b() : dp;
                 // a batch whose records all fail (E109) has no bytes: the kernels still want a
                 // 16-B aligned output pointer, which they never write at capacity 0
-                launch(srv, dp, reinterpret_cast<const uint32_t*>(dp + s.o_len),
-                       reinterpret_cast<const uint64_t*>(dp + s.o_u64), reinterpret_cast<const uint32_t*>(dp + s.o_u32), n,
+                launch(srv, ip != dp, ip, reinterpret_cast<const uint32_t*>(ip + s.o_len),
+                       reinterpret_cast<const uint64_t*>(ip + s.o_u64), reinterpret_cast<const uint32_t*>(ip + s.o_u32), n,
                        dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst, c.d_ws.b(), ws_bytes, P.s_comp);
                 tr.lap(tr.enqueue);
                 if (!srv) hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
@@ -1009,7 +1028,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         hipStream_t st = P.compute(sl);
         const uint8_t* di = sl.d_in.b();
         uint8_t* dout = sl.d_out.b();
-        launch(nullptr, di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
+        launch(nullptr, false, di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
                reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
                reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st);
         st = P.copy_out(sl);
@@ -1210,11 +1229,15 @@ EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength
     return run_encode(
         msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
         [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; }, plan,
-        [&](sbe_server* srv, const uint8_t* arena, const uint32_t* len, const uint64_t* ts, const uint32_t*, size_t m,
-            uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+        [&](sbe_server* srv, bool host_in, const uint8_t* arena, const uint32_t* len, const uint64_t* ts,
+            const uint32_t*, size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb,
+            hipStream_t s) {
             sbe_tm_batch in{arena, nullptr, len, ts};
             int rc;
-            if (srv)
+            if (srv && host_in)
+                rc = session ? sbe_serve_encode_session_host(srv, &in, m, ts_default, flags, term, sess, out, cap, off, st)
+                             : sbe_serve_encode_topic_host(srv, &in, m, ts_default, flags, out, cap, off, st);
+            else if (srv)
                 rc = session ? sbe_serve_encode_session(srv, &in, m, ts_default, flags, term, sess, out, cap, off, st)
                              : sbe_serve_encode_topic(srv, &in, m, ts_default, flags, out, cap, off, st);
             else
@@ -1560,10 +1583,13 @@ EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOf
         offsets.size(), 2,
         [&](size_t i, int k) { return std::string_view(k == 0 ? offsets[i].message_id : offsets[i].message_identifier); },
         [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; }, plan,
-        [&](sbe_server* srv, const uint8_t* arena, const uint32_t* len, const uint64_t* seq, const uint32_t* tid,
-            size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb, hipStream_t s) {
+        [&](sbe_server* srv, bool host_in, const uint8_t* arena, const uint32_t* len, const uint64_t* seq,
+            const uint32_t* tid, size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb,
+            hipStream_t s) {
             sbe_lite_batch in{arena, nullptr, len, tid, seq};
-            const int rc = srv ? sbe_serve_encode_lite(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
+            const int rc =
+                srv && host_in ? sbe_serve_encode_lite_host(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
+                : srv          ? sbe_serve_encode_lite(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
                                : sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
                                                        wsb, s);
             if (rc != SBE_OK) fail("sbe_encode_lite_batch");

@@ -175,6 +175,15 @@ def _load():
     lib.sbe_serve_encode_lite.argtypes = [ctypes.c_void_p, ctypes.POINTER(_LiteBatch), ctypes.c_uint64,
                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                           ctypes.c_void_p]
+    lib.sbe_serve_encode_topic_host.restype = ctypes.c_int
+    lib.sbe_serve_encode_topic_host.argtypes = lib.sbe_serve_encode_topic.argtypes
+    lib.sbe_serve_encode_session_host.restype = ctypes.c_int
+    lib.sbe_serve_encode_session_host.argtypes = lib.sbe_serve_encode_session.argtypes
+    lib.sbe_serve_encode_lite_host.restype = ctypes.c_int
+    lib.sbe_serve_encode_lite_host.argtypes = lib.sbe_serve_encode_lite.argtypes
+    lib.sbe_serve_decode_host.restype = ctypes.c_int
+    lib.sbe_serve_decode_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_uint32, ctypes.POINTER(_Decoded)]
     lib.sbe_serve_decode.restype = ctypes.c_int
     lib.sbe_serve_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_uint32, ctypes.POINTER(_Decoded)]
@@ -724,6 +733,65 @@ class Server:
         torch.cuda.current_stream().synchronize()
         _check(lib().sbe_serve_decode(self._h, _ptr(data), _ptr(rec_off), n, mode, ctypes.byref(d)),
                "sbe_serve_decode")
+        keys = ("status", "flags", "hdr", "ts", "view_off", "view_len")
+        out = Decoded(*(getattr(out, k)[:n] for k in keys))
+        out.seq = None if seq is None else seq[:n]
+        return out
+
+    # host-memory inputs (numpy arrays), copied into the request slot: the *_host entry points
+    def encode_topic_host(self, arena, str_len, timestamp, flags=0, ts_default=0, session=None, dev="cuda"):
+        """TopicMessage (session=None) or session-framed (session=(term, session_id)) encode of host
+        numpy inputs: arena uint8, str_len uint32 [n,5], timestamp uint64 [n]."""
+        import numpy as np
+        arena = np.ascontiguousarray(arena, np.uint8)
+        str_len = np.ascontiguousarray(str_len, np.uint32).reshape(-1, 5)
+        timestamp = np.ascontiguousarray(timestamp, np.uint64)
+        n = int(timestamp.size)
+        out, out_off, status = self._outputs(n, output_bound(n, int(arena.size), flags), torch.device(dev),
+                                             None, None, None)
+        batch = _TmBatch(arena.ctypes.data if arena.size else None, None, str_len.ctypes.data, timestamp.ctypes.data)
+        if session is None:
+            rc = lib().sbe_serve_encode_topic_host(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                                   _ptr(out), out.numel(), _ptr(out_off), _ptr(status))
+        else:
+            rc = lib().sbe_serve_encode_session_host(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                                     int(session[0]), int(session[1]), _ptr(out), out.numel(),
+                                                     _ptr(out_off), _ptr(status))
+        _check(rc, "sbe_serve_encode_*_host")
+        return Encoded(out, out_off, status[:n])
+
+    def encode_lite_host(self, template_id, arena, str_len, topic_id, sequence, dev="cuda"):
+        import numpy as np
+        nf = LITE_FIELDS.get(int(template_id))
+        if nf is None:
+            raise SbeError(f"not a Lite template: {template_id}")
+        arena = np.ascontiguousarray(arena, np.uint8)
+        str_len = np.ascontiguousarray(str_len, np.uint32).reshape(-1, nf)
+        topic_id = np.ascontiguousarray(topic_id, np.uint32)
+        sequence = np.ascontiguousarray(sequence, np.uint64)
+        n = int(sequence.size)
+        cap = int(lib().sbe_lite_output_bound(n, int(arena.size), int(template_id)))
+        out, out_off, status = self._outputs(n, cap, torch.device(dev), None, None, None)
+        batch = _LiteBatch(arena.ctypes.data if arena.size else None, None, str_len.ctypes.data, topic_id.ctypes.data,
+                           sequence.ctypes.data)
+        _check(lib().sbe_serve_encode_lite_host(self._h, ctypes.byref(batch), n, int(template_id), _ptr(out),
+                                                out.numel(), _ptr(out_off), _ptr(status)), "sbe_serve_encode_lite_host")
+        return Encoded(out, out_off, status[:n])
+
+    def decode_host(self, data, rec_off, mode=DEC_PARSE_MESSAGE, seq=None, dev="cuda") -> Decoded:
+        """Decode of host numpy inputs: data uint8, rec_off uint64 [n+1] (any base, no alignment)."""
+        import numpy as np
+        data = np.ascontiguousarray(data, np.uint8)
+        rec_off = np.ascontiguousarray(rec_off, np.uint64)
+        n = int(rec_off.size) - 1
+        out = alloc_decoded(n, torch.device(dev))
+        if seq is True:
+            seq = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+        d = _Decoded(*(getattr(out, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")),
+                     None if seq is None else seq.data_ptr())
+        torch.cuda.current_stream().synchronize()
+        _check(lib().sbe_serve_decode_host(self._h, data.ctypes.data if data.size else None, rec_off.ctypes.data, n,
+                                           mode, ctypes.byref(d)), "sbe_serve_decode_host")
         keys = ("status", "flags", "hdr", "ts", "view_off", "view_len")
         out = Decoded(*(getattr(out, k)[:n] for k in keys))
         out.seq = None if seq is None else seq[:n]

@@ -424,6 +424,24 @@ int sbe_serve_encode_lite(sbe_server* srv, const sbe_lite_batch* in, uint64_t n,
 /* sbe_decode_batch's modes and outputs (seq evaluated in the same request when non-NULL). */
 int sbe_serve_decode(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                      const sbe_decoded* out);
+/* The same with the inputs in host memory (any memory the calling thread reads; packed strings,
+ * no alignment needed): they are copied into the server's request slot, and the kernel moves them
+ * to device scratch in the round trip that fetches the request, so its dependent reads (offsets,
+ * then records; lengths, then strings) hit the L2 instead of crossing PCIe twice.  At most
+ * SBE_SERVE_INLINE_BYTES of inputs per request, laid out 16-B aligned: decode
+ * 8 (n + 1) + (rec_off[n] - rec_off[0]); encode Σlen + 4 nf n + 8 n (+ 4 n Lite topicIds).
+ * SBE_EINVAL when they do not fit.  Outputs are device-visible pointers, as above. */
+#define SBE_SERVE_INLINE_BYTES 16384u
+int sbe_serve_encode_topic_host(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                uint32_t flags, uint8_t* out, uint64_t out_capacity, uint64_t* out_off,
+                                uint8_t* status);
+int sbe_serve_encode_session_host(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                  uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id,
+                                  uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
+int sbe_serve_encode_lite_host(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id,
+                               uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
+int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
+                          const sbe_decoded* out);
 /* Requests this server ran and kernel launches it took (a launch per idle exit). */
 int sbe_server_stats(const sbe_server* srv, uint64_t* requests, uint64_t* launches);
 

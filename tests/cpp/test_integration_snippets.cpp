@@ -68,3 +68,12 @@ void snippet_gather() {
     hipStream_t stream = nullptr;
 #include "snip_gather.inc"
 }
+
+void snippet_serve() {
+    std::uint8_t *d_arena = nullptr, *d_out = nullptr, *d_status = nullptr, *d_rec = nullptr;
+    std::uint32_t* d_len = nullptr;
+    std::uint64_t *d_ts = nullptr, *d_off = nullptr, *d_rec_off = nullptr;
+    std::uint64_t now_ns = 0, cap = 0;
+    sbe_decoded dd{};
+#include "snip_serve.inc"
+}

@@ -219,3 +219,62 @@ def test_serve_idle_exit_and_relaunch(codec):
         assert req == 20 and launches <= 3
     finally:
         s.close()
+
+
+# ---- host-memory inputs (sbe_serve_*_host: inputs copied into the request slot) ----------------
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8, T.ENC_PUBLISH_TOPIC])
+@pytest.mark.parametrize("n", [1, 2, 33, 60])
+def test_serve_host_encode_topic(codec, server, n, flags):
+    arena, L, ts = T.var_orders(n, seed=0x90 + n)
+    got = host(server.encode_topic_host(arena, L, ts, flags=flags, ts_default=5), n)
+    check_same(got, T.oracle_encode(arena, L, ts, flags=flags, ts_default=5))
+
+
+def test_serve_host_encode_session_and_lite(codec, server):
+    arena, L, ts = T.var_orders(20, seed=0x91)
+    got = host(server.encode_topic_host(arena, L, ts, flags=T.ENC_REF_TRUNCATE8, session=(4, -9)), 20)
+    check_same(got, T.oracle_encode_session(arena, L, ts, 4, -9, flags=T.ENC_REF_TRUNCATE8))
+    for tid in (301, 201):
+        a, Ll, t, q = T.lite_records(30, tid)
+        check_same(host(server.encode_lite_host(tid, a, Ll, t, q), 30), T.oracle_encode_lite(tid, a, Ll, t, q))
+
+
+def test_serve_host_encode_limits(codec, server):
+    arena, L, ts = T.fixed256_orders(80)  # 80 x 250 B of inputs: past the 16 KiB inline area
+    with pytest.raises(codec.SbeError):
+        server.encode_topic_host(arena, L, ts)
+    e = np.zeros(0, np.uint8)
+    got = server.encode_topic_host(e, np.zeros((0, 5), np.uint32), np.zeros(0, np.uint64))
+    assert got.out_off[:1].cpu().tolist() == [0]
+    # E109 lengths count against the inline area too (their strings are part of the packed input)
+    L2 = np.array([[70000, 0, 0, 0, 0]], np.uint32)
+    with pytest.raises(codec.SbeError):
+        server.encode_topic_host(np.zeros(70000, np.uint8), L2, np.ones(1, np.uint64))
+
+
+@pytest.mark.parametrize("mode", [T.DEC_PARSE, T.DEC_EGRESS, T.DEC_LITE])
+def test_serve_host_decode_edges_any_base(codec, server, mode):
+    recs = [r for _, r in T.edge_records()]
+    for lead in (0, 1, 7, 13):
+        data, off = T.pack_records([b"\0" * lead] + recs)
+        # the records after the lead-in, offsets not starting at 0: the host entry point rebases
+        sub = off[1:]
+        exp = T.oracle_decode(data, sub, mode)
+        for a in range(0, len(sub) - 1, 50):
+            b = min(a + 50, len(sub) - 1)
+            got = server.decode_host(data, sub[a: b + 1], mode=mode).numpy()
+            assert_same_decode(got, {k: v[a:b] for k, v in exp.items()})
+
+
+def test_serve_host_decode_mixed_and_seq(codec, server):
+    data, off = T.mixed_records(60, seed=0x92)
+    for mode in (T.DEC_PARSE, T.DEC_EGRESS):
+        assert_same_decode(server.decode_host(data, off, mode=mode).numpy(), T.oracle_decode(data, off, mode))
+    key = b"_sequence_number"
+    recs = [T.tm_wire([b"t", b"y", b"u", b'{"' + key + b'":%d}' % (i + 7), b"{}"], i) for i in range(10)]
+    d2, o2 = T.pack_records(recs)
+    dec = server.decode_host(d2, o2, seq=True)
+    assert dec.seq.cpu().numpy().view(np.uint64).tolist() == [i + 7 for i in range(10)]
+    with pytest.raises(codec.SbeError):  # past the inline area
+        big, boff = T.mixed_records(200, seed=1)
+        server.decode_host(big, boff)
