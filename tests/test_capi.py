@@ -118,3 +118,26 @@ def test_codec_library_does_not_link_rccl():
     out = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True, check=True).stdout
     needed = re.findall(r"\(NEEDED\).*\[(.+?)\]", out)
     assert needed and not any("rccl" in n for n in needed), needed
+
+
+def test_serve_entry_points_without_a_server(lib):
+    """The serve API's host-side checks: a NULL server or out-of-range arguments are refused before
+    anything touches a device (sbe_server_create itself needs one)."""
+    EINVAL = -1
+    for name, nargs in (("sbe_serve_encode_topic", 9), ("sbe_serve_encode_topic_host", 9),
+                        ("sbe_serve_encode_session", 11), ("sbe_serve_encode_session_host", 11),
+                        ("sbe_serve_encode_lite", 8), ("sbe_serve_encode_lite_host", 8),
+                        ("sbe_serve_decode", 6), ("sbe_serve_decode_host", 6)):
+        f = getattr(lib, name)
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * nargs
+        assert f(*([None] * nargs)) == EINVAL, name
+    lib.sbe_server_destroy.restype = ctypes.c_int
+    lib.sbe_server_destroy.argtypes = [ctypes.c_void_p]
+    assert lib.sbe_server_destroy(None) == 0
+    lib.sbe_server_stats.restype = ctypes.c_int
+    lib.sbe_server_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    assert lib.sbe_server_stats(None, None, None) == EINVAL
+    lib.sbe_server_create.restype = ctypes.c_int
+    lib.sbe_server_create.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    assert lib.sbe_server_create(None, 0) == EINVAL
