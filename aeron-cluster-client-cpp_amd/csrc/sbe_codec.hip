@@ -2853,8 +2853,12 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
     if (kMode == SBE_DEC_PARSE_MESSAGE) {
         const bool pend = here && (d.flags & kFlSeqPending);
         if (!wide) {
+#ifdef SBE_TIMING_NOSEQ  // timing builds only (scripts/serve_probe.cpp): the per-lane scan skipped
+            if (pend) d.flags &= ~kFlSeqPending;
+#else
             if (pend)
                 d.flags = (d.flags & ~kFlSeqPending) | has_seq_key_lane(LdsRec{win, (uint32_t)(rs - wb)}, d.off[3], d.len[3]);
+#endif
         } else if (__ballot(pend)) {
             uint32_t hit = 0;
             if (__ballot(sm != 0)) {  // some staged chunk holds a key slice or a backslash
@@ -2883,8 +2887,18 @@ __device__ __forceinline__ void dec_window(const uint32_t* win, uint64_t wb, uin
 #endif
 // One 64-record tile (the decode kernel: tile = blockIdx.x; the serve kernel: tile 0 of a one-tile
 // batch); win is the workgroup's LDS window of kWin bytes.
+#ifdef SBE_SERVE_PROF
+__device__ uint64_t g_serve_prof[16];
+#define SBE_SVP(k, t) tpk[(k) - 5] = __builtin_amdgcn_s_memrealtime()
+#else
+#define SBE_SVP(k, t) do { } while (0)
+#endif
 template <uint32_t kMode, uint32_t kWin, bool kServe = false>
 __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32_t* win) {
+#ifdef SBE_SERVE_PROF
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tpk[4] = {tp0, tp0, tp0, tp0};
+#endif
     const int lane = threadIdx.x;
     const uint64_t t0 = tile * kTile;
     const uint64_t r = t0 + (uint64_t)lane;
@@ -2908,10 +2922,15 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
     // first window: the whole tile when its records are at most 256 B on average
     uint64_t wb = T0 & ~15ull;
     uint64_t we = wb + kWin < end ? wb + kWin : (end > wb ? end : wb);
-    const bool wide = __ballot(valid && rl > kSeqLaneRec) != 0;
+    // the served path classifies the staged chunks in parallel (one chunk a lane for a small
+    // batch) instead of a per-lane payload scan, whose dependent steps a lone wave cannot hide
+    // (1.4 µs of a one-record request, profiles/r04_serve_probe.log)
+    const bool wide = kServe || __ballot(valid && rl > kSeqLaneRec) != 0;
     uint4 I[dec_regs<kWin>()];
+    SBE_SVP(5, tp0);  // offsets read
     dec_issue<kWin>(a, wb, we, lane, I);
     uint32_t sm = dec_commit<kMode, kWin>(win, wb, we, wide, lane, I);
+    SBE_SVP(6, tp0);  // first window in LDS
     // The second window starts at the first record the first one cannot hold, which the record
     // offsets already tell: its loads go out before the first window is parsed (tiles of records
     // over 256 B on average take two windows; each would otherwise wait one more HBM round trip).
@@ -2969,6 +2988,7 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
             dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
         }
     }
+    SBE_SVP(7, tp0);  // parsed
     if (valid) {
         dst_store(a.status + r, (uint8_t)d.status);
         dst_store(a.flags + r, (uint8_t)d.flags);
@@ -2991,12 +3011,17 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
     }
     // ParseResult.sequence_number of flagged TopicMessages (rare: payloads with the key or a
     // backslash), evaluated from HBM by the lanes that hold one
+    SBE_SVP(8, tp0);  // descriptor stores issued
     if (kMode == SBE_DEC_PARSE_MESSAGE && a.seq) {
         const bool cand = valid && d.status == SBE_ST_TM && (d.flags & kSeqCand);
         if (__ballot(cand) && cand)
             a.seq[r] = kServe ? json_seq_eval_call_serve(a.in + rs + d.off[3], d.len[3])
                               : json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
     }
+#ifdef SBE_SERVE_PROF
+    if (kServe && lane == 0)
+        for (int k = 0; k < 4; ++k) g_serve_prof[5 + k] += tpk[k] - tp0;
+#endif
 }
 
 template <uint32_t kMode, uint32_t kWin>
@@ -3609,6 +3634,17 @@ __device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>
     enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L, 0);  // one chunk: the zero prefix of tile 0 is the only base
 }
 
+#ifdef SBE_SERVE_PROF
+// Debug builds only: per-request phase times of the serve kernel, s_memrealtime ticks (10 ns)
+// summed over requests: [0] request seen → request words in registers, [1] → inline inputs in
+// scratch, [2] → body issued, [3] → done_seq stored (the release waits for every store), [4] count;
+// inside a served decode tile, from its start: [5] offsets read, [6] window in LDS, [7] parsed,
+// [8] descriptor stores issued (read with sbe_debug_serve_prof)
+#define SBE_SV_T(x) const uint64_t x = __builtin_amdgcn_s_memrealtime()
+#else
+#define SBE_SV_T(x)
+#endif
+
 // idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits; scratch:
 // the device copy of the inline area.
 __global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks, uint8_t* scratch) {
@@ -3623,6 +3659,7 @@ __global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, ui
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
+        SBE_SV_T(t0);
         // the request, one dword per lane (after the acquire: fresh from host memory)
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&slot->req);
         const uint32_t v = lane < kReqWords ? __builtin_nontemporal_load(w + lane) : 0u;
@@ -3635,14 +3672,17 @@ __global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, ui
         } q;
 #pragma unroll
         for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
+        SBE_SV_T(t1);
         if (q.r.inl) {
             g_v4* dst = reinterpret_cast<g_v4*>(reinterpret_cast<uintptr_t>(scratch));
             if (16u * (uint32_t)lane < q.r.inl) dst[lane] = i0;
             for (uint32_t o = 1024u + 16u * (uint32_t)lane; o < q.r.inl; o += 1024u) dst[o >> 4] = inl[o >> 4];
-            // the wave's stores complete (and no stale line of an earlier request stays cached)
-            // before its reads of the scratch
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            // the wave's stores complete (this XCD's L2 holds them) and no line of an earlier
+            // request stays in the CU's vector L1, before its reads of the scratch
+            __builtin_amdgcn_s_waitcnt(0);
+            __asm__ volatile("buffer_inv sc0" ::: "memory");
         }
+        SBE_SV_T(t2);
         switch (q.r.op) {
             case kSvDecParse: serve_decode<SBE_DEC_PARSE_MESSAGE>(q.r.d, lds.win); break;
             case kSvDecEgress: serve_decode<SBE_DEC_ON_EGRESS>(q.r.d, lds.win); break;
@@ -3657,8 +3697,20 @@ __global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, ui
             default: break;
         }
         wsync();
-        __threadfence_system();  // every lane's result stores reach memory before done_seq
+        SBE_SV_T(t3);
+        // lane 0's system-scope release (an L2 write-back and a wait for every outstanding store of
+        // the wave) orders all lanes' result stores before done_seq
         if (lane == 0) sys_release(&slot->done_seq, seq);
+#ifdef SBE_SERVE_PROF
+        SBE_SV_T(t4);
+        if (lane == 0) {
+            g_serve_prof[0] += t1 - t0;
+            g_serve_prof[1] += t2 - t1;
+            g_serve_prof[2] += t3 - t2;
+            g_serve_prof[3] += t4 - t3;
+            g_serve_prof[4] += 1;
+        }
+#endif
         last = seq;
         if (q.r.op == kSvShutdown) break;
         t_idle = __builtin_amdgcn_s_memrealtime();
@@ -3962,6 +4014,17 @@ int sbe_server_destroy(sbe_server* s) {
     delete s;
     return rc;
 }
+
+#ifdef SBE_SERVE_PROF
+int sbe_debug_serve_prof(uint64_t* out16) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_serve_prof), 16 * sizeof(uint64_t));
+    if (e == hipSuccess) {
+        const uint64_t z[16] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_serve_prof), z, sizeof z);
+    }
+    return record_hip(e);
+}
+#endif
 
 #ifdef SBE_VT_GUARD
 // debug builds: the virtual-tile guard record (16 u64; [0] = 0 when nothing was caught), then cleared

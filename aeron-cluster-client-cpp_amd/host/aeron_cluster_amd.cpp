@@ -368,11 +368,14 @@ struct Pipeline {
 
 // Batches of at most this many records (and within the zero-copy size) go to the thread's serve
 // kernel (sbe_server_*: a resident wave polling a page-locked request slot, no launch per call);
-// larger ones to the batch kernels.  AERON_AMD_SERVE_RECORDS overrides (0: never serve).
+// larger ones to the batch kernels.  One wave walks a served batch tile by tile, so the batch
+// kernels overtake it between 64 and 256 fixed-256 records (profiles/r04_host_latency_serve.log:
+// 64 records served 16.8 / 10.1 µs encode / decode against 24.2 / 18.8 µs launched, 256 records
+// 50.0 / 28.6 against 28.1 / 19.6).  AERON_AMD_SERVE_RECORDS overrides (0: never serve).
 size_t serve_max_records() {
     static const size_t v = [] {
         const char* e = std::getenv("AERON_AMD_SERVE_RECORDS");
-        const long long x = e ? std::atoll(e) : 256;
+        const long long x = e ? std::atoll(e) : 96;
         return (size_t)std::min<long long>(std::max(0LL, x), SBE_SERVE_MAX_RECORDS);
     }();
     return v;

@@ -13,7 +13,10 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "aeron_cluster_amd.hpp"
+#include "sbecodec.h"
 #include "../oracle/sbe_oracle.h"
 
 using namespace aeron_cluster;
@@ -51,6 +54,49 @@ int main(int argc, char** argv) {
         const double ack = us_since(t0) / iters;
         std::printf("{\"op\": \"single_call\", \"encode_topic_message_us\": %.2f, \"parse_message_us\": %.2f, "
                     "\"decode_ack_us\": %.2f}\n", enc, par, ack);
+    }
+    // the serve kernel through the C ABI alone (no mirror): an empty request (a round trip and one
+    // store), one record decoded from host memory, one record encoded from host memory; outputs in
+    // page-locked memory through their device addresses
+    if (!only) {
+        sbe_server* srv = nullptr;
+        if (sbe_server_create(&srv, 0) == SBE_OK) {
+            void* pin = nullptr;
+            (void)hipHostMalloc(&pin, 1 << 16, hipHostMallocDefault);
+            void* dpin = nullptr;
+            (void)hipHostGetDevicePointer(&dpin, pin, 0);
+            uint8_t* d = static_cast<uint8_t*>(dpin);
+            const uint64_t ro[2] = {0, rec.size()};
+            sbe_decoded out{d, d + 64, reinterpret_cast<uint16_t*>(d + 128), reinterpret_cast<uint64_t*>(d + 192),
+                            reinterpret_cast<uint32_t*>(d + 256), reinterpret_cast<uint32_t*>(d + 320),
+                            reinterpret_cast<uint64_t*>(d + 384)};
+            std::vector<uint8_t> arena;
+            for (const std::string* f : {&topic, &type, &uuid, &payload, &headers}) arena.insert(arena.end(), f->begin(), f->end());
+            const uint32_t lens[5] = {(uint32_t)topic.size(), (uint32_t)type.size(), (uint32_t)uuid.size(),
+                                      (uint32_t)payload.size(), (uint32_t)headers.size()};
+            const uint64_t ts1 = 1;
+            sbe_tm_batch tb{arena.data(), nullptr, lens, &ts1};
+            sbe_tm_batch t0{nullptr, nullptr, nullptr, nullptr};
+            const int iters = 4000;
+            auto bench = [&](auto&& f) {
+                for (int i = 0; i < 200; ++i) f();
+                const auto t0c = clk::now();
+                for (int i = 0; i < iters; ++i) f();
+                return us_since(t0c) / iters;
+            };
+            const double ping = bench([&] {
+                (void)sbe_serve_encode_topic(srv, &t0, 0, 0, 0, d + 4096, 0, reinterpret_cast<uint64_t*>(d + 8192), nullptr);
+            });
+            const double dec1 = bench([&] { (void)sbe_serve_decode_host(srv, rec.data(), ro, 1, SBE_DEC_PARSE_MESSAGE, &out); });
+            const double enc1 = bench([&] {
+                (void)sbe_serve_encode_topic_host(srv, &tb, 1, 0, 0, d + 4096, 4096, reinterpret_cast<uint64_t*>(d + 8192),
+                                                  d + 8256);
+            });
+            std::printf("{\"op\": \"serve_abi\", \"empty_request_us\": %.2f, \"decode_1_host_us\": %.2f, "
+                        "\"encode_1_host_us\": %.2f}\n", ping, dec1, enc1);
+            (void)sbe_server_destroy(srv);
+            (void)hipHostFree(pin);
+        }
     }
     // batches: mirror (stage + H2D + kernels + D2H, pipelined over two streams) vs the oracle on
     // one thread.  decode = MessageParser::decode_batch (device descriptors + views, ParseResults on
