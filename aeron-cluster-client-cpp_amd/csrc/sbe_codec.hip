@@ -1472,7 +1472,7 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
 template <class LY>
 __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout, lds_cu8* inb, lds_i32* rt,
                                                 const TileSt& S, int32_t wrel, int32_t wlen, uintptr_t swb, int32_t nb,
-                                                int lane, int ra, int rb, Ph& ph) {
+                                                int lane, int ra, int rb, Ph& ph, bool spread = false) {
     SBE_TILE_SHAPE(LY);
     const int q = lane % kLpr, r = lane / kLpr;
     const bool live = S.rec_out != 0 && r >= ra && r < rb;
@@ -1517,7 +1517,9 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
 #ifndef SBE_REBAL_MIN  // A/B: chunks per lane above which a window is rebalanced
 #define SBE_REBAL_MIN kCpl
 #endif
-    if (__ballot(n_mine > SBE_REBAL_MIN)) {
+    // spread (the serve kernel: a lone wave with few records): rebalance whenever some lane has
+    // more than one chunk, so the chunks of a few records use the whole wave
+    if (__ballot(n_mine > (spread ? 1 : SBE_REBAL_MIN))) {
         const bool lead = q == 0 && nc > 0;
         const uint32_t C = lane_u32(wave_incl_scan(lead ? (uint32_t)nc : 0u, lane), kWave - 1);
         const uint32_t nrec = (uint32_t)__builtin_popcountll(__ballot(lead));
@@ -1539,7 +1541,7 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
         for (int k = 3; k >= 0; --k)
             if (((S4 >> (8 * k)) & 0xffu) <= (uint32_t)kWave) T = T0 + (uint32_t)k;
         const uint32_t mx = lane_u32(wave_incl_max((uint32_t)(n_mine > 0 ? n_mine : 0)), kWave - 1);
-        rebal = T != 0 && (kGuard ? T < mx : true);
+        rebal = T != 0 && (kGuard && !spread ? T < mx : true);
     }
     if (rebal) {
         // records of unequal lengths (variable-length records, or one long record): two lanes per
@@ -1929,7 +1931,7 @@ __device__ uint64_t g_vt_guard[16];
 
 template <class LY, bool kPacked, int kLen>
 __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first, uint64_t G, PackLds<LY, kPacked>& L,
-                                                uint64_t chunk_tiles = SBE_VT_CHUNK) {
+                                                uint64_t chunk_tiles = SBE_VT_CHUNK, bool spread = false) {
     SBE_TILE_SHAPE(LY);
     lds_u8* const wout = (lds_u8*)L.wout;
     lds_u8* const win_in = (lds_u8*)L.win + kInSlack;
@@ -2062,7 +2064,7 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
         if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
         ph.lap(0);
         if (fast) {
-            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb, ph)) {
+            if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb, ph, spread)) {
                 pack_window<LY>(a, wout, win_in, rt, bk, sbase, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb);
                 ph.lap(6);
             } else {
@@ -3631,7 +3633,8 @@ __device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>
         if (threadIdx.x == 0) a.out_off[0] = 0;
         return;
     }
-    enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L, 0);  // one chunk: the zero prefix of tile 0 is the only base
+    // one chunk (the zero prefix of tile 0 is the only base), chunks spread over the wave
+    enc_pack_run_vt<LY, true, kLen>(a, 0, 1, L, 0, true);
 }
 
 #ifdef SBE_SERVE_PROF

@@ -79,6 +79,18 @@ int main(int argc, char** argv) {
     run("empty", [&] { (void)sbe_serve_encode_topic(srv, &t0, 0, 0, 0, out, 0, off, nullptr); });
     run("decode_1_host", [&] { (void)sbe_serve_decode_host(srv, rec.data(), ro, 1, SBE_DEC_PARSE_MESSAGE, &dd); });
     run("encode_1_host", [&] { (void)sbe_serve_encode_topic_host(srv, &tb, 1, 0, 0, out, 4096, off, d + 8256); });
+    // a -DSBE_PACK_PHASES build: the pack loop's phase clocks (s_memtime) of the last served encode
+    if (auto ph = reinterpret_cast<int (*)(uint64_t*, int)>(dlsym(h, "sbe_debug_phases"))) {
+        uint64_t v[8] = {};
+        (void)sbe_serve_encode_topic_host(srv, &tb, 1, 0, 0, out, 4096, off, d + 8256);
+        if (ph(v, 1) == 0)
+            std::printf("{\"probe\": \"encode_1_phases_clk\", \"prologue_and_issue\": %llu, \"chunks\": %llu, "
+                        "\"zone_fixup\": %llu, \"literals\": %llu, \"store\": %llu, \"stage_write\": %llu, "
+                        "\"slow_path\": %llu, \"prepare_next\": %llu}\n",
+                        (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2],
+                        (unsigned long long)v[3], (unsigned long long)v[4], (unsigned long long)v[5],
+                        (unsigned long long)v[6], (unsigned long long)v[7]);
+    }
     sbe_server_destroy(srv);
     return 0;
 }
