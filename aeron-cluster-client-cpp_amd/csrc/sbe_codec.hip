@@ -1447,10 +1447,10 @@ __device__ __forceinline__ void pack_window(const EncArgs& ea, lds_u8* wout, lds
                                             uint64_t* sbase, const TileSt& S, int32_t wrel, int32_t wlen,
                                             uintptr_t swb, int32_t nb, int lane, int ra = 0, int rb = LY::kRpt) {
     SBE_TILE_SHAPE(LY);
-    // chunks per lane for this window: 1, 2, 4 or 8 (the lane's range: 16 kk = 2^lg bytes)
-    const int kk = wlen <= 1024 ? 1 : wlen <= 2048 ? 2 : wlen <= 4096 ? 4 : kCpl;
-    const int lg = kk == 1 ? 4 : kk == 2 ? 5 : kk == 4 ? 6 : 7;
-    static_assert(kCpl == 8 || kCpl == 4, "chunk ownership sizes");
+    // chunks per lane for this window: 1, 2, 4, 8 or 16 (the lane's range: 16 kk = 2^lg bytes)
+    const int kk = wlen <= 1024 ? 1 : wlen <= 2048 ? 2 : wlen <= 4096 ? 4 : wlen <= 8192 ? 8 : kCpl;
+    const int lg = kk == 1 ? 4 : kk == 2 ? 5 : kk == 4 ? 6 : kk == 8 ? 7 : 8;
+    static_assert(kCpl == 16 || kCpl == 8 || kCpl == 4, "chunk ownership sizes");
     const bool outside = build_tables<LY>(rt, bk, sbase, S, wrel, wlen, swb, nb, ra, rb, lg, lane);
     wsync();
     chunk_pass<LY>(wout, inb, rt, bk, wlen, nb, kk, lg, lane);
