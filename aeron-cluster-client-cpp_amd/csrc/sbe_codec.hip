@@ -3580,9 +3580,14 @@ enum : uint32_t {
     kSvTmWire, kSvTmRef, kSvTmPub, kSvTmsWire, kSvTmsRef, kSvLite2, kSvLite3
 };
 
+// op | kSvPlanned: an encode whose tile sums the host supplied (e.tsum / e.bsum as sbe_enc_sums
+// writes them), run by the tile loop over the request's workgroups
+constexpr uint32_t kSvPlanned = 0x100u;
 struct ServeReq {
     uint32_t op;
     uint32_t inl;  // bytes of the slot's inline area to copy to the device scratch before running
+    uint32_t nwg;  // workgroups that take part (1: the leader alone)
+    uint32_t tag;  // the request's sequence number (a follower checks its copy against the header)
     EncArgs e;
     DecArgs d;
 };
@@ -3604,6 +3609,20 @@ struct ServeSlot {
     alignas(64) uint8_t inl[kServeInline];
 };
 
+// Device-memory side of a multi-workgroup server: the leader (workgroup 0) polls the host slot and
+// republishes a request for the followers here (an L2 poll instead of a PCIe one); arrive counts
+// the workgroups done with the current request, exited the workgroups gone at an idle exit.
+// hdr packs seq (bits 0-31), nwg (32-47) and op (48-63) in one word, so a follower learns with one
+// atomic load whether it takes part; only those that do read req, which cannot change before they
+// have counted themselves in arrive.
+struct ServeDev {
+    alignas(64) uint64_t hdr;
+    uint32_t quit;  // the launch epoch whose leader went idle (its followers exit)
+    alignas(64) uint32_t arrive;
+    uint32_t exited;
+    alignas(64) ServeReq req;
+};
+
 union ServeLds {
     PackLds<LayTM, true> tm;
     PackLds<LayTMS, true> tms;
@@ -3615,22 +3634,33 @@ union ServeLds {
 __device__ __forceinline__ uint32_t sys_acquire(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Polls are relaxed loads that bypass the non-coherent caches; the acquire (its cache
+// invalidation) is paid once, when the value has changed: an acquiring load on every poll
+// invalidates the L2 each time, which a resident server must not do to the kernels around it.
+__device__ __forceinline__ uint32_t sys_poll(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void sys_release(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <uint32_t kMode>
-__device__ __forceinline__ void serve_decode(const DecArgs& a, uint32_t* win) {
-    for (uint64_t t = 0; t * kTile < a.n; ++t) {
+__device__ __forceinline__ void serve_decode(const DecArgs& a, uint32_t* win, uint32_t first, uint32_t G) {
+    for (uint64_t t = first; t * kTile < a.n; t += G) {
         dec_tile<kMode, kWin, true>(a, t, win);
         wsync();
     }
 }
 
 template <class LY, int kLen>
-__device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>& L) {
+__device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>& L, bool planned, uint32_t first,
+                                             uint32_t G) {
     if (a.n == 0) {
-        if (threadIdx.x == 0) a.out_off[0] = 0;
+        if (threadIdx.x == 0 && first == 0) a.out_off[0] = 0;
+        return;
+    }
+    if (planned) {  // the host's tile sums: the batch kernel's tile loop over the request's workgroups
+        enc_pack_run<LY, true, kLen>(a, first, G, L);
         return;
     }
     // one chunk (the zero prefix of tile 0 is the only base), chunks spread over the wave
@@ -3648,78 +3678,155 @@ __device__ __forceinline__ void serve_encode(const EncArgs& a, PackLds<LY, true>
 #define SBE_SV_T(x)
 #endif
 
-// idle_ticks: s_memrealtime ticks (100 MHz) without a request before the kernel exits; scratch:
-// the device copy of the inline area.
-__global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks, uint8_t* scratch) {
+// idle_ticks: s_memrealtime ticks (100 MHz) without a request before the leader exits; scratch:
+// the device copy of the inline area; dev / epoch: the followers' mailbox and this launch's number.
+// Workgroup 0 (the leader) polls the host slot.  A request for more than one workgroup is
+// republished in dev; every taking part workgroup runs its share (decode: tiles first, first + G,
+// ...; planned encode: the tile loop), makes its stores visible system-wide and counts itself in
+// dev->arrive; the last one resets the count and publishes done_seq.  On an idle exit the leader
+// posts its epoch in dev->quit, and the last workgroup to leave clears the host's alive flag.
+__global__ __launch_bounds__(kWave, 1) void sbe_serve_kernel(ServeSlot* slot, uint64_t idle_ticks, uint8_t* scratch,
+                                                             ServeDev* dev, uint32_t epoch) {
     __shared__ ServeLds lds;
     const int lane = threadIdx.x;
-    uint32_t last = __builtin_amdgcn_readfirstlane(sys_acquire(&slot->done_seq));
+    const uint32_t wg = blockIdx.x;
+    const bool leader = wg == 0;
+    auto dev_hdr = [&]() -> uint64_t {  // relaxed: the caller fences once it sees a change
+        const uint64_t h = __hip_atomic_load(&dev->hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return uniform64(h);
+    };
+    uint32_t last = leader ? __builtin_amdgcn_readfirstlane(sys_acquire(&slot->done_seq)) : (uint32_t)dev_hdr();
     uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        const uint32_t seq = __builtin_amdgcn_readfirstlane(sys_acquire(&slot->req_seq));
-        if (seq == last) {
-            if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) break;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
+        uint32_t seq;
+        uint64_t h = 0;
+        if (leader) {
+            seq = __builtin_amdgcn_readfirstlane(sys_poll(&slot->req_seq));
+            if (seq == last) {
+                if (__builtin_amdgcn_s_memrealtime() - t_idle > idle_ticks) {
+                    if (lane == 0) __hip_atomic_store(&dev->quit, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request and inputs, fresh
+        } else {
+            h = dev_hdr();
+            seq = (uint32_t)h;
+            if (seq == last) {
+                if (__builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&dev->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == epoch)
+                    break;
+                __builtin_amdgcn_s_sleep(16);
+                continue;
+            }
+            // system scope: the inputs may have come from the host or a copy engine since
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         SBE_SV_T(t0);
-        // the request, one dword per lane (after the acquire: fresh from host memory)
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&slot->req);
-        const uint32_t v = lane < kReqWords ? __builtin_nontemporal_load(w + lane) : 0u;
-        typedef __attribute__((address_space(1))) u32x4 g_v4;
-        const g_v4* inl = reinterpret_cast<const g_v4*>(reinterpret_cast<uintptr_t>(slot->inl));
-        const u32x4 i0 = inl[lane];  // the first KiB of inline input, with the request (unused if none)
         union {
             ServeReq r;
             uint32_t u[kReqWords];
         } q;
+        if (leader) {
+            // the request, one dword per lane (after the acquire: fresh from host memory)
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&slot->req);
+            const uint32_t v = lane < kReqWords ? __builtin_nontemporal_load(w + lane) : 0u;
+            typedef __attribute__((address_space(1))) u32x4 g_v4;
+            const g_v4* inl = reinterpret_cast<const g_v4*>(reinterpret_cast<uintptr_t>(slot->inl));
+            const u32x4 i0 = inl[lane];  // the first KiB of inline input, with the request (unused if none)
 #pragma unroll
-        for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
-        SBE_SV_T(t1);
-        if (q.r.inl) {
-            g_v4* dst = reinterpret_cast<g_v4*>(reinterpret_cast<uintptr_t>(scratch));
-            if (16u * (uint32_t)lane < q.r.inl) dst[lane] = i0;
-            for (uint32_t o = 1024u + 16u * (uint32_t)lane; o < q.r.inl; o += 1024u) dst[o >> 4] = inl[o >> 4];
-            // the wave's stores complete (this XCD's L2 holds them) and no line of an earlier
-            // request stays in the CU's vector L1, before its reads of the scratch
-            __builtin_amdgcn_s_waitcnt(0);
-            __asm__ volatile("buffer_inv sc0" ::: "memory");
+            for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
+            if (q.r.inl) {
+                g_v4* dst = reinterpret_cast<g_v4*>(reinterpret_cast<uintptr_t>(scratch));
+                if (16u * (uint32_t)lane < q.r.inl) dst[lane] = i0;
+                for (uint32_t o = 1024u + 16u * (uint32_t)lane; o < q.r.inl; o += 1024u) dst[o >> 4] = inl[o >> 4];
+                // the wave's stores complete (this XCD's L2 holds them) and no line of an earlier
+                // request stays in the CU's vector L1, before its reads of the scratch
+                __builtin_amdgcn_s_waitcnt(0);
+                __asm__ volatile("buffer_inv sc0" ::: "memory");
+            }
+            if (q.r.nwg > 1) {  // republish for the followers (agent-scope release: other XCDs' L2s)
+                uint32_t* dw = reinterpret_cast<uint32_t*>(&dev->req);
+                if (lane < kReqWords) dw[lane] = v;
+                const uint64_t hv = (uint64_t)seq | ((uint64_t)(q.r.nwg & 0xffffu) << 32) | ((uint64_t)(q.r.op & 0xffffu) << 48);
+                if (lane == 0) __hip_atomic_store(&dev->hdr, hv, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            const uint32_t hn = (uint32_t)(h >> 32) & 0xffffu, hop = (uint32_t)(h >> 48);
+            if (wg < hn) {  // taking part: the request stays put until this workgroup has arrived
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(&dev->req);
+                const uint32_t v = lane < kReqWords ? w[lane] : 0u;
+#pragma unroll
+                for (int i = 0; i < kReqWords; ++i) q.u[i] = __builtin_amdgcn_readlane(v, i);
+                if (q.r.tag != seq) {  // not the request the header names: take no part
+                    q.r.op = hop;
+                    q.r.nwg = 0;
+                }
+            } else {
+                q.r.op = hop;
+                q.r.nwg = hn;
+            }
         }
-        SBE_SV_T(t2);
-        switch (q.r.op) {
-            case kSvDecParse: serve_decode<SBE_DEC_PARSE_MESSAGE>(q.r.d, lds.win); break;
-            case kSvDecEgress: serve_decode<SBE_DEC_ON_EGRESS>(q.r.d, lds.win); break;
-            case kSvDecLite: serve_decode<SBE_DEC_LITE>(q.r.d, lds.win); break;
-            case kSvTmWire: serve_encode<LayTM, kLenWire>(q.r.e, lds.tm); break;
-            case kSvTmRef: serve_encode<LayTM, kLenRef>(q.r.e, lds.tm); break;
-            case kSvTmPub: serve_encode<LayTM, kLenPub>(q.r.e, lds.tm); break;
-            case kSvTmsWire: serve_encode<LayTMS, kLenWire>(q.r.e, lds.tms); break;
-            case kSvTmsRef: serve_encode<LayTMS, kLenRef>(q.r.e, lds.tms); break;
-            case kSvLite2: serve_encode<LayL2, kLenWire>(q.r.e, lds.l2); break;
-            case kSvLite3: serve_encode<LayL3, kLenWire>(q.r.e, lds.l3); break;
-            default: break;
-        }
-        wsync();
-        SBE_SV_T(t3);
-        // lane 0's system-scope release (an L2 write-back and a wait for every outstanding store of
-        // the wave) orders all lanes' result stores before done_seq
-        if (lane == 0) sys_release(&slot->done_seq, seq);
-#ifdef SBE_SERVE_PROF
-        SBE_SV_T(t4);
-        if (lane == 0) {
-            g_serve_prof[0] += t1 - t0;
-            g_serve_prof[1] += t2 - t1;
-            g_serve_prof[2] += t3 - t2;
-            g_serve_prof[3] += t4 - t3;
-            g_serve_prof[4] += 1;
-        }
-#endif
         last = seq;
-        if (q.r.op == kSvShutdown) break;
+        SBE_SV_T(t1);
+        SBE_SV_T(t2);
+        const uint32_t G = leader && q.r.nwg == 0 ? 1u : q.r.nwg;
+        const uint32_t op = q.r.op & ~kSvPlanned;
+        const bool planned = (q.r.op & kSvPlanned) != 0;
+        if (wg < G) {
+            switch (op) {
+                case kSvDecParse: serve_decode<SBE_DEC_PARSE_MESSAGE>(q.r.d, lds.win, wg, G); break;
+                case kSvDecEgress: serve_decode<SBE_DEC_ON_EGRESS>(q.r.d, lds.win, wg, G); break;
+                case kSvDecLite: serve_decode<SBE_DEC_LITE>(q.r.d, lds.win, wg, G); break;
+                case kSvTmWire: serve_encode<LayTM, kLenWire>(q.r.e, lds.tm, planned, wg, G); break;
+                case kSvTmRef: serve_encode<LayTM, kLenRef>(q.r.e, lds.tm, planned, wg, G); break;
+                case kSvTmPub: serve_encode<LayTM, kLenPub>(q.r.e, lds.tm, planned, wg, G); break;
+                case kSvTmsWire: serve_encode<LayTMS, kLenWire>(q.r.e, lds.tms, planned, wg, G); break;
+                case kSvTmsRef: serve_encode<LayTMS, kLenRef>(q.r.e, lds.tms, planned, wg, G); break;
+                case kSvLite2: serve_encode<LayL2, kLenWire>(q.r.e, lds.l2, planned, wg, G); break;
+                case kSvLite3: serve_encode<LayL3, kLenWire>(q.r.e, lds.l3, planned, wg, G); break;
+                default: break;
+            }
+            wsync();
+            SBE_SV_T(t3);
+            if (G == 1) {
+                // lane 0's system-scope release (an L2 write-back and a wait for every outstanding
+                // store of the wave) orders all lanes' result stores before done_seq
+                if (lane == 0) sys_release(&slot->done_seq, seq);
+            } else {
+                // this workgroup's results visible system-wide, then counted; the last one publishes
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                if (lane == 0) {
+                    const uint32_t old = __hip_atomic_fetch_add(&dev->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                    if (old == G - 1) {
+                        __hip_atomic_store(&dev->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        sys_release(&slot->done_seq, seq);
+                    }
+                }
+            }
+#ifdef SBE_SERVE_PROF
+            SBE_SV_T(t4);
+            if (leader && lane == 0) {
+                g_serve_prof[0] += t1 - t0;
+                g_serve_prof[1] += t2 - t1;
+                g_serve_prof[2] += t3 - t2;
+                g_serve_prof[3] += t4 - t3;
+                g_serve_prof[4] += 1;
+            }
+#endif
+        }
+        if (op == kSvShutdown) break;
         t_idle = __builtin_amdgcn_s_memrealtime();
     }
     __threadfence_system();
-    if (lane == 0) sys_release(&slot->alive, 0u);
+    if (lane == 0) {
+        const uint32_t n = gridDim.x;
+        const uint32_t old = n > 1 ? __hip_atomic_fetch_add(&dev->exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0u;
+        if (old == n - 1) sys_release(&slot->alive, 0u);
+    }
 }
 
 }  // namespace
@@ -3728,8 +3835,10 @@ struct sbe_server {
     ServeSlot* h = nullptr;  // page-locked slot, host address
     ServeSlot* d = nullptr;  // its device address
     uint64_t* ws = nullptr;  // device: zero tile sums (2 u64, never written) + the pack's sink
+    ServeDev* dev = nullptr; // device: the followers' mailbox and counters
     hipStream_t stream = nullptr;
     uint32_t seq = 0;
+    uint32_t nwg = 1;        // workgroups per launch
     uint64_t idle_ticks = 0;
     uint64_t requests = 0, launches = 0;
 };
@@ -3742,9 +3851,11 @@ constexpr size_t kServeWsBytes = kServeScratchOff + kServeInline;
 
 int serve_launch(sbe_server* s) {
     __atomic_store_n(&s->h->alive, 1u, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(sbe_serve_kernel, dim3(1), dim3(kWave), 0, s->stream, s->d, s->idle_ticks,
-                       reinterpret_cast<uint8_t*>(s->ws) + kServeScratchOff);
+    // the exit count of the previous launch back to 0 (stream order: before the kernel starts)
+    if (const int rc = record_hip(hipMemsetAsync(&s->dev->exited, 0, sizeof(uint32_t), s->stream))) return rc;
     ++s->launches;
+    hipLaunchKernelGGL(sbe_serve_kernel, dim3(s->nwg), dim3(kWave), 0, s->stream, s->d, s->idle_ticks,
+                       reinterpret_cast<uint8_t*>(s->ws) + kServeScratchOff, s->dev, (uint32_t)s->launches);
     return record_hip(hipGetLastError());
 }
 
@@ -3753,7 +3864,9 @@ int serve_call(sbe_server* s, const ServeReq& r) {
     if (!s || !s->h) return SBE_EINVAL;
     ServeSlot* h = s->h;
     std::memcpy(&h->req, &r, sizeof r);
+    if (h->req.nwg == 0) h->req.nwg = 1;
     const uint32_t seq = ++s->seq;
+    h->req.tag = seq;
     __atomic_store_n(&h->req_seq, seq, __ATOMIC_RELEASE);
     ++s->requests;
     const auto t0 = std::chrono::steady_clock::now();
@@ -3786,6 +3899,25 @@ int serve_encode_req(sbe_server* s, const EncReq& q, uint64_t n, uint64_t ts_def
     r.op = op;
     r.e = EncArgs{q.arena, nullptr, q.str_len, q.ts, q.tid, q.tmpl, q.term_id, q.sess_id, n, ts_default,
                   out, out_capacity, out_off, status, s->ws, s->ws, reinterpret_cast<uint8_t*>(s->ws + 2)};
+    return serve_call(s, r);
+}
+
+// Planned encode: device-visible inputs plus the tile sums the caller computed (the layout
+// sbe_enc_sums writes), run by the tile loop over up to the server's workgroups.
+template <class LY>
+int serve_encode_planned(sbe_server* s, const EncReq& q, uint64_t n, uint64_t ts_default, uint32_t flags,
+                         uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                         const uint64_t* tile_sums, const uint64_t* sb_sums, uint32_t op) {
+    if (!s) return SBE_EINVAL;
+    if (const int rc = enc_check<LY>(q, n, flags, out, out_off)) return rc;
+    if (n > SBE_SERVE_MAX_RECORDS || (n && (q.str_off || !tile_sums || !sb_sums))) return SBE_EINVAL;
+    const uint64_t tiles = (n + LY::kRpt - 1) / LY::kRpt;
+    ServeReq r{};
+    r.op = op | kSvPlanned;
+    r.nwg = (uint32_t)(tiles < s->nwg ? (tiles ? tiles : 1) : s->nwg);
+    r.e = EncArgs{q.arena, nullptr, q.str_len, q.ts, q.tid, q.tmpl, q.term_id, q.sess_id, n, ts_default,
+                  out, out_capacity, out_off, status, const_cast<uint64_t*>(tile_sums), const_cast<uint64_t*>(sb_sums),
+                  reinterpret_cast<uint8_t*>(s->ws + 2)};
     return serve_call(s, r);
 }
 
@@ -3971,11 +4103,15 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
     return sbe_decode_batch_sized(in, rec_off, n, 0, mode, out, stream);
 }
 
-int sbe_server_create(sbe_server** srv, uint32_t idle_us) {
+int sbe_server_create(sbe_server** srv, uint32_t idle_us) { return sbe_server_create_wide(srv, idle_us, 1); }
+
+int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgroups) {
     if (!srv) return SBE_EINVAL;
     *srv = nullptr;
+    if (workgroups == 0 || workgroups > SBE_SERVE_MAX_WORKGROUPS) return SBE_EINVAL;
     sbe_server* s = new (std::nothrow) sbe_server;
     if (!s) return SBE_EINVAL;
+    s->nwg = workgroups;
     s->idle_ticks = 100ull * (idle_us ? idle_us : 20000u);
     void* h = nullptr;
     void* d = nullptr;
@@ -3985,8 +4121,12 @@ int sbe_server_create(sbe_server** srv, uint32_t idle_us) {
         e = hipHostGetDevicePointer(&d, h, 0);
     }
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s->ws), kServeWsBytes);
+    // the followers' mailbox uncached: their polls and the request copy bypass the XCDs' L2s, which
+    // do not see each other's lines inside a kernel
+    if (e == hipSuccess) e = hipExtMallocWithFlags(reinterpret_cast<void**>(&s->dev), sizeof(ServeDev), hipDeviceMallocUncached);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMemsetAsync(s->ws, 0, kServeWsBytes, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->dev, 0, sizeof(ServeDev), s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     s->h = static_cast<ServeSlot*>(h);
     s->d = static_cast<ServeSlot*>(d);
@@ -4005,6 +4145,7 @@ int sbe_server_destroy(sbe_server* s) {
     if (s->h && s->stream && __atomic_load_n(&s->h->alive, __ATOMIC_ACQUIRE)) {
         ServeReq r{};
         r.op = kSvShutdown;
+        r.nwg = s->nwg;  // every workgroup sees it
         rc = serve_call(s, r);
     }
     if (s->stream) {
@@ -4013,6 +4154,7 @@ int sbe_server_destroy(sbe_server* s) {
         (void)hipStreamDestroy(s->stream);
     }
     if (s->ws) (void)hipFree(s->ws);
+    if (s->dev) (void)hipFree(s->dev);
     if (s->h) (void)hipHostFree(s->h);
     delete s;
     return rc;
@@ -4105,6 +4247,48 @@ int sbe_serve_encode_lite_host(sbe_server* srv, const sbe_lite_batch* in, uint64
     return serve_encode_host<LayL3>(srv, q, n, 0, 0, out, out_capacity, out_off, status, kSvLite3);
 }
 
+int sbe_serve_encode_topic_planned(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                   uint32_t flags, uint8_t* out, uint64_t out_capacity, uint64_t* out_off,
+                                   uint8_t* status, const uint64_t* tile_sums, const uint64_t* sb_sums) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, 0, 0};
+    return serve_encode_planned<LayTM>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status, tile_sums,
+                                       sb_sums, serve_tm_op(false, flags));
+}
+
+int sbe_serve_encode_session_planned(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                     uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id,
+                                     uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                                     const uint64_t* tile_sums, const uint64_t* sb_sums) {
+    if (!in) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->timestamp, nullptr, 0, leadership_term_id, cluster_session_id};
+    return serve_encode_planned<LayTMS>(srv, q, n, ts_default, flags, out, out_capacity, out_off, status, tile_sums,
+                                        sb_sums, serve_tm_op(true, flags));
+}
+
+int sbe_serve_encode_lite_planned(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id,
+                                  uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                                  const uint64_t* tile_sums, const uint64_t* sb_sums) {
+    const uint32_t nf = sbe_lite_fields(template_id);
+    if (!in || nf == 0) return SBE_EINVAL;
+    if (n && !in->topic_id) return SBE_EINVAL;
+    EncReq q{in->arena, in->str_off, in->str_len, in->sequence, in->topic_id, template_id, 0, 0};
+    if (nf == 2)
+        return serve_encode_planned<LayL2>(srv, q, n, 0, 0, out, out_capacity, out_off, status, tile_sums, sb_sums,
+                                           kSvLite2);
+    return serve_encode_planned<LayL3>(srv, q, n, 0, 0, out, out_capacity, out_off, status, tile_sums, sb_sums,
+                                       kSvLite3);
+}
+
+uint32_t sbe_encode_tile_records(uint32_t layout) {
+    switch (layout) {
+        case SBE_LAYOUT_TOPIC: return LayTM::kRpt;
+        case SBE_LAYOUT_SESSION: return LayTMS::kRpt;
+        case SBE_LAYOUT_LITE: return LayL2::kRpt;
+        default: return 0;
+    }
+}
+
 int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                           const sbe_decoded* out) {
     if (!srv || !srv->h) return SBE_EINVAL;
@@ -4122,6 +4306,7 @@ int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* re
     ServeReq r{};
     r.op = mode == SBE_DEC_ON_EGRESS ? kSvDecEgress : mode == SBE_DEC_LITE ? kSvDecLite : kSvDecParse;
     r.inl = (uint32_t)(o_data + bytes);
+    r.nwg = (uint32_t)std::min<uint64_t>(srv->nwg, (n + kTile - 1) / kTile);
     r.d = DecArgs{scr + o_data, reinterpret_cast<const uint64_t*>(scr), n, out->status, out->flags, out->hdr,
                   out->ts, out->view_off, out->view_len, mode == SBE_DEC_PARSE_MESSAGE ? out->seq : nullptr};
     return serve_call(srv, r);
@@ -4135,6 +4320,7 @@ int sbe_serve_decode(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off
     if (n == 0) return SBE_OK;
     ServeReq r{};
     r.op = mode == SBE_DEC_ON_EGRESS ? kSvDecEgress : mode == SBE_DEC_LITE ? kSvDecLite : kSvDecParse;
+    r.nwg = (uint32_t)std::min<uint64_t>(srv->nwg, (n + kTile - 1) / kTile);
     r.d = DecArgs{in,          rec_off,      n,           out->status,
                   out->flags,  out->hdr,     out->ts,     out->view_off,
                   out->view_len, mode == SBE_DEC_PARSE_MESSAGE ? out->seq : nullptr};

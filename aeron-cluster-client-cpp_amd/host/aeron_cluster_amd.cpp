@@ -381,6 +381,27 @@ size_t serve_max_records() {
     return v;
 }
 
+// Batches of up to this many records that the single wave does not take go to the server's other
+// workgroups as a whole (decode: tile per workgroup; encode: the tile loop with tile sums from the
+// host's plan) instead of a launch: AERON_AMD_SERVE_WIDE_RECORDS (0: never); the server has
+// AERON_AMD_SERVE_WGS workgroups (default 64).
+size_t serve_wide_max_records() {
+    static const size_t v = [] {
+        const char* e = std::getenv("AERON_AMD_SERVE_WIDE_RECORDS");
+        const long long x = e ? std::atoll(e) : 4096;
+        return (size_t)std::min<long long>(std::max(0LL, x), SBE_SERVE_MAX_RECORDS);
+    }();
+    return v;
+}
+uint32_t serve_workgroups() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("AERON_AMD_SERVE_WGS");
+        const long long x = e ? std::atoll(e) : 64;
+        return (uint32_t)std::min<long long>(std::max(1LL, x), SBE_SERVE_MAX_WORKGROUPS);
+    }();
+    return v;
+}
+
 // How long an idle serve kernel keeps polling before it exits (AERON_AMD_SERVE_IDLE_US, default
 // 20 ms); the next small call relaunches it.
 uint32_t serve_idle_us() {
@@ -410,9 +431,10 @@ struct Ctx {
     }
     // The serve kernel for a batch of n records, or nullptr (too large, disabled, or unavailable:
     // the batch kernels take it).
-    sbe_server* server(size_t n) {
-        if (n == 0 || n > serve_max_records() || srv_failed) return nullptr;
-        if (!srv && sbe_server_create(&srv, serve_idle_us()) != SBE_OK) {
+    // wide: a batch for several workgroups (up to serve_wide_max_records())
+    sbe_server* server(size_t n, bool wide = false) {
+        if (n == 0 || n > (wide ? serve_wide_max_records() : serve_max_records()) || srv_failed) return nullptr;
+        if (!srv && sbe_server_create_wide(&srv, serve_idle_us(), serve_workgroups()) != SBE_OK) {
             srv = nullptr;
             srv_failed = true;
             (void)hipGetLastError();
@@ -787,7 +809,7 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
                     reinterpret_cast<uint32_t*>(dblk + d.o_off),
                     reinterpret_cast<uint32_t*>(dblk + d.o_len),
                     parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
-    if (sbe_server* srv = c.server(n)) {  // larger than the inline area: inputs through the staging buffer
+    if (sbe_server* srv = c.server(n, true)) {  // inputs through the staging buffer, several workgroups
         if (sbe_serve_decode(srv, drec, reinterpret_cast<const uint64_t*>(dpin), n, mode, &out) != SBE_OK)
             fail("sbe_serve_decode");
         return true;
@@ -892,6 +914,7 @@ struct EncodePlan {
     uint32_t overhead = 0;
     bool e109 = true;
     bool wrap16 = false;
+    uint32_t layout = SBE_LAYOUT_TOPIC;  // tile shape of the kernels (planned serve encodes)
 };
 
 // Encode n records (nf strings, a u64 and a u32 each) through the chunk pipeline.  launch(...)
@@ -975,7 +998,14 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         const Stage s = stage_layout(0, n);
         Pipeline::Slot& sl = P.slot[0];
         if (s.bytes <= zero_copy_max_bytes()) {
-            sl.pin.need(s.bytes);
+            // one wave and inputs in its request slot (small batches), or several workgroups with
+            // the tile sums of this plan after the staged inputs, or the batch launches
+            sbe_server* srv = c.server(n);
+            sbe_server* wsrv = srv ? nullptr : c.server(n, true);
+            const size_t R = sbe_encode_tile_records(plan.layout), SB = 128 * R;
+            const size_t tiles = (n + R - 1) / R, sbs = (n + SB - 1) / SB;
+            const size_t o_sums = al16(s.bytes);
+            sl.pin.need(wsrv ? o_sums + 16 * (tiles + sbs) : s.bytes);
             uint8_t* dp = sl.pin.dev;
             // offsets, status and stream share one block (above): one lookup for all three
             uint8_t* const hb = reinterpret_cast<uint8_t*>(b.offsets.data());
@@ -985,19 +1015,37 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
             uint8_t* dst = db ? db + (b.status.data() - hb) : nullptr;
             if (dp && doff && dst && (dbytes || pout[n] == 0)) {
                 stage_fill(sl.pin.b(), s, 0, n);
+                const uint64_t* tsums = nullptr;
+                const uint64_t* bsums = nullptr;
+                if (wsrv) {  // what sbe_enc_sums would compute, from the plan's prefix sums
+                    uint64_t* ts = reinterpret_cast<uint64_t*>(sl.pin.b() + o_sums);
+                    uint64_t* bs = ts + 2 * tiles;
+                    for (size_t t = 0; t < tiles; ++t) {
+                        const size_t r0 = t * R, b0 = (r0 / SB) * SB;
+                        ts[2 * t] = pout[r0] - pout[b0];
+                        ts[2 * t + 1] = pin[r0] - pin[b0];
+                    }
+                    for (size_t b = 0; b < sbs; ++b) {
+                        const size_t r0 = b * SB, r1 = std::min(n, r0 + SB);
+                        bs[2 * b] = pout[r1] - pout[r0];
+                        bs[2 * b + 1] = pin[r1] - pin[r0];
+                    }
+                    tsums = reinterpret_cast<const uint64_t*>(dp + o_sums);
+                    bsums = tsums + 2 * tiles;
+                    srv = wsrv;
+                }
                 tr.lap(tr.stage);
                 PipeGuard zguard(c);
-                sbe_server* srv = c.server(n);
                 const size_t ws_bytes = srv ? 16 : sbe_encode_workspace_size(n);
                 c.d_ws.need(ws_bytes);
-                // the serve kernel takes the staged inputs by their host addresses (copied into its
-                // request slot when they fit, else read through their device addresses)
-                const uint8_t* ip = srv && s.bytes <= SBE_SERVE_INLINE_BYTES ? sl.pin.b() : dp;
+                // the single-wave serve takes the staged inputs by their host addresses (copied into
+                // its request slot when they fit, else read through their device addresses)
+                const uint8_t* ip = srv && !wsrv && s.bytes <= SBE_SERVE_INLINE_BYTES ? sl.pin.b() : dp;
                 // a batch whose records all fail (E109) has no bytes: the kernels still want a
                 // 16-B aligned output pointer, which they never write at capacity 0
                 launch(srv, ip != dp, ip, reinterpret_cast<const uint32_t*>(ip + s.o_len),
                        reinterpret_cast<const uint64_t*>(ip + s.o_u64), reinterpret_cast<const uint32_t*>(ip + s.o_u32), n,
-                       dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst, c.d_ws.b(), ws_bytes, P.s_comp);
+                       dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst, c.d_ws.b(), ws_bytes, P.s_comp, tsums, bsums);
                 tr.lap(tr.enqueue);
                 if (!srv) hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
                 zguard.release();
@@ -1033,7 +1081,8 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         uint8_t* dout = sl.d_out.b();
         launch(nullptr, false, di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
                reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
-               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st);
+               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st, nullptr,
+               nullptr);
         st = P.copy_out(sl);
         if (out_bytes) hip_check(hipMemcpyAsync(b.bytes.data() + out_lo, dout, out_bytes, hipMemcpyDeviceToHost, st), "D2H");
         hip_check(hipMemcpyAsync(hmeta + k * meta_stride, dout + d_off, (m + 1) * 8 + m, hipMemcpyDeviceToHost, st), "D2H");
@@ -1229,15 +1278,21 @@ EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength
                     (session ? SBE_SESSION_HDR_LEN : 0u);
     plan.e109 = length != EncodeLength::Publish;
     plan.wrap16 = length == EncodeLength::Publish;
+    plan.layout = session ? SBE_LAYOUT_SESSION : SBE_LAYOUT_TOPIC;
     return run_encode(
         msgs.size(), 5, [&](size_t i, int k) { return tm_field(msgs[i], k); },
         [&](size_t i) { return (uint64_t)msgs[i].timestamp; }, [](size_t) { return 0u; }, plan,
         [&](sbe_server* srv, bool host_in, const uint8_t* arena, const uint32_t* len, const uint64_t* ts,
             const uint32_t*, size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb,
-            hipStream_t s) {
+            hipStream_t s, const uint64_t* tsums, const uint64_t* bsums) {
             sbe_tm_batch in{arena, nullptr, len, ts};
             int rc;
-            if (srv && host_in)
+            if (srv && tsums)
+                rc = session ? sbe_serve_encode_session_planned(srv, &in, m, ts_default, flags, term, sess, out, cap, off,
+                                                                st, tsums, bsums)
+                             : sbe_serve_encode_topic_planned(srv, &in, m, ts_default, flags, out, cap, off, st, tsums,
+                                                              bsums);
+            else if (srv && host_in)
                 rc = session ? sbe_serve_encode_session_host(srv, &in, m, ts_default, flags, term, sess, out, cap, off, st)
                              : sbe_serve_encode_topic_host(srv, &in, m, ts_default, flags, out, cap, off, st);
             else if (srv)
@@ -1582,16 +1637,19 @@ EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOf
     }
     EncodePlan plan;
     plan.overhead = SBE_LITE_OVERHEAD(2);
+    plan.layout = SBE_LAYOUT_LITE;
     return run_encode(
         offsets.size(), 2,
         [&](size_t i, int k) { return std::string_view(k == 0 ? offsets[i].message_id : offsets[i].message_identifier); },
         [&](size_t i) { return offsets[i].sequence_number; }, [&](size_t i) { return ids[i]; }, plan,
         [&](sbe_server* srv, bool host_in, const uint8_t* arena, const uint32_t* len, const uint64_t* seq,
             const uint32_t* tid, size_t m, uint8_t* out, uint64_t cap, uint64_t* off, uint8_t* st, void* ws, size_t wsb,
-            hipStream_t s) {
+            hipStream_t s, const uint64_t* tsums, const uint64_t* bsums) {
             sbe_lite_batch in{arena, nullptr, len, tid, seq};
             const int rc =
-                srv && host_in ? sbe_serve_encode_lite_host(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
+                srv && tsums ? sbe_serve_encode_lite_planned(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap,
+                                                             off, st, tsums, bsums)
+                : srv && host_in ? sbe_serve_encode_lite_host(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
                 : srv          ? sbe_serve_encode_lite(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
                                : sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
                                                        wsb, s);

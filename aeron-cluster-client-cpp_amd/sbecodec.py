@@ -184,6 +184,16 @@ def _load():
     lib.sbe_serve_decode_host.restype = ctypes.c_int
     lib.sbe_serve_decode_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                           ctypes.c_uint32, ctypes.POINTER(_Decoded)]
+    lib.sbe_server_create_wide.restype = ctypes.c_int
+    lib.sbe_server_create_wide.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32]
+    lib.sbe_encode_tile_records.restype = ctypes.c_uint32
+    lib.sbe_encode_tile_records.argtypes = [ctypes.c_uint32]
+    for name, base in (("sbe_serve_encode_topic_planned", lib.sbe_serve_encode_topic.argtypes),
+                       ("sbe_serve_encode_session_planned", lib.sbe_serve_encode_session.argtypes),
+                       ("sbe_serve_encode_lite_planned", lib.sbe_serve_encode_lite.argtypes)):
+        f = getattr(lib, name)
+        f.restype = ctypes.c_int
+        f.argtypes = list(base) + [ctypes.c_void_p, ctypes.c_void_p]
     lib.sbe_serve_decode.restype = ctypes.c_int
     lib.sbe_serve_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_uint32, ctypes.POINTER(_Decoded)]
@@ -630,6 +640,8 @@ def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, ds
 
 
 SERVE_MAX_RECORDS = 4096
+SERVE_MAX_WORKGROUPS = 64
+LAYOUT_TOPIC, LAYOUT_SESSION, LAYOUT_LITE = 0, 1, 2
 
 
 class Server:
@@ -639,11 +651,12 @@ class Server:
     inputs.  Inputs must be complete when a method is called (it synchronises torch's current
     stream first); encodes take packed input (no str_off); n <= SERVE_MAX_RECORDS."""
 
-    def __init__(self, idle_us: int = 0):
+    def __init__(self, idle_us: int = 0, workgroups: int = 1):
         require_device()
         h = ctypes.c_void_p()
-        _check(lib().sbe_server_create(ctypes.byref(h), int(idle_us)), "sbe_server_create")
+        _check(lib().sbe_server_create_wide(ctypes.byref(h), int(idle_us), int(workgroups)), "sbe_server_create_wide")
         self._h = h
+        self.workgroups = int(workgroups)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -796,6 +809,64 @@ class Server:
         out = Decoded(*(getattr(out, k)[:n] for k in keys))
         out.seq = None if seq is None else seq[:n]
         return out
+
+    # planned encodes (several workgroups): the tile sums from host-side record sizes
+    @staticmethod
+    def tile_sums(layout, out_bytes, in_bytes, dev="cuda"):
+        """sbe_enc_sums' output for records of the given output / input sizes (numpy u64 [n]):
+        (tile_sums [T,2], sb_sums [S,2]) as int64 device tensors."""
+        import numpy as np
+        R = int(lib().sbe_encode_tile_records(int(layout)))
+        SB = 128 * R
+        n = int(out_bytes.size)
+        po = np.zeros(n + 1, np.uint64)
+        pi = np.zeros(n + 1, np.uint64)
+        po[1:] = np.cumsum(out_bytes.astype(np.uint64))
+        pi[1:] = np.cumsum(in_bytes.astype(np.uint64))
+        if n == 0:
+            ts = bs = np.zeros((1, 2), np.uint64)
+        else:
+            t0 = np.arange(0, n, R)
+            b0 = (t0 // SB) * SB
+            ts = np.stack([po[t0] - po[b0], pi[t0] - pi[b0]], 1)
+            s0 = np.arange(0, n, SB)
+            s1 = np.minimum(s0 + SB, n)
+            bs = np.stack([po[s1] - po[s0], pi[s1] - pi[s0]], 1)
+        cv = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
+        return cv(ts), cv(bs)
+
+    def encode_planned(self, layout, arena, str_len, timestamp, tile_sums, sb_sums, flags=0, ts_default=0,
+                       session=None, template_id=None, topic_id=None) -> Encoded:
+        """Planned encode on device tensors (packed input) with host-made tile sums (tile_sums())."""
+        arena = _dev(arena, torch.uint8, "arena")
+        str_len = _dev(str_len, torch.int32, "str_len")
+        timestamp = _dev(timestamp, torch.int64, "timestamp")
+        n = int(timestamp.numel())
+        if layout == LAYOUT_LITE:
+            cap = int(lib().sbe_lite_output_bound(n, int(arena.numel()), int(template_id)))
+        else:
+            cap = output_bound(n, int(arena.numel()), flags)
+        out, out_off, status = self._outputs(n, cap, arena.device, None, None, None)
+        torch.cuda.current_stream().synchronize()
+        if layout == LAYOUT_LITE:
+            batch = _LiteBatch(arena.data_ptr(), None, str_len.data_ptr(), _dev(topic_id, torch.int32, "topic_id").data_ptr(),
+                               timestamp.data_ptr())
+            rc = lib().sbe_serve_encode_lite_planned(self._h, ctypes.byref(batch), n, int(template_id), _ptr(out),
+                                                     out.numel(), _ptr(out_off), _ptr(status), _ptr(tile_sums),
+                                                     _ptr(sb_sums))
+        elif layout == LAYOUT_SESSION:
+            batch = _TmBatch(arena.data_ptr(), None, str_len.data_ptr(), timestamp.data_ptr())
+            rc = lib().sbe_serve_encode_session_planned(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1),
+                                                        flags, int(session[0]), int(session[1]), _ptr(out),
+                                                        out.numel(), _ptr(out_off), _ptr(status), _ptr(tile_sums),
+                                                        _ptr(sb_sums))
+        else:
+            batch = _TmBatch(arena.data_ptr(), None, str_len.data_ptr(), timestamp.data_ptr())
+            rc = lib().sbe_serve_encode_topic_planned(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
+                                                      _ptr(out), out.numel(), _ptr(out_off), _ptr(status),
+                                                      _ptr(tile_sums), _ptr(sb_sums))
+        _check(rc, "sbe_serve_encode_*_planned")
+        return Encoded(out, out_off, status[:n])
 
     @staticmethod
     def _outputs(n, cap, dev, out, out_off, status):

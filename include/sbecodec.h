@@ -412,6 +412,12 @@ int sbe_gather_plan(const uint64_t* ranks, int world, int root, uint64_t* byte_b
 typedef struct sbe_server sbe_server;
 /* idle_us: how long the resident kernel waits for a request before it exits (0: 20000). */
 int sbe_server_create(sbe_server** srv, uint32_t idle_us);
+/* A server of `workgroups` resident workgroups (1..SBE_SERVE_MAX_WORKGROUPS): workgroup 0 polls the
+ * slot and republishes a request of several tiles to the others through device memory; a decode
+ * of T tiles (64 records each) then runs on min(T, workgroups) of them, as does a planned encode
+ * (below).  One-tile requests run on workgroup 0 alone, as with sbe_server_create. */
+#define SBE_SERVE_MAX_WORKGROUPS 64u
+int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgroups);
 /* Stops the kernel (a shutdown request, then the stream is synchronised) and frees the server. */
 int sbe_server_destroy(sbe_server* srv);
 int sbe_serve_encode_topic(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
@@ -442,6 +448,27 @@ int sbe_serve_encode_lite_host(sbe_server* srv, const sbe_lite_batch* in, uint64
                                uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
 int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint32_t mode,
                           const sbe_decoded* out);
+/* Planned encodes: device-visible inputs (packed) plus the tile sums sbe_encode_*_batch's first
+ * launch would compute, supplied by a caller that knows every record's sizes (the C++ mirror
+ * does): tile_sums [T][2] = output / input bytes before tile t inside its superblock, sb_sums
+ * [S][2] = output / input bytes of superblock s, with T = ceil(n / R) tiles of R =
+ * sbe_encode_tile_records(layout) records and superblocks of 128 R records; a record's output
+ * bytes are 0 for an E109 record, its input bytes the sum of its string lengths.  The tile loop
+ * of the batch kernel then runs on min(T, workgroups) workgroups.  Outputs are byte-identical. */
+#define SBE_LAYOUT_TOPIC 0u
+#define SBE_LAYOUT_SESSION 1u
+#define SBE_LAYOUT_LITE 2u
+uint32_t sbe_encode_tile_records(uint32_t layout);
+int sbe_serve_encode_topic_planned(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                   uint32_t flags, uint8_t* out, uint64_t out_capacity, uint64_t* out_off,
+                                   uint8_t* status, const uint64_t* tile_sums, const uint64_t* sb_sums);
+int sbe_serve_encode_session_planned(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default,
+                                     uint32_t flags, int64_t leadership_term_id, int64_t cluster_session_id,
+                                     uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                                     const uint64_t* tile_sums, const uint64_t* sb_sums);
+int sbe_serve_encode_lite_planned(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id,
+                                  uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
+                                  const uint64_t* tile_sums, const uint64_t* sb_sums);
 /* Requests this server ran and kernel launches it took (a launch per idle exit). */
 int sbe_server_stats(const sbe_server* srv, uint64_t* requests, uint64_t* launches);
 

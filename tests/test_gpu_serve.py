@@ -278,3 +278,100 @@ def test_serve_host_decode_mixed_and_seq(codec, server):
     with pytest.raises(codec.SbeError):  # past the inline area
         big, boff = T.mixed_records(200, seed=1)
         server.decode_host(big, boff)
+
+
+# ---- several workgroups (sbe_server_create_wide): decode tiles and planned encodes ------------
+def sizes_tm(L, flags=0, session=False):
+    """Output / input bytes per record as sbe_enc_sums counts them (E109: no output)."""
+    L = np.asarray(L, np.uint64).reshape(-1, 5)
+    if flags & T.ENC_PUBLISH_TOPIC:
+        out = (L & np.uint64(0xFFFF)).sum(1) + np.uint64(34)
+    else:
+        ovh = 26 if flags & T.ENC_REF_TRUNCATE8 else 34
+        out = L.sum(1) + np.uint64(ovh + (32 if session else 0))
+        out[(L > 65534).any(1)] = 0
+    return out.astype(np.uint64), L.sum(1).astype(np.uint64)
+
+
+@pytest.fixture(scope="module")
+def wide(codec):
+    s = codec.Server(workgroups=codec.SERVE_MAX_WORKGROUPS)
+    yield s
+    s.close()
+
+
+@pytest.mark.parametrize("n", [1, 65, 1000, 4096])
+def test_wide_decode_mixed(codec, wide, n):
+    data, off = T.mixed_records(n, seed=0x51 + n)
+    for mode in (T.DEC_PARSE, T.DEC_EGRESS):
+        assert_same_decode(serve_decode(wide, data, off, mode).numpy(), T.oracle_decode(data, off, mode))
+
+
+def test_wide_decode_long_and_host(codec, wide):
+    arena, L, ts = long_records(300, 19)
+    out, off, _ = T.oracle_encode(arena, L, ts)
+    assert_same_decode(serve_decode(wide, out, off, T.DEC_PARSE).numpy(), T.oracle_decode(out, off, T.DEC_PARSE))
+    data, off = T.mixed_records(60, seed=0x52)  # inline inputs, 1 tile: the leader alone
+    assert_same_decode(wide.decode_host(data, off).numpy(), T.oracle_decode(data, off, T.DEC_PARSE))
+
+
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8, T.ENC_PUBLISH_TOPIC])
+@pytest.mark.parametrize("n", [33, 1000, 4096])
+def test_wide_planned_topic(codec, wide, n, flags):
+    arena, L, ts = T.var_orders(n, seed=0x53 + n)
+    ob, ib = sizes_tm(L, flags)
+    tsum, bsum = codec.Server.tile_sums(codec.LAYOUT_TOPIC, ob, ib)
+    got = wide.encode_planned(codec.LAYOUT_TOPIC, *tm_inputs(arena, L, ts), tsum, bsum, flags=flags, ts_default=3)
+    check_same(host(got, n), T.oracle_encode(arena, L, ts, flags=flags, ts_default=3))
+
+
+def test_wide_planned_e109_and_session(codec, wide):
+    arena, L, ts = long_records(500, 23)
+    L[7, 3] = 70000
+    L[300, 1] = 65535
+    arena = np.concatenate([arena, np.full(70000 + 65535, 66, np.uint8)])
+    ob, ib = sizes_tm(L)
+    tsum, bsum = codec.Server.tile_sums(codec.LAYOUT_TOPIC, ob, ib)
+    got = wide.encode_planned(codec.LAYOUT_TOPIC, *tm_inputs(arena, L, ts), tsum, bsum)
+    check_same(host(got, 500), T.oracle_encode(arena, L, ts))
+    arena, L, ts = T.var_orders(2000, seed=0x54)
+    ob, ib = sizes_tm(L, T.ENC_REF_TRUNCATE8, session=True)
+    tsum, bsum = codec.Server.tile_sums(codec.LAYOUT_SESSION, ob, ib)
+    got = wide.encode_planned(codec.LAYOUT_SESSION, *tm_inputs(arena, L, ts), tsum, bsum, flags=T.ENC_REF_TRUNCATE8,
+                              session=(2, 5))
+    check_same(host(got, 2000), T.oracle_encode_session(arena, L, ts, 2, 5, flags=T.ENC_REF_TRUNCATE8))
+
+
+@pytest.mark.parametrize("template_id", [301, 201])
+def test_wide_planned_lite(codec, wide, template_id):
+    n = 3000
+    arena, L, tid, seq = T.lite_records(n, template_id)
+    nf = T.LITE_NF[template_id]
+    Lu = np.asarray(L, np.uint64).reshape(-1, nf)
+    ob = Lu.sum(1) + np.uint64(20 + 2 * nf)
+    ob[(Lu > 65534).any(1)] = 0
+    tsum, bsum = codec.Server.tile_sums(codec.LAYOUT_LITE, ob, Lu.sum(1))
+    got = wide.encode_planned(codec.LAYOUT_LITE, to_dev(arena, torch.uint8), to_dev(L, torch.int32),
+                              to_dev(seq, torch.int64), tsum, bsum, template_id=template_id,
+                              topic_id=to_dev(tid, torch.int32))
+    check_same(host(got, n), T.oracle_encode_lite(template_id, arena, L, tid, seq))
+
+
+def test_wide_alternating_and_relaunch(codec):
+    """One-tile requests (the leader alone, not republished) between wide ones, then idle exits:
+    the followers' view of the sequence numbers and the exit count stay right."""
+    s = codec.Server(idle_us=3000, workgroups=16)
+    try:
+        d1, o1 = T.mixed_records(1, seed=0x61)
+        d2, o2 = T.mixed_records(900, seed=0x62)
+        e1, e2 = T.oracle_decode(d1, o1, T.DEC_PARSE), T.oracle_decode(d2, o2, T.DEC_PARSE)
+        for k in range(12):
+            assert_same_decode(serve_decode(s, d2, o2, T.DEC_PARSE).numpy(), e2)
+            for _ in range(k % 3):
+                assert_same_decode(serve_decode(s, d1, o1, T.DEC_PARSE).numpy(), e1)
+            if k % 4 == 3:
+                time.sleep(0.02)  # past the idle time: all workgroups leave, the next request relaunches
+        req, launches = s.stats()
+        assert launches >= 3
+    finally:
+        s.close()
