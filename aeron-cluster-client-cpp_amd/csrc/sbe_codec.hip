@@ -2336,25 +2336,42 @@ __device__ __forceinline__ uint32_t q_bytes(uint32_t w) {  // 0x80 in each byte 
 // Staged records: every key dword contains 'q' (key[3]), so a 16-byte chunk (one ds_read_b128) without a 'q'
 // byte holds no candidate.  Only flagged chunks run the exact per-dword test.  Per lane: tiles of
 // records up to kSeqLaneRec bytes, and the fallback of window_exact (two hits in one lane).
+// SBE_SEQ_LANE_K: chunk reads in flight per step.  4, 6 and 8 measured no faster (config 3 decode
+// 60.1 -> 61.1 / 63.2 / 72.0 us, profiles/r04_ab_seqlane_k.log): the other waves already hide the
+// LDS latency; the scan costs instructions, not waits.
+#ifndef SBE_SEQ_LANE_K
+#define SBE_SEQ_LANE_K 2
+#endif
 __device__ uint32_t has_seq_key_lane(const LdsRec& R, uint32_t p, uint32_t n) {
     if (n < 16) return 0u;
+    constexpr uint32_t K = SBE_SEQ_LANE_K;  // chunks whose LDS reads are in flight together
     const uint32_t a0 = R.base + p, a1 = a0 + n;  // window byte range
     const uint32_t c1 = (a1 + 15) >> 4;
     uint32_t fl = 0;
-    for (uint32_t c = a0 >> 4; c < c1; c += 2) {
-        const uint4 v0 = lds_read_chunk_raw(R.win, c);
-        const uint4 v1 = c + 1 < c1 ? lds_read_chunk_raw(R.win, c + 1) : make_uint4(0, 0, 0, 0);
+    for (uint32_t c = a0 >> 4; c < c1; c += K) {
+        // a group's reads past the payload's last chunk re-read that chunk (clamped address, no
+        // branch between the reads): a duplicate can only repeat a suspect, never hide one
+        uint4 v[K];
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) v[k] = lds_read_chunk_raw(R.win, min(c + k, c1 - 1));
         // any-tests (exact as "some byte matches": borrow noise only sits above a real match); the
-        // exact per-dword tests below run only for a chunk pair that holds a 'q' forming a key slice,
-        // or a backslash anywhere in its 32 bytes (the range test there decides whether it is inside
+        // exact per-dword tests below run only for a group that holds a 'q' forming a key slice,
+        // or a backslash anywhere in its bytes (the range test there decides whether it is inside
         // the payload)
-        const uint32_t t = (q_bytes(v0.x) | q_bytes(v0.y) | q_bytes(v0.z) | q_bytes(v0.w) | q_bytes(v1.x) |
-                            q_bytes(v1.y) | q_bytes(v1.z) | q_bytes(v1.w)) & 0x80808080u;
-        const uint32_t b = (bs_any(v0.x) | bs_any(v0.y) | bs_any(v0.z) | bs_any(v0.w) | bs_any(v1.x) | bs_any(v1.y) |
-                            bs_any(v1.z) | bs_any(v1.w)) & 0x80808080u;
-        if ((t && (has_slice(v0) || has_slice(v1))) || b) {
+        uint32_t t = 0, b = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            t |= q_bytes(v[k].x) | q_bytes(v[k].y) | q_bytes(v[k].z) | q_bytes(v[k].w);
+            b |= bs_any(v[k].x) | bs_any(v[k].y) | bs_any(v[k].z) | bs_any(v[k].w);
+        }
+        bool sus = (b & 0x80808080u) != 0u;
+        if (t & 0x80808080u) {
+#pragma unroll
+            for (uint32_t k = 0; k < K; ++k) sus |= has_slice(v[k]);
+        }
+        if (sus) {
 #pragma nounroll
-            for (uint32_t k = 0; k < 8; ++k) {
+            for (uint32_t k = 0; k < 4 * K; ++k) {
                 const uint32_t A = 16 * c + 4 * k;  // window offset of an aligned dword
                 if (A + 4 <= a0 || A >= a1) continue;
                 const uint32_t w = lds_dw(R.win, A >> 2);
