@@ -454,7 +454,10 @@ int sbe_serve_decode_host(sbe_server* srv, const uint8_t* in, const uint64_t* re
  * [S][2] = output / input bytes of superblock s, with T = ceil(n / R) tiles of R =
  * sbe_encode_tile_records(layout) records and superblocks of 128 R records; a record's output
  * bytes are 0 for an E109 record, its input bytes the sum of its string lengths.  The tile loop
- * of the batch kernel then runs on min(T, workgroups) workgroups.  Outputs are byte-identical. */
+ * of the batch kernel then runs on min(T, workgroups) workgroups.  Outputs are byte-identical.
+ * The sums are trusted as the lengths are: output stores stay inside out_capacity whatever they
+ * say, but input reads follow them, so sums that do not match the lengths read past the arena
+ * (undefined, as lengths that overrun the arena are for every encode entry point). */
 #define SBE_LAYOUT_TOPIC 0u
 #define SBE_LAYOUT_SESSION 1u
 #define SBE_LAYOUT_LITE 2u
