@@ -3858,6 +3858,7 @@ struct sbe_server {
     uint32_t nwg = 1;        // workgroups per launch
     uint64_t idle_ticks = 0;
     uint64_t requests = 0, launches = 0;
+    bool failed = false;     // a request timed out or the stream failed: the slot may still hold it
 };
 
 namespace {
@@ -3879,6 +3880,11 @@ int serve_launch(sbe_server* s) {
 // Post one request and wait for its completion (relaunching the kernel whenever it is not running).
 int serve_call(sbe_server* s, const ServeReq& r) {
     if (!s || !s->h) return SBE_EINVAL;
+    if (s->failed) {
+        // a request this server gave up on may still run: no new one is posted over it
+        std::snprintf(g_last_error, sizeof g_last_error, "serve: an earlier request failed; destroy this server");
+        return SBE_EHIP;
+    }
     ServeSlot* h = s->h;
     std::memcpy(&h->req, &r, sizeof r);
     if (h->req.nwg == 0) h->req.nwg = 1;
@@ -3896,8 +3902,12 @@ int serve_call(sbe_server* s, const ServeReq& r) {
         }
         if ((spin & 4095) == 4095) {
             const hipError_t e = hipStreamQuery(s->stream);
-            if (e != hipSuccess && e != hipErrorNotReady) return record_hip(e);
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                s->failed = true;
+                return record_hip(e);
+            }
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                s->failed = true;
                 std::snprintf(g_last_error, sizeof g_last_error, "serve request %u timed out", seq);
                 return SBE_EHIP;
             }
@@ -4159,7 +4169,7 @@ int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgrou
 int sbe_server_destroy(sbe_server* s) {
     if (!s) return SBE_OK;
     int rc = SBE_OK;
-    if (s->h && s->stream && __atomic_load_n(&s->h->alive, __ATOMIC_ACQUIRE)) {
+    if (s->h && s->stream && !s->failed && __atomic_load_n(&s->h->alive, __ATOMIC_ACQUIRE)) {
         ServeReq r{};
         r.op = kSvShutdown;
         r.nwg = s->nwg;  // every workgroup sees it

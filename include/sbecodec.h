@@ -418,7 +418,10 @@ int sbe_server_create(sbe_server** srv, uint32_t idle_us);
  * (below).  One-tile requests run on workgroup 0 alone, as with sbe_server_create. */
 #define SBE_SERVE_MAX_WORKGROUPS 64u
 int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgroups);
-/* Stops the kernel (a shutdown request, then the stream is synchronised) and frees the server. */
+/* Stops the kernel (a shutdown request, then the stream is synchronised) and frees the server.
+ * A request that times out (10 s) or finds the server's stream failed returns SBE_EHIP and leaves
+ * the server failed: every later request returns SBE_EHIP at once, and destroy only waits for the
+ * kernel to leave (it exits idle_us after its last request) before freeing. */
 int sbe_server_destroy(sbe_server* srv);
 int sbe_serve_encode_topic(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
                            uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);
