@@ -28,6 +28,7 @@
 #include <thread>
 
 #include "sbecodec.h"
+#include "workers.hpp"
 
 namespace aeron_cluster {
 
@@ -44,91 +45,7 @@ void hip_check(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("sbecodec: ") + what + ": " + hipGetErrorString(e));
 }
 
-// A fixed set of worker threads (AERON_AMD_HOST_THREADS, default min(16, cores)) that run the
-// tasks of one parallel_for at a time; the calling thread takes tasks too.  A second caller
-// arriving while a loop runs executes its own loop inline (the mirror's entry points are
-// reentrant across threads, like the reference's static codec functions).
-class Workers {
-public:
-    static Workers& get() {
-        static Workers* w = new Workers();  // never destroyed: the threads outlive static teardown
-        return *w;
-    }
-    unsigned size() const { return (unsigned)threads_.size() + 1; }
-
-    template <class F>
-    void parallel_for(size_t ntasks, F&& fn) {
-        if (ntasks == 0) return;
-        std::unique_lock<std::mutex> call(call_m_, std::try_to_lock);
-        if (ntasks == 1 || threads_.empty() || !call.owns_lock()) {
-            for (size_t t = 0; t < ntasks; ++t) fn(t);
-            return;
-        }
-        std::function<void(size_t)> job(std::forward<F>(fn));
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &job;
-            ntasks_ = ntasks;
-            next_.store(0);
-            busy_ = (unsigned)threads_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        run_tasks(job, ntasks);
-        std::unique_lock<std::mutex> g(m_);
-        done_cv_.wait(g, [&] { return busy_ == 0; });
-        job_ = nullptr;
-        if (err_) {
-            std::exception_ptr e = err_;
-            err_ = nullptr;
-            std::rethrow_exception(e);
-        }
-    }
-
-private:
-    Workers() {
-        unsigned n = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-        if (const char* e = std::getenv("AERON_AMD_HOST_THREADS")) n = (unsigned)std::max(1, std::atoi(e));
-        for (unsigned i = 1; i < n; ++i) threads_.emplace_back([this] { loop(); });
-        for (auto& t : threads_) t.detach();
-    }
-    void run_tasks(const std::function<void(size_t)>& job, size_t ntasks) {
-        for (size_t t; (t = next_.fetch_add(1)) < ntasks;) {
-            try {
-                job(t);
-            } catch (...) {
-                std::lock_guard<std::mutex> g(m_);
-                if (!err_) err_ = std::current_exception();
-            }
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(size_t)>* job;
-            size_t ntasks;
-            {
-                std::unique_lock<std::mutex> g(m_);
-                cv_.wait(g, [&] { return gen_ != seen; });
-                seen = gen_;
-                job = job_;
-                ntasks = ntasks_;
-            }
-            run_tasks(*job, ntasks);
-            std::lock_guard<std::mutex> g(m_);
-            if (--busy_ == 0) done_cv_.notify_one();
-        }
-    }
-    std::vector<std::thread> threads_;
-    std::mutex call_m_, m_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(size_t)>* job_ = nullptr;
-    size_t ntasks_ = 0;
-    std::atomic<size_t> next_{0};
-    unsigned busy_ = 0;
-    uint64_t gen_ = 0;
-    std::exception_ptr err_;
-};
+using detail::Workers;  // the worker pool (workers.hpp)
 
 // parallel_for over [0, n) in contiguous ranges of at least `grain` items: fn(lo, hi).
 template <class F>
@@ -801,7 +718,7 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
         for (size_t i = x; i < y; ++i) ro[i] = rec_off[i] - base;
     });
     if (!direct && bytes)
-        for_ranges((size_t)bytes, size_t(1) << 18, [&](size_t x, size_t y) { copy_small(pin + o_data + x, data + lo + x, y - x); });
+        for_ranges((size_t)bytes, size_t(1) << 16, [&](size_t x, size_t y) { copy_small(pin + o_data + x, data + lo + x, y - x); });
     sbe_decoded out{dblk,
                     dblk + d.o_fl,
                     reinterpret_cast<uint16_t*>(dblk + d.o_hdr),
@@ -976,7 +893,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         uint32_t* lp = reinterpret_cast<uint32_t*>(p + s.o_len);
         uint64_t* up = reinterpret_cast<uint64_t*>(p + s.o_u64);
         uint32_t* wp = reinterpret_cast<uint32_t*>(p + s.o_u32);
-        for_ranges(m, 2048, [&](size_t x, size_t y) {
+        for_ranges(m, 256, [&](size_t x, size_t y) {
             for (size_t r = x; r < y; ++r) {
                 const size_t i = a + r;
                 uint8_t* at = p + (pin[i] - in_lo);
@@ -1866,7 +1783,7 @@ void MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* r
     if (n == 0) return;
     // each chunk's ParseResults are built while the next chunk is on the device
     const ChunkFn fill = [&](const Descriptors& d, size_t a, size_t m) {
-        for_ranges(m, 1024, [&](size_t x, size_t y) {
+        for_ranges(m, 256, [&](size_t x, size_t y) {
             for (size_t i = a + x; i < a + y; ++i) materialize_into(out[i], data + rec_off[i], d, i);
         });
     };
