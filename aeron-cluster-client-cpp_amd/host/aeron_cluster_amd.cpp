@@ -893,7 +893,7 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         uint32_t* lp = reinterpret_cast<uint32_t*>(p + s.o_len);
         uint64_t* up = reinterpret_cast<uint64_t*>(p + s.o_u64);
         uint32_t* wp = reinterpret_cast<uint32_t*>(p + s.o_u32);
-        for_ranges(m, 256, [&](size_t x, size_t y) {
+        for_ranges(m, 1024, [&](size_t x, size_t y) {  // 256: 1 K-record encodes 5-9 us slower (wakes)
             for (size_t r = x; r < y; ++r) {
                 const size_t i = a + r;
                 uint8_t* at = p + (pin[i] - in_lo);

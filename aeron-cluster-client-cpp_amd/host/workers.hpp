@@ -6,10 +6,12 @@
 // runs executes its own loop inline (the mirror's entry points are reentrant across threads, like
 // the reference's static codec functions).
 //
-// Small loops are cheap: a loop of T tasks lets at most T - 1 workers join (the others are not
-// woken), and a worker that finished a loop watches for the next one for AERON_AMD_SPIN_US
-// (default 50 us) before it sleeps, so the back-to-back calls of a caller's batch loop find their
-// helpers awake instead of waking them through the kernel one by one.
+// Small loops are cheaper: a loop of T tasks wakes at most T - 1 workers (the others sleep on), and
+// the caller waits for the tasks it did not run by watching a counter.  A worker that finished a
+// loop can watch for the next one for AERON_AMD_SPIN_US microseconds before it sleeps (default 0:
+// on a GPU box whose process gets 16 cores, 15 spinning helpers took the cores the HIP runtime's
+// own threads needed, and 1 K-record calls got slower, profiles/r04_host_latency_pool.log against
+// r04_host_latency_pool_nospin.log).
 #pragma once
 
 #include <algorithm>
@@ -49,7 +51,7 @@ public:
     // a pool of `n` threads in all (n - 1 workers and the caller); tests make their own
     explicit Workers(unsigned n, int spin_us = -1) {
         if (spin_us < 0) {
-            spin_us = 50;
+            spin_us = 0;
             if (const char* e = std::getenv("AERON_AMD_SPIN_US")) spin_us = std::max(0, std::atoi(e));
         }
         spin_ = std::chrono::microseconds(spin_us);
