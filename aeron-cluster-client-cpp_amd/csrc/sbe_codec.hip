@@ -3381,6 +3381,10 @@ __device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
 // wave copy of src[0, len) to dst with 16-byte stores once dst is aligned; each output chunk
 // joins the two aligned 16-byte source blocks it spans (never past the source's last block);
 // four chunks per lane per step, all eight loads issued before the first join
+#ifndef SBE_FC_U  // A/B builds: chunks per lane per copy step
+#define SBE_FC_U 4
+#endif
+constexpr int kFcU = SBE_FC_U;
 __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
     if (len == 0) return;
     uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
@@ -3391,17 +3395,17 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
     const uint32_t sh = (uint32_t)(p0 & 15u);
     const uintptr_t q0 = p0 & ~(uintptr_t)15;
     uint4* d16 = reinterpret_cast<uint4*>(dst + head);
-    for (uint64_t c0 = 0; c0 < nc; c0 += 4 * kWave) {
-        uint4 x[4], y[4];
+    for (uint64_t c0 = 0; c0 < nc; c0 += kFcU * kWave) {
+        uint4 x[kFcU], y[kFcU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kFcU; ++u) {
             const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
             const uintptr_t q = q0 + 16 * (c < nc ? c : nc - 1);
             x[u] = gload128(q);
             y[u] = gload128(q + (sh ? 16 : 0));
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kFcU; ++u) {
             const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
             if (c < nc) d16[c] = sh ? join16(x[u], y[u], sh) : x[u];
         }
@@ -4410,7 +4414,10 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     e = hipGetLastError();
     if (e != hipSuccess) return record_hip(e);
     const uint64_t cb = (n + 1 + 4 * kFragGroup - 1) / (4 * kFragGroup);  // four waves per block
-    hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < 4096 ? cb : 4096)), dim3(256), 0, s, a);
+#ifndef SBE_FC_MAXB  // A/B builds: the copy's grid cap (blocks of four waves; they loop over the groups)
+#define SBE_FC_MAXB 4096
+#endif
+    hipLaunchKernelGGL(frag_copy, dim3((uint32_t)(cb < SBE_FC_MAXB ? cb : SBE_FC_MAXB)), dim3(256), 0, s, a);
     return record_hip(hipGetLastError());
 }
 
