@@ -3043,8 +3043,11 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
 #endif
 }
 
+#ifndef SBE_DEC_MINW_WIDE  // A/B builds: waves per SIMD the kWinWide kernel is compiled for
+#define SBE_DEC_MINW_WIDE SBE_DEC_MINW
+#endif
 template <uint32_t kMode, uint32_t kWin>
-__global__ __launch_bounds__(kWave, SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
+__global__ __launch_bounds__(kWave, kWin == kWinWide ? SBE_DEC_MINW_WIDE : SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
     __shared__ uint32_t win[kWin / 4];
     dec_tile<kMode, kWin>(a, blockIdx.x, win);
 }
