@@ -68,7 +68,10 @@ constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWin
 #ifndef SBE_DEC_MID_AVG
 #define SBE_DEC_MID_AVG 204
 #endif
-constexpr uint32_t kWinMid = 14336, kWinSmall = 8192;
+#ifndef SBE_DEC_WIN_MID  // A/B builds only
+#define SBE_DEC_WIN_MID 14336
+#endif
+constexpr uint32_t kWinMid = SBE_DEC_WIN_MID, kWinSmall = 8192;
 constexpr uint64_t kMidAvg = SBE_DEC_MID_AVG, kSmallAvg = SBE_DEC_SMALL_AVG;
 
 // ------------------------------------------------------------------------------------------
@@ -2775,7 +2778,10 @@ __device__ void dec_lite(const R_t& R, uint32_t len, Desc& d) {
 }
 
 template <uint32_t kW>
-constexpr int dec_regs() { return (int)(kW / 16 / kWave); }  // uint4 staging registers per lane (one window)
+constexpr int dec_regs() {  // uint4 staging registers per lane (one window)
+    static_assert(kW % (16 * kWave) == 0, "decode windows are whole 1 KiB staging rows");
+    return (int)(kW / 16 / kWave);
+}
 
 
 template <uint32_t kMode, typename R_t>
