@@ -4152,7 +4152,7 @@ int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgrou
     sbe_server* s = new (std::nothrow) sbe_server;
     if (!s) return SBE_EINVAL;
     s->nwg = workgroups;
-    s->idle_ticks = 100ull * (idle_us ? idle_us : 20000u);
+    s->idle_ticks = 100ull * (idle_us ? idle_us : 1000u);
     void* h = nullptr;
     void* d = nullptr;
     hipError_t e = hipHostMalloc(&h, sizeof(ServeSlot), hipHostMallocCoherent | hipHostMallocMapped);
@@ -4177,6 +4177,25 @@ int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgrou
     }
     *srv = s;
     return SBE_OK;
+}
+
+int sbe_server_quiesce(sbe_server* s) {
+    if (!s) return SBE_EINVAL;
+    if (s->failed) {
+        std::snprintf(g_last_error, sizeof g_last_error, "serve: an earlier request failed; destroy this server");
+        return SBE_EHIP;
+    }
+    if (!s->h || !s->stream || !__atomic_load_n(&s->h->alive, __ATOMIC_ACQUIRE)) return SBE_OK;
+    ServeReq r{};
+    r.op = kSvShutdown;
+    r.nwg = s->nwg;  // every workgroup sees it
+    int rc = serve_call(s, r);
+    const hipError_t e = hipStreamSynchronize(s->stream);  // the kernel has left
+    if (rc == SBE_OK && e != hipSuccess) {
+        s->failed = true;
+        rc = record_hip(e);
+    }
+    return rc;
 }
 
 int sbe_server_destroy(sbe_server* s) {
@@ -4555,6 +4574,7 @@ struct sbe_comm {
     uint64_t* d_mine = nullptr;   // {bytes, n, root byte capacity, root offset capacity} (device, 32 B)
     uint64_t* d_all = nullptr;    // the same of every rank (device, 32 B per rank)
     uint64_t* h_all = nullptr;    // pinned host copy of d_all
+    uint64_t* plan = nullptr;       // host [world][4]: {bytes, records, root capacity, root offset capacity}
     uint64_t* byte_base = nullptr;  // host [world + 1]: the gather plan
     uint64_t* rec_base = nullptr;
 };
@@ -4616,6 +4636,7 @@ int sbe_comm_init(sbe_comm** comm, int world, int rank, const uint8_t id[SBE_COM
     sbe_comm* c = new sbe_comm;
     c->world = world;
     c->rank = rank;
+    c->plan = new uint64_t[4 * (size_t)world];
     c->byte_base = new uint64_t[world + 1];
     c->rec_base = new uint64_t[world + 1];
     rc = record_hip(hipMalloc(reinterpret_cast<void**>(&c->d_mine), 32));
@@ -4641,10 +4662,55 @@ int sbe_comm_destroy(sbe_comm* c) {
     if (c->d_mine) (void)hipFree(c->d_mine);
     if (c->d_all) (void)hipFree(c->d_all);
     if (c->h_all) (void)hipHostFree(c->h_all);
+    delete[] c->plan;
     delete[] c->byte_base;
     delete[] c->rec_base;
     delete c;
     return rc;
+}
+
+// Steps 2-3 of both gathers: from the plan in c->plan ({bytes, records, ...} per rank, 4 words a
+// rank) and c->byte_base / c->rec_base, one group of sends / receives, then the root's own shard,
+// the rebase and the closing offset.  Everything is enqueued on s; nothing waits on the host.
+static int gather_transfer(sbe_comm* c, int root, const uint8_t* out, const uint64_t* out_off, uint8_t* dst,
+                           uint64_t* dst_off, const uint64_t tot[2], hipStream_t s) {
+    const RcclApi& R = rccl_api();
+    const bool am_root = c->rank == root;
+    const uint64_t* plan = c->plan;
+    int rc = record_nccl(R.GroupStart(), "ncclGroupStart");
+    if (rc != SBE_OK) return rc;
+    for (int r = 0; r < c->world && rc == SBE_OK; ++r) {
+        const uint64_t b = plan[4 * r], m = plan[4 * r + 1];
+        if (r == c->rank && !am_root) {
+            if (b) rc = record_nccl(R.Send(out, b, ncclUint8, root, c->nc, s), "ncclSend");
+            if (m && rc == SBE_OK) rc = record_nccl(R.Send(out_off, m, ncclUint64, root, c->nc, s), "ncclSend");
+        } else if (am_root && r != root) {
+            if (b) rc = record_nccl(R.Recv(dst + c->byte_base[r], b, ncclUint8, r, c->nc, s), "ncclRecv");
+            if (m && rc == SBE_OK)
+                rc = record_nccl(R.Recv(dst_off + c->rec_base[r], m, ncclUint64, r, c->nc, s), "ncclRecv");
+        }
+    }
+    const int rc_end = record_nccl(R.GroupEnd(), "ncclGroupEnd");
+    if (rc != SBE_OK) return rc;
+    if (rc_end != SBE_OK) return rc_end;
+    if (!am_root) return SBE_OK;
+    // root: its own shard, the offset rebase, the closing offset
+    for (int r = 0; r < c->world; ++r) {
+        const uint64_t b = plan[4 * r], m = plan[4 * r + 1];
+        if (r == root && b)
+            rc = record_hip(hipMemcpyAsync(dst + c->byte_base[r], out, b, hipMemcpyDeviceToDevice, s));
+        if (rc != SBE_OK) return rc;
+        if (m) {
+            const uint64_t blocks = (m + 255) / 256;
+            uint64_t* d = dst_off + c->rec_base[r];
+            hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d,
+                               r == root ? out_off : d, m, c->byte_base[r]);
+            rc = record_hip(hipGetLastError());
+            if (rc != SBE_OK) return rc;
+        }
+    }
+    hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + tot[1], tot[0]);
+    return record_hip(hipGetLastError());
 }
 
 int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t* out_off, uint64_t n,
@@ -4665,48 +4731,39 @@ int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t
     rc = record_hip(hipMemcpyAsync(c->h_all, c->d_all, 32 * (size_t)c->world, hipMemcpyDeviceToHost, s));
     if (rc == SBE_OK) rc = record_hip(hipStreamSynchronize(s));
     if (rc != SBE_OK) return rc;
+    std::memcpy(c->plan, c->h_all, 32 * (size_t)c->world);
     uint64_t tot[2];
-    rc = sbe_gather_plan(c->h_all, c->world, root, c->byte_base, c->rec_base, tot);
+    rc = sbe_gather_plan(c->plan, c->world, root, c->byte_base, c->rec_base, tot);
     if (totals) {
         totals[0] = tot[0];
         totals[1] = tot[1];
     }
     if (rc != SBE_OK) return rc;
-    // 2. the shards and their offsets, in one group
-    rc = record_nccl(R.GroupStart(), "ncclGroupStart");
-    if (rc != SBE_OK) return rc;
-    for (int r = 0; r < c->world && rc == SBE_OK; ++r) {
-        const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
-        if (r == c->rank && !am_root) {
-            if (b) rc = record_nccl(R.Send(out, b, ncclUint8, root, c->nc, s), "ncclSend");
-            if (m && rc == SBE_OK) rc = record_nccl(R.Send(out_off, m, ncclUint64, root, c->nc, s), "ncclSend");
-        } else if (am_root && r != root) {
-            if (b) rc = record_nccl(R.Recv(dst + c->byte_base[r], b, ncclUint8, r, c->nc, s), "ncclRecv");
-            if (m && rc == SBE_OK)
-                rc = record_nccl(R.Recv(dst_off + c->rec_base[r], m, ncclUint64, r, c->nc, s), "ncclRecv");
-        }
-    }
-    const int rc_end = record_nccl(R.GroupEnd(), "ncclGroupEnd");
-    if (rc != SBE_OK) return rc;
-    if (rc_end != SBE_OK) return rc_end;
-    if (!am_root) return SBE_OK;
-    // 3. root: its own shard, the offset rebase, the closing offset
+    // 2. the shards and their offsets, in one group; 3. the root's rebase
+    return gather_transfer(c, root, out, out_off, dst, dst_off, tot, s);
+}
+
+int sbe_gather_encoded_sized(sbe_comm* c, int root, const uint64_t* sizes, const uint8_t* out,
+                             const uint64_t* out_off, uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off,
+                             uint64_t dst_off_capacity, uint64_t* totals, void* stream) {
+    if (!c || !sizes || !out_off || root < 0 || root >= c->world) return SBE_EINVAL;
+    const bool am_root = c->rank == root;
+    if (am_root && !dst_off) return SBE_EINVAL;
+    // the plan from the caller's sizes, with the root's capacities every rank was given
     for (int r = 0; r < c->world; ++r) {
-        const uint64_t b = c->h_all[4 * r], m = c->h_all[4 * r + 1];
-        if (r == root && b)
-            rc = record_hip(hipMemcpyAsync(dst + c->byte_base[r], out, b, hipMemcpyDeviceToDevice, s));
-        if (rc != SBE_OK) return rc;
-        if (m) {
-            const uint64_t blocks = (m + 255) / 256;
-            uint64_t* d = dst_off + c->rec_base[r];
-            hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, d,
-                               r == root ? out_off : d, m, c->byte_base[r]);
-            rc = record_hip(hipGetLastError());
-            if (rc != SBE_OK) return rc;
-        }
+        c->plan[4 * r] = sizes[2 * r];
+        c->plan[4 * r + 1] = sizes[2 * r + 1];
+        c->plan[4 * r + 2] = r == root ? dst_capacity : 0;
+        c->plan[4 * r + 3] = r == root ? dst_off_capacity : 0;
     }
-    hipLaunchKernelGGL(u64_put, dim3(1), dim3(64), 0, s, dst_off + tot[1], tot[0]);
-    return record_hip(hipGetLastError());
+    uint64_t tot[2];
+    const int rc = sbe_gather_plan(c->plan, c->world, root, c->byte_base, c->rec_base, tot);
+    if (totals) {
+        totals[0] = tot[0];
+        totals[1] = tot[1];
+    }
+    if (rc != SBE_OK) return rc;
+    return gather_transfer(c, root, out, out_off, dst, dst_off, tot, reinterpret_cast<hipStream_t>(stream));
 }
 
 #ifdef SBE_PACK_PHASES

@@ -218,6 +218,12 @@ struct Pipeline {
     // one-chunk calls: copy-in, kernels and copy-out in order on the compute stream, no events
     // (a small batch is latency-bound: each event record / wait costs more than it overlaps)
     bool serial = false;
+    // called before the first copy or kernel of a batch is enqueued (Ctx: stop the resident server)
+    void (*before_enqueue)(void*) = nullptr;
+    void* before_arg = nullptr;
+    void enqueue_hook() {
+        if (before_enqueue) before_enqueue(before_arg);
+    }
 
     void create() {
         for (hipStream_t* st : {&s_in, &s_comp, &s_out})
@@ -256,6 +262,7 @@ struct Pipeline {
     }
     // the slot's staged bytes to d_in, plus (direct) `dbytes` page-locked caller bytes to d_in + doff
     void copy_in(Slot& sl, size_t bytes, const void* direct = nullptr, size_t doff = 0, size_t dbytes = 0) {
+        enqueue_hook();
         hipStream_t st = serial ? s_comp : s_in;
         if (!serial && sl.used) hip_check(hipStreamWaitEvent(s_in, sl.comp_done, 0), "hipStreamWaitEvent");  // d_in read
         hip_check(hipMemcpyAsync(sl.d_in.p, sl.pin.p, bytes, hipMemcpyHostToDevice, st), "H2D");
@@ -264,6 +271,7 @@ struct Pipeline {
     }
     // the stream to launch the chunk's kernels on (after its input copy and the slot's last D2H)
     hipStream_t compute(Slot& sl) {
+        enqueue_hook();
         if (serial) return s_comp;
         hip_check(hipStreamWaitEvent(s_comp, sl.in_done, 0), "hipStreamWaitEvent");
         if (sl.used) hip_check(hipStreamWaitEvent(s_comp, sl.out_done, 0), "hipStreamWaitEvent");
@@ -301,7 +309,7 @@ size_t serve_max_records() {
 // Batches of up to this many records that the single wave does not take go to the server's other
 // workgroups as a whole (decode: tile per workgroup; encode: the tile loop with tile sums from the
 // host's plan) instead of a launch: AERON_AMD_SERVE_WIDE_RECORDS (0: never); the server has
-// AERON_AMD_SERVE_WGS workgroups (default 64).
+// AERON_AMD_SERVE_WGS workgroups (default 32).
 size_t serve_wide_max_records() {
     static const size_t v = [] {
         const char* e = std::getenv("AERON_AMD_SERVE_WIDE_RECORDS");
@@ -313,18 +321,20 @@ size_t serve_wide_max_records() {
 uint32_t serve_workgroups() {
     static const uint32_t v = [] {
         const char* e = std::getenv("AERON_AMD_SERVE_WGS");
-        const long long x = e ? std::atoll(e) : 64;
+        const long long x = e ? std::atoll(e) : 32;
         return (uint32_t)std::min<long long>(std::max(1LL, x), SBE_SERVE_MAX_WORKGROUPS);
     }();
     return v;
 }
 
 // How long an idle serve kernel keeps polling before it exits (AERON_AMD_SERVE_IDLE_US, default
-// 20 ms); the next small call relaunches it.
+// 1 ms); the next small call relaunches it (one launch, ≈ 6-12 µs).  While it is resident, work
+// that HIP maps to the same hardware queue waits behind it (streams share GPU_MAX_HW_QUEUES
+// queues), as does any device-wide synchronisation: short is the safe default.
 uint32_t serve_idle_us() {
     static const uint32_t v = [] {
         const char* e = std::getenv("AERON_AMD_SERVE_IDLE_US");
-        return e ? (uint32_t)std::max(1LL, std::atoll(e)) : 20000u;
+        return e ? (uint32_t)std::max(1LL, std::atoll(e)) : 1000u;
     }();
     return v;
 }
@@ -341,6 +351,13 @@ struct Ctx {
     Ctx() {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");
         pipe.create();
+        pipe.before_enqueue = [](void* self) { static_cast<Ctx*>(self)->quiesce(); };
+        pipe.before_arg = this;
+    }
+    // the compute stream for a launch outside the chunk loop (the resident server stopped first)
+    hipStream_t batch_stream() {
+        quiesce();
+        return pipe.s_comp;
     }
     ~Ctx() {
         if (srv) (void)sbe_server_destroy(srv);
@@ -357,6 +374,21 @@ struct Ctx {
             (void)hipGetLastError();
         }
         return srv;
+    }
+    // A serve request failed (timed out, or the server's stream failed): this thread stops using
+    // the serve kernel (its batches go to the batch kernels from now on) and frees the server.
+    void drop_server() noexcept {
+        if (srv) (void)sbe_server_destroy(srv);
+        srv = nullptr;
+        srv_failed = true;
+        (void)hipGetLastError();
+    }
+    // Before batch work is enqueued on this thread's streams: a resident server of this thread
+    // exits first (a shutdown request, then its stream drains), so that no kernel or copy of the
+    // batch can wait behind it on a shared hardware queue.  Free when the server is not running;
+    // the next small call relaunches it.
+    void quiesce() noexcept {
+        if (srv && sbe_server_quiesce(srv) != SBE_OK) drop_server();
     }
     void sync_all() { pipe.drain(); }
     // After a throw inside a chunk loop: wait for every copy and kernel already queued (their
@@ -700,8 +732,8 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
                             reinterpret_cast<uint32_t*>(dblk + d.o_off),
                             reinterpret_cast<uint32_t*>(dblk + d.o_len),
                             parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
-            if (sbe_serve_decode_host(srv, data, rec_off, n, mode, &out) != SBE_OK) fail("sbe_serve_decode_host");
-            return true;
+            if (sbe_serve_decode_host(srv, data, rec_off, n, mode, &out) == SBE_OK) return true;
+            c.drop_server();  // the batch kernels take this call and every later one
         }
     }
     // the kernel reads its records from a 16-B aligned base: page-locked caller bytes are read from
@@ -727,11 +759,11 @@ bool decode_zero_copy(Ctx& c, const uint8_t* data, const uint64_t* rec_off, size
                     reinterpret_cast<uint32_t*>(dblk + d.o_len),
                     parse ? reinterpret_cast<uint64_t*>(dblk + d.o_seq) : nullptr};
     if (sbe_server* srv = c.server(n, true)) {  // inputs through the staging buffer, several workgroups
-        if (sbe_serve_decode(srv, drec, reinterpret_cast<const uint64_t*>(dpin), n, mode, &out) != SBE_OK)
-            fail("sbe_serve_decode");
-        return true;
+        if (sbe_serve_decode(srv, drec, reinterpret_cast<const uint64_t*>(dpin), n, mode, &out) == SBE_OK) return true;
+        c.drop_server();
     }
-    if (sbe_decode_batch_sized(drec, reinterpret_cast<const uint64_t*>(dpin), n, bytes, mode, &out, P.s_comp) != SBE_OK) {
+    if (sbe_decode_batch_sized(drec, reinterpret_cast<const uint64_t*>(dpin), n, bytes, mode, &out, c.batch_stream()) !=
+        SBE_OK) {
         c.abort_all();
         fail("sbe_decode_batch");
     }
@@ -953,18 +985,33 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
                 }
                 tr.lap(tr.stage);
                 PipeGuard zguard(c);
-                const size_t ws_bytes = srv ? 16 : sbe_encode_workspace_size(n);
-                c.d_ws.need(ws_bytes);
-                // the single-wave serve takes the staged inputs by their host addresses (copied into
-                // its request slot when they fit, else read through their device addresses)
-                const uint8_t* ip = srv && !wsrv && s.bytes <= SBE_SERVE_INLINE_BYTES ? sl.pin.b() : dp;
                 // a batch whose records all fail (E109) has no bytes: the kernels still want a
                 // 16-B aligned output pointer, which they never write at capacity 0
-                launch(srv, ip != dp, ip, reinterpret_cast<const uint32_t*>(ip + s.o_len),
-                       reinterpret_cast<const uint64_t*>(ip + s.o_u64), reinterpret_cast<const uint32_t*>(ip + s.o_u32), n,
-                       dbytes ? dbytes : c.d_ws.b(), pout[n], doff, dst, c.d_ws.b(), ws_bytes, P.s_comp, tsums, bsums);
-                tr.lap(tr.enqueue);
-                if (!srv) hip_check(hipStreamSynchronize(P.s_comp), "hipStreamSynchronize");
+                if (srv) {
+                    c.d_ws.need(16);
+                    // the single-wave serve takes the staged inputs by their host addresses (copied
+                    // into its request slot when they fit, else read through their device addresses)
+                    const uint8_t* ip = !wsrv && s.bytes <= SBE_SERVE_INLINE_BYTES ? sl.pin.b() : dp;
+                    if (launch(srv, ip != dp, ip, reinterpret_cast<const uint32_t*>(ip + s.o_len),
+                               reinterpret_cast<const uint64_t*>(ip + s.o_u64),
+                               reinterpret_cast<const uint32_t*>(ip + s.o_u32), n, dbytes ? dbytes : c.d_ws.b(), pout[n],
+                               doff, dst, c.d_ws.b(), 16, P.s_comp, tsums, bsums) != SBE_OK) {
+                        c.drop_server();  // the batch kernels take this call and every later one
+                        srv = nullptr;
+                    }
+                }
+                if (!srv) {
+                    const size_t ws_bytes = sbe_encode_workspace_size(n);
+                    c.d_ws.need(ws_bytes);
+                    hipStream_t st = c.batch_stream();
+                    if (launch(nullptr, false, dp, reinterpret_cast<const uint32_t*>(dp + s.o_len),
+                               reinterpret_cast<const uint64_t*>(dp + s.o_u64),
+                               reinterpret_cast<const uint32_t*>(dp + s.o_u32), n, dbytes ? dbytes : c.d_ws.b(), pout[n],
+                               doff, dst, c.d_ws.b(), ws_bytes, st, nullptr, nullptr) != SBE_OK)
+                        fail("sbe_encode batch");
+                    tr.lap(tr.enqueue);
+                    hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+                }
                 zguard.release();
                 tr.lap(tr.sync);
                 if (b.offsets[n] != pout[n]) throw std::logic_error("sbecodec: encoded batch size differs from its plan");
@@ -996,10 +1043,11 @@ EncodedBatch run_encode(size_t n, int nf, Field&& field, U64&& u64, U32&& u32, E
         hipStream_t st = P.compute(sl);
         const uint8_t* di = sl.d_in.b();
         uint8_t* dout = sl.d_out.b();
-        launch(nullptr, false, di, reinterpret_cast<const uint32_t*>(di + o_len), reinterpret_cast<const uint64_t*>(di + o_u64),
-               reinterpret_cast<const uint32_t*>(di + o_u32), m, dout, out_bytes,
-               reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes, st, nullptr,
-               nullptr);
+        if (launch(nullptr, false, di, reinterpret_cast<const uint32_t*>(di + o_len),
+                   reinterpret_cast<const uint64_t*>(di + o_u64), reinterpret_cast<const uint32_t*>(di + o_u32), m, dout,
+                   out_bytes, reinterpret_cast<uint64_t*>(dout + d_off), dout + d_off + (m + 1) * 8, dout + d_ws, ws_bytes,
+                   st, nullptr, nullptr) != SBE_OK)
+            fail("sbe_encode batch");
         st = P.copy_out(sl);
         if (out_bytes) hip_check(hipMemcpyAsync(b.bytes.data() + out_lo, dout, out_bytes, hipMemcpyDeviceToHost, st), "D2H");
         hip_check(hipMemcpyAsync(hmeta + k * meta_stride, dout + d_off, (m + 1) * 8 + m, hipMemcpyDeviceToHost, st), "D2H");
@@ -1219,7 +1267,7 @@ EncodedBatch encode_tm(const std::vector<TopicMessageFields>& msgs, EncodeLength
                 rc = session ? sbe_encode_session_batch(&in, m, ts_default, flags, term, sess, out, cap, off, st, ws,
                                                         wsb, s)
                              : sbe_encode_topic_batch(&in, m, ts_default, flags, out, cap, off, st, ws, wsb, s);
-            if (rc != SBE_OK) fail(session ? "sbe_encode_session_batch" : "sbe_encode_topic_batch");
+            return rc;
         });
 }
 
@@ -1373,7 +1421,11 @@ std::string ParseResult::get_description() const {
 // ======================================================================================
 namespace {
 // SBEDecoder::extract_variable_string (:285-318): a u32 length prefix at offset, the string after
-// it; 0 (output untouched) when the prefix or the string does not fit or the length is over 10 MiB
+// it; 0 (output untouched) when the prefix or the string does not fit or the length is over 10 MiB.
+// The reference checks the length against `remaining - 4` whatever the offset (:302), so for a
+// field after the first one a corrupt length can make it read up to `offset` bytes past the
+// record (undefined behaviour on network input).  Here the string must end inside the record:
+// identical results for every record the reference reads in bounds, a refusal for the others.
 size_t extract_variable_string(const uint8_t* data, size_t offset, size_t remaining, std::string& output) {
     if (offset + sizeof(uint32_t) > remaining) {
         debug_log("[ERROR] Not enough data for length prefix at offset ", offset, ", remaining: ", remaining);
@@ -1383,7 +1435,7 @@ size_t extract_variable_string(const uint8_t* data, size_t offset, size_t remain
     std::memcpy(&length, data + offset, sizeof(uint32_t));
     debug_log("[DEBUG] Extracting string at offset ", offset, ", length prefix: ", length, ", remaining: ", remaining);
     offset += sizeof(uint32_t);
-    if (length > remaining - sizeof(uint32_t) || length > 10u * 1024u * 1024u) {
+    if (length > remaining - offset || length > 10u * 1024u * 1024u) {
         debug_log("[ERROR] Invalid string length: ", length, ", remaining data: ", (remaining - sizeof(uint32_t)));
         return 0;
     }
@@ -1462,6 +1514,8 @@ bool SBEDecoder::decode_acknowledgment(const std::uint8_t* data, std::size_t len
 std::int64_t SBEEncoder::get_current_timestamp() {
     return (std::int64_t)std::chrono::high_resolution_clock::now().time_since_epoch().count();
 }
+
+void quiesce() { ctx().quiesce(); }
 
 bool gpu_codec_available() { return sbe_device_ready() == 1; }
 unsigned host_threads() { return Workers::get().size(); }
@@ -1570,7 +1624,7 @@ EncodedBatch CommitManager::build_commit_offset_batch(const std::vector<CommitOf
                 : srv          ? sbe_serve_encode_lite(srv, &in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st)
                                : sbe_encode_lite_batch(&in, m, SBE_COMMIT_OFFSET_LITE_TEMPLATE_ID, out, cap, off, st, ws,
                                                        wsb, s);
-            if (rc != SBE_OK) fail("sbe_encode_lite_batch");
+            return rc;
         });
 }
 
@@ -1614,7 +1668,7 @@ OrderJsonBatch orders_to_json(const std::vector<Order>& orders, const std::vecto
     };
     Ctx& c = ctx();
     Pipeline::Slot& s = c.pipe.slot[0];  // serial use of the pipeline's first slot (idle between calls)
-    hipStream_t stream = c.pipe.s_comp;
+    hipStream_t stream = c.batch_stream();
     std::vector<uint64_t> pin;
     prefix(n, pin, [&](size_t i) {
         uint64_t t = 0;
@@ -1880,7 +1934,7 @@ EncodedBatch FragmentReassembler::on_fragments(const std::uint8_t* data, const s
                                                const std::uint8_t* flags, std::size_t n) {
     Ctx& c = ctx();
     Pipeline::Slot& s = c.pipe.slot[0];  // serial use of the pipeline's first slot (idle between calls)
-    hipStream_t stream = c.pipe.s_comp;
+    hipStream_t stream = c.batch_stream();
     EncodedBatch b;
     // the accumulator so far goes first as a middle fragment (flags 0): it is appended to exactly
     // as the reference's acc_ would be, or cleared by a BEGIN

@@ -476,6 +476,13 @@ bool gpu_codec_available();
 // default min(16, cores)
 unsigned host_threads();
 
+// Stops the calling thread's small-batch serve kernel if it is resident (it exits after
+// AERON_AMD_SERVE_IDLE_US without a call, default 1 ms; the next small call relaunches it).  While
+// resident it holds a hardware queue that other streams of the process may share, and a
+// device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize()) waits for it to go
+// idle: call this before such a synchronisation, or before handing the GPU to other work.
+void quiesce();
+
 // Page-locks a long-lived host buffer (e.g. an Aeron term buffer mapped from /dev/shm) for the
 // device's copy engines: batches decoded from registered (or hipHostMalloc'd) memory are copied to
 // HBM in place, without the staging copy.  The memory stays registered until host_unregister.

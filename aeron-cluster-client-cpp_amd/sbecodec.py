@@ -153,6 +153,11 @@ def _load():
     lib.sbe_gather_encoded.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    lib.sbe_gather_encoded_sized.restype = ctypes.c_int
+    lib.sbe_gather_encoded_sized.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.c_void_p]
     lib.sbe_gather_plan.restype = ctypes.c_int
     lib.sbe_gather_plan.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
@@ -161,6 +166,8 @@ def _load():
     lib.sbe_server_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32]
     lib.sbe_server_destroy.restype = ctypes.c_int
     lib.sbe_server_destroy.argtypes = [ctypes.c_void_p]
+    lib.sbe_server_quiesce.restype = ctypes.c_int
+    lib.sbe_server_quiesce.argtypes = [ctypes.c_void_p]
     lib.sbe_server_stats.restype = ctypes.c_int
     lib.sbe_server_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.sbe_serve_encode_topic.restype = ctypes.c_int
@@ -639,6 +646,38 @@ def gather_encoded(comm: Comm, out, out_off, n: int, root: int = 0, dst=None, ds
     return None, None, nbytes, nrec
 
 
+def gather_encoded_sized(comm: Comm, sizes, out, out_off, root: int = 0, dst=None, dst_off=None,
+                         dst_capacity: int = 0, dst_off_capacity: int = 0, stream=None):
+    """Collective, for callers that know every shard's size: sizes = [(bytes, records)] per rank,
+    identical on every rank.  No size all-gather and no host wait (sbe_gather_encoded_sized): the
+    transfers and the root's rebase are enqueued on `stream`.  Every rank passes the ROOT's
+    capacities (the root's own default to its dst / dst_off sizes); returns as gather_encoded."""
+    world = comm.world
+    if len(sizes) != world:
+        raise SbeError(f"sizes has {len(sizes)} entries for a world of {world}")
+    out = _dev(out, torch.uint8, "out")
+    out_off = _dev(out_off, torch.int64, "out_off")
+    am_root = comm.rank == root
+    if am_root:
+        dst = _dev(dst, torch.uint8, "dst")
+        dst_off = _dev(dst_off, torch.int64, "dst_off")
+        if dst is None or dst_off is None:
+            raise SbeError("the root passes dst and dst_off")
+        dst_capacity = dst_capacity or int(dst.numel())
+        dst_off_capacity = dst_off_capacity or int(dst_off.numel())
+    flat = (ctypes.c_uint64 * (2 * world))(*[int(v) for sz in sizes for v in sz])
+    totals = (ctypes.c_uint64 * 2)()
+    rc = lib().sbe_gather_encoded_sized(comm._h, int(root), flat, _ptr(out), _ptr(out_off),
+                                        _ptr(dst) if am_root else None, int(dst_capacity),
+                                        _ptr(dst_off) if am_root else None, int(dst_off_capacity),
+                                        totals, _stream(stream))
+    _check(rc, "sbe_gather_encoded_sized")
+    nbytes, nrec = int(totals[0]), int(totals[1])
+    if am_root:
+        return dst[:nbytes], dst_off[: nrec + 1], nbytes, nrec
+    return None, None, nbytes, nrec
+
+
 SERVE_MAX_RECORDS = 4096
 SERVE_MAX_WORKGROUPS = 64
 LAYOUT_TOPIC, LAYOUT_SESSION, LAYOUT_LITE = 0, 1, 2
@@ -668,6 +707,12 @@ class Server:
             self.close()
         except Exception:
             pass
+
+    def quiesce(self):
+        """Make the resident kernel exit now (sbe_server_quiesce); the next request relaunches it.
+        A resident server holds up device-wide synchronisation (torch.cuda.synchronize()) and
+        work on streams that share its hardware queue until it goes idle."""
+        _check(lib().sbe_server_quiesce(self._h), "sbe_server_quiesce")
 
     def stats(self):
         """(requests served, kernel launches) so far."""
@@ -762,6 +807,7 @@ class Server:
         n = int(timestamp.size)
         out, out_off, status = self._outputs(n, output_bound(n, int(arena.size), flags), torch.device(dev),
                                              None, None, None)
+        torch.cuda.current_stream().synchronize()  # the fresh outputs may still be in use on torch's stream
         batch = _TmBatch(arena.ctypes.data if arena.size else None, None, str_len.ctypes.data, timestamp.ctypes.data)
         if session is None:
             rc = lib().sbe_serve_encode_topic_host(self._h, ctypes.byref(batch), n, ts_default & (2**64 - 1), flags,
@@ -785,6 +831,7 @@ class Server:
         n = int(sequence.size)
         cap = int(lib().sbe_lite_output_bound(n, int(arena.size), int(template_id)))
         out, out_off, status = self._outputs(n, cap, torch.device(dev), None, None, None)
+        torch.cuda.current_stream().synchronize()  # the fresh outputs may still be in use on torch's stream
         batch = _LiteBatch(arena.ctypes.data if arena.size else None, None, str_len.ctypes.data, topic_id.ctypes.data,
                            sequence.ctypes.data)
         _check(lib().sbe_serve_encode_lite_host(self._h, ctypes.byref(batch), n, int(template_id), _ptr(out),

@@ -384,6 +384,20 @@ int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint6
                        uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off, uint64_t dst_off_capacity,
                        uint64_t* totals, void* stream);
 
+/* The same gather for a caller that already knows every rank's shard size (fixed-size records:
+ * bytes = records x record size; or the host size plan the C++ mirror keeps for every encode):
+ * sizes (host u64 [world][2]) = {bytes, records} of each rank's shard, identical on every rank.
+ * No size all-gather and no host synchronisation: it enqueues the grouped ncclSend / ncclRecv and
+ * the root's rebase on `stream` and returns, so a rank can go on to encode its next shard while
+ * this one travels.  dst_capacity / dst_off_capacity are the ROOT's capacities, passed on every
+ * rank (non-roots pass dst = dst_off = NULL), so every rank reaches the same SBE_ENOSPC verdict
+ * before anything is sent.  The sizes are trusted as a planned encode's tile sums are: they must
+ * equal out_off[n] and n of the shard each rank encoded (a wrong plan moves the wrong bytes; it
+ * never writes past the root's capacities). */
+int sbe_gather_encoded_sized(sbe_comm* comm, int root, const uint64_t* sizes, const uint8_t* out,
+                             const uint64_t* out_off, uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off,
+                             uint64_t dst_off_capacity, uint64_t* totals, void* stream);
+
 /* The gather's plan (host only, no device): from every rank's {bytes, records, dst_capacity,
  * dst_off_capacity} (ranks: host u64 [world][4], the capacities read from the root's entry) the
  * byte and record base of each rank's shard on the root (byte_base / rec_base: host u64
@@ -410,7 +424,8 @@ int sbe_gather_plan(const uint64_t* ranks, int world, int root, uint64_t* byte_b
  * large batches belong on the batch entry points).  A server is used by one host thread at a time. */
 #define SBE_SERVE_MAX_RECORDS 4096u
 typedef struct sbe_server sbe_server;
-/* idle_us: how long the resident kernel waits for a request before it exits (0: 20000). */
+/* idle_us: how long the resident kernel waits for a request before it exits (0: 1000).  Keep it
+ * short: see sbe_server_quiesce on what a resident server holds up. */
 int sbe_server_create(sbe_server** srv, uint32_t idle_us);
 /* A server of `workgroups` resident workgroups (1..SBE_SERVE_MAX_WORKGROUPS): workgroup 0 polls the
  * slot and republishes a request of several tiles to the others through device memory; a decode
@@ -475,6 +490,18 @@ int sbe_serve_encode_session_planned(sbe_server* srv, const sbe_tm_batch* in, ui
 int sbe_serve_encode_lite_planned(sbe_server* srv, const sbe_lite_batch* in, uint64_t n, uint32_t template_id,
                                   uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status,
                                   const uint64_t* tile_sums, const uint64_t* sb_sums);
+/* Makes a resident server exit now (a shutdown request, then its stream is synchronised) and
+ * keeps it usable: the next request relaunches it.  SBE_OK at once when it is not running.
+ *
+ * WHY THIS MATTERS.  While its kernel is resident (from a request until idle_us after the last
+ * one), a server occupies a HIP hardware queue, and HIP maps streams onto GPU_MAX_HW_QUEUES
+ * queues (4 by default) shared by every stream of the process.  Work on a stream that shares the
+ * server's queue, and any device-wide synchronisation (hipDeviceSynchronize,
+ * torch.cuda.synchronize()), waits until the server exits: up to idle_us after its last request,
+ * and for as long as its owner keeps it busy.  Quiesce the thread's server before such a
+ * synchronisation or before enqueueing large work; keep idle_us short (the C++ mirror's default is
+ * 1 ms, and the mirror quiesces its own server before every batch it launches). */
+int sbe_server_quiesce(sbe_server* srv);
 /* Requests this server ran and kernel launches it took (a launch per idle exit). */
 int sbe_server_stats(const sbe_server* srv, uint64_t* requests, uint64_t* launches);
 

@@ -1237,7 +1237,10 @@ static uint64_t sbedec_extract(const uint8_t* p, uint64_t off, uint64_t rem, uin
     if (off + 4 > rem) return 0;                                   /* :287-290 */
     uint64_t L = rd32(p + off);                                    /* :295-296 */
     off += 4;
-    if (L > rem - 4 || L > 10u * 1024u * 1024u) return 0;          /* :302-305 */
+    /* :302-305 checks L > rem - 4 whatever the offset, so the reference reads past the record
+     * when a later field's length overruns it (undefined); the defined reading: the string must
+     * end inside the record (same result for every in-bounds record) */
+    if (L > rem - off || L > 10u * 1024u * 1024u) return 0;
     *s_off = (uint32_t)off;
     *s_len = (uint32_t)L;                                          /* :308-315 (0: clear) */
     return off + L;

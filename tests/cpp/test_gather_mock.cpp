@@ -8,6 +8,7 @@
 // shards and both SBE_ENOSPC limits (every rank refuses; the root's buffers stay untouched).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -68,9 +69,33 @@ struct RankResult {
     uint64_t totals[2] = {0, 0};
 };
 
+static double now_s() {
+    static const auto t0 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+// a rank's phase, unbuffered, so that a stall shows how far every rank got
+static void phase(int world, int root, int r, const char* what) {
+    std::fprintf(stderr, "[%.3fs] world=%d root=%d rank %d: %s\n", now_s(), world, root, r, what);
+}
+
+struct RankBufs {  // one rank's device buffers, all allocated by the main thread
+    hipStream_t s = nullptr;
+    uint8_t *arena = nullptr, *out = nullptr, *st = nullptr;
+    uint32_t* len = nullptr;
+    uint64_t *ts = nullptr, *off = nullptr;
+    void* ws = nullptr;
+    uint64_t cap = 0;
+    size_t wsb = 0;
+    sbe_comm* c = nullptr;
+};
+
+// Memory management, stream creation and communicator setup / teardown all happen on the main
+// thread, before the rank threads start and after they have joined: a rank thread only launches
+// (encode, gather) and waits on its own stream, so no rank ever allocates or frees (device-wide
+// synchronising calls) while a peer is parked inside a collective.
 static void run_case(const Batch& B, int world, int root, const std::vector<size_t>& cuts, int limit,
-                     const std::vector<uint8_t>& eo, const std::vector<uint64_t>& eoff, const char* lib) {
-    (void)lib;
+                     const std::vector<uint8_t>& eo, const std::vector<uint64_t>& eoff, bool sized) {
+    const double t_case = now_s();
     const size_t N = B.n;
     const uint64_t total = eoff[N];
     uint8_t id[SBE_COMM_ID_BYTES];
@@ -84,53 +109,60 @@ static void run_case(const Batch& B, int world, int root, const std::vector<size
     HIPCK(hipMalloc(&dst_off, (off_cap + 1) * 8));
     HIPCK(hipMemset(dst, 0xAB, dst_cap + 16));
     HIPCK(hipMemset(dst_off, 0xCD, (off_cap + 1) * 8));
+    std::vector<RankBufs> rb(world);
+    std::vector<uint64_t> sizes(2 * (size_t)world);  // the sized entry's {bytes, records} per rank
+    for (int r = 0; r < world; ++r) {
+        RankBufs& b = rb[r];
+        const size_t lo = cuts[r], hi = cuts[r + 1], m = hi - lo;
+        const size_t ab = B.in_base[hi] - B.in_base[lo];
+        b.cap = sbe_encode_output_bound(m, ab, 0);
+        b.wsb = sbe_encode_workspace_size(m);
+        HIPCK(hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
+        HIPCK(hipMalloc(&b.arena, ab + 16));
+        HIPCK(hipMalloc(&b.len, m * 20 + 16));
+        HIPCK(hipMalloc(&b.ts, m * 8 + 16));
+        HIPCK(hipMalloc(&b.out, b.cap + 16));
+        HIPCK(hipMalloc(&b.off, (m + 1) * 8));
+        HIPCK(hipMalloc(&b.st, m + 16));
+        HIPCK(hipMalloc(&b.ws, b.wsb + 16));
+        if (ab) HIPCK(hipMemcpy(b.arena, B.arena.data() + B.in_base[lo], ab, hipMemcpyHostToDevice));
+        if (m) {
+            HIPCK(hipMemcpy(b.len, B.len.data() + 5 * lo, m * 20, hipMemcpyHostToDevice));
+            HIPCK(hipMemcpy(b.ts, B.ts.data() + lo, m * 8, hipMemcpyHostToDevice));
+        }
+        const int rci = sbe_comm_init(&b.c, world, r, id);
+        if (rci != SBE_OK) std::fprintf(stderr, "rank %d: sbe_comm_init %d (%s)\n", r, rci, sbe_last_error());
+        CHECK(rci == SBE_OK);
+        sizes[2 * r] = eoff[hi] - eoff[lo];  // the caller's own size plan (fixed-size records, or a host plan)
+        sizes[2 * r + 1] = m;
+    }
+    HIPCK(hipDeviceSynchronize());
     std::vector<RankResult> res(world);
     std::vector<std::thread> th;
     for (int r = 0; r < world; ++r) {
         th.emplace_back([&, r] {
+            RankBufs& b = rb[r];
+            if (!b.c) return;
             HIPCK(hipSetDevice(0));
-            hipStream_t s;
-            HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            const size_t lo = cuts[r], hi = cuts[r + 1], m = hi - lo;
-            // the shard's packed input
-            const size_t ab = B.in_base[hi] - B.in_base[lo];
-            uint8_t *d_arena, *d_out, *d_st;
-            uint32_t* d_len;
-            uint64_t *d_ts, *d_off;
-            void* d_ws;
-            const uint64_t cap = sbe_encode_output_bound(m, ab, 0);
-            const size_t wsb = sbe_encode_workspace_size(m);
-            HIPCK(hipMalloc(&d_arena, ab + 16));
-            HIPCK(hipMalloc(&d_len, m * 20 + 16));
-            HIPCK(hipMalloc(&d_ts, m * 8 + 16));
-            HIPCK(hipMalloc(&d_out, cap + 16));
-            HIPCK(hipMalloc(&d_off, (m + 1) * 8));
-            HIPCK(hipMalloc(&d_st, m + 16));
-            HIPCK(hipMalloc(&d_ws, wsb + 16));
-            if (ab) HIPCK(hipMemcpy(d_arena, B.arena.data() + B.in_base[lo], ab, hipMemcpyHostToDevice));
-            if (m) {
-                HIPCK(hipMemcpy(d_len, B.len.data() + 5 * lo, m * 20, hipMemcpyHostToDevice));
-                HIPCK(hipMemcpy(d_ts, B.ts.data() + lo, m * 8, hipMemcpyHostToDevice));
-            }
-            sbe_comm* c = nullptr;
-            const int rci = sbe_comm_init(&c, world, r, id);
-            if (rci != SBE_OK) {
-                std::fprintf(stderr, "rank %d: sbe_comm_init %d (%s)\n", r, rci, sbe_last_error());
-                res[r].rc_gather = rci;
-                return;
-            }
-            sbe_tm_batch in{d_arena, nullptr, d_len, d_ts};
-            res[r].rc_enc = sbe_encode_topic_batch(&in, m, 1, 0, d_out, cap, d_off, d_st, d_ws, wsb, s);
+            const size_t m = cuts[r + 1] - cuts[r];
+            phase(world, root, r, "encode");
+            sbe_tm_batch in{b.arena, nullptr, b.len, b.ts};
+            res[r].rc_enc = sbe_encode_topic_batch(&in, m, 1, 0, b.out, b.cap, b.off, b.st, b.ws, b.wsb, b.s);
+            phase(world, root, r, sized ? "gather (sized)" : "gather");
             const bool am_root = r == root;
-            res[r].rc_gather = sbe_gather_encoded(c, root, d_out, d_off, m, am_root ? dst : nullptr, am_root ? dst_cap : 0,
-                                                  am_root ? dst_off : nullptr, am_root ? off_cap : 0, res[r].totals, s);
+            if (sized)
+                res[r].rc_gather = sbe_gather_encoded_sized(b.c, root, sizes.data(), b.out, b.off,
+                                                            am_root ? dst : nullptr, dst_cap,  // the root's, on every rank
+                                                            am_root ? dst_off : nullptr, off_cap, res[r].totals, b.s);
+            else
+                res[r].rc_gather = sbe_gather_encoded(b.c, root, b.out, b.off, m, am_root ? dst : nullptr,
+                                                      am_root ? dst_cap : 0, am_root ? dst_off : nullptr,
+                                                      am_root ? off_cap : 0, res[r].totals, b.s);
             if (res[r].rc_gather != SBE_OK && res[r].rc_gather != SBE_ENOSPC)
                 std::fprintf(stderr, "rank %d: gather %d (%s)\n", r, res[r].rc_gather, sbe_last_error());
-            HIPCK(hipStreamSynchronize(s));
-            CHECK(sbe_comm_destroy(c) == SBE_OK);
-            for (void* p : {(void*)d_arena, (void*)d_len, (void*)d_ts, (void*)d_out, (void*)d_off, (void*)d_st, d_ws})
-                HIPCK(hipFree(p));
-            HIPCK(hipStreamDestroy(s));
+            phase(world, root, r, "stream sync");
+            HIPCK(hipStreamSynchronize(b.s));
+            phase(world, root, r, "done");
         });
     }
     for (auto& t : th) t.join();
@@ -153,11 +185,19 @@ static void run_case(const Batch& B, int world, int root, const std::vector<size
         for (uint64_t x : goff) clean = clean && x == 0xCDCDCDCDCDCDCDCDull;
         CHECK(clean);
     }
+    HIPCK(hipDeviceSynchronize());
+    for (int r = 0; r < world; ++r) {
+        RankBufs& b = rb[r];
+        CHECK(sbe_comm_destroy(b.c) == SBE_OK);
+        for (void* p : {(void*)b.arena, (void*)b.len, (void*)b.ts, (void*)b.out, (void*)b.off, (void*)b.st, b.ws})
+            HIPCK(hipFree(p));
+        HIPCK(hipStreamDestroy(b.s));
+    }
     HIPCK(hipFree(dst));
     HIPCK(hipFree(dst_off));
-    std::printf("case world=%d root=%d limit=%d shards=", world, root, limit);
+    std::printf("case %s world=%d root=%d limit=%d shards=", sized ? "sized" : "plain", world, root, limit);
     for (int r = 0; r < world; ++r) std::printf("%zu%s", cuts[r + 1] - cuts[r], r + 1 < world ? "," : "");
-    std::printf(" -> %s\n", failures ? "FAIL" : "ok");
+    std::printf(" -> %s (%.3f s)\n", failures ? "FAIL" : "ok", now_s() - t_case);
     std::fflush(stdout);
 }
 
@@ -191,16 +231,18 @@ int main() {
     std::vector<uint64_t> eoff(N + 1);
     std::vector<uint8_t> est(N);
     orc_encode_batch(B.arena.data(), nullptr, B.len.data(), B.ts.data(), N, 1, 0, eo.data(), eoff.data(), est.data(), 1);
-    run_case(B, 2, 0, even_cuts(N, 2), kOk, eo, eoff, lib);
-    run_case(B, 2, 1, even_cuts(N, 2), kOk, eo, eoff, lib);
-    run_case(B, 3, 2, even_cuts(N, 3), kOk, eo, eoff, lib);
-    run_case(B, 3, 1, sized_cuts({0, 12345, N - 12345}), kOk, eo, eoff, lib);   // a zero-record shard
-    run_case(B, 8, 0, even_cuts(N, 8), kOk, eo, eoff, lib);
-    run_case(B, 8, 5, sized_cuts({1, 0, 4999, 0, 7000, 3, 0, N - 12003}), kOk, eo, eoff, lib);
-    run_case(B, 8, 7, sized_cuts({0, 0, 0, 0, 0, 0, 0, N}), kOk, eo, eoff, lib);  // all on the last rank
-    run_case(B, 4, 3, even_cuts(N, 4), kShortBytes, eo, eoff, lib);
-    run_case(B, 4, 0, even_cuts(N, 4), kShortOffsets, eo, eoff, lib);
-    run_case(B, 2, 0, sized_cuts({N, 0}), kOk, eo, eoff, lib);  // everything on the root
+    for (const bool sized : {false, true}) {
+        run_case(B, 2, 0, even_cuts(N, 2), kOk, eo, eoff, sized);
+        run_case(B, 2, 1, even_cuts(N, 2), kOk, eo, eoff, sized);
+        run_case(B, 3, 2, even_cuts(N, 3), kOk, eo, eoff, sized);
+        run_case(B, 3, 1, sized_cuts({0, 12345, N - 12345}), kOk, eo, eoff, sized);   // a zero-record shard
+        run_case(B, 8, 0, even_cuts(N, 8), kOk, eo, eoff, sized);
+        run_case(B, 8, 5, sized_cuts({1, 0, 4999, 0, 7000, 3, 0, N - 12003}), kOk, eo, eoff, sized);
+        run_case(B, 8, 7, sized_cuts({0, 0, 0, 0, 0, 0, 0, N}), kOk, eo, eoff, sized);  // all on the last rank
+        run_case(B, 4, 3, even_cuts(N, 4), kShortBytes, eo, eoff, sized);
+        run_case(B, 4, 0, even_cuts(N, 4), kShortOffsets, eo, eoff, sized);
+        run_case(B, 2, 0, sized_cuts({N, 0}), kOk, eo, eoff, sized);  // everything on the root
+    }
     std::printf("gather mock test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }

@@ -154,6 +154,18 @@ int main() {
         CHECK(!SBEDecoder::decode_acknowledgment(r1.data(), r1.size(), id, st, er, ts) && id == "only" && st == "old" &&
               ts == 9);
         CHECK(!SBEDecoder::decode_acknowledgment(r.data(), 15, id, st, er, ts));
+        // a status length that passes the reference's `remaining - 4` check but runs past the
+        // record: refused, nothing read past the end
+        {
+            auto ro = ack32(11, {"msg_3", "OK"});
+            const size_t status_prefix = 16 + 4 + 5;   // header 8 + block 8, messageId prefix + bytes
+            const uint32_t bad = (uint32_t)(ro.size() - 16 - 4);  // <= remaining - 4, > remaining - offset
+            std::memcpy(ro.data() + status_prefix, &bad, 4);
+            id = st = "old";
+            CHECK(!SBEDecoder::decode_acknowledgment(ro.data(), ro.size(), id, st, er, ts) && id == "msg_3" &&
+                  st == "old");
+            cmp_ack(ro, ro.size());
+        }
         auto rt = r;
         rt[2] = 1;
         ts = 3;

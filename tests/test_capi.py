@@ -68,6 +68,9 @@ def test_host_side_entry_points(lib):
     lib.sbe_gather_encoded.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,
                                        ctypes.c_uint64, vp, vp]
     assert lib.sbe_gather_encoded(None, 0, None, None, 0, None, 0, None, 0, None, None) == -1
+    lib.sbe_gather_encoded_sized.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint64, vp,
+                                             ctypes.c_uint64, vp, vp]
+    assert lib.sbe_gather_encoded_sized(None, 0, None, None, None, None, 0, None, 0, None, None) == -1
     lib.sbe_comm_destroy.argtypes = [vp]
     assert lib.sbe_comm_destroy(None) == 0
 

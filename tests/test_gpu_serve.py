@@ -209,14 +209,45 @@ def test_serve_idle_exit_and_relaunch(codec):
         assert req == 4 and launches >= 2
     finally:
         s.close()
-    # back-to-back requests (well inside the default 20 ms idle time) reuse the running kernel
-    s = codec.Server()
+    # back-to-back requests (well inside a 20 ms idle time) reuse the running kernel
+    s = codec.Server(idle_us=20000)
     try:
         a, Ld, t = tm_inputs(arena, L, ts)
         for k in range(20):
             check_same(host(s.encode_topic(a, Ld, t), 5), exp)
         req, launches = s.stats()
         assert req == 20 and launches <= 3
+    finally:
+        s.close()
+
+
+def test_device_sync_after_a_served_call(codec):
+    """A resident server holds up device-wide synchronisation until it goes idle (sbecodec.h,
+    sbe_server_quiesce): torch.cuda.synchronize() after a served call returns within the idle time,
+    and at once after quiesce(), which leaves the server usable (the next request relaunches it)."""
+    arena, L, ts = T.fixed256_orders(5)
+    exp = T.oracle_encode(arena, L, ts)
+    idle_s = 0.05
+    s = codec.Server(idle_us=int(idle_s * 1e6))
+    try:
+        a, Ld, t = tm_inputs(arena, L, ts)
+        s.encode_topic(a, Ld, t)
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        waited = time.perf_counter() - t0
+        assert waited < idle_s + 0.5, waited  # bounded by the idle exit (plus scheduling slack)
+        got = s.encode_topic(a, Ld, t)
+        s.quiesce()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        after_quiesce = time.perf_counter() - t0
+        assert after_quiesce < idle_s / 2, after_quiesce  # the kernel has already left
+        check_same(host(got, 5), exp)
+        check_same(host(s.encode_topic(a, Ld, t), 5), exp)  # relaunched by the next request
+        req, launches = s.stats()
+        assert req == 3 + 1 and launches >= 2  # the quiesce's shutdown counts as a request
+        print(f"device sync after a served call: {waited * 1e3:.2f} ms (idle {idle_s * 1e3:.0f} ms); "
+              f"after quiesce {after_quiesce * 1e3:.3f} ms")
     finally:
         s.close()
 
