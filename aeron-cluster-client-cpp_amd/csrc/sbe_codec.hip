@@ -20,7 +20,7 @@
 //           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105 /
 //           the Lite flyweights), one launch, one wave per 64-record tile:
 //    1. the tile's bytes are staged window by window (16 KiB windows; 12 KiB for batches of records
-//       over 256 B on average, 14 KiB up to 204 B, 8 KiB up to 112 B: sbe_decode_batch_sized) into
+//       over 256 B on average, 15 KiB up to 204 B, 8 KiB up to 112 B: sbe_decode_batch_sized) into
 //       an XOR-swizzled LDS window with 16-byte loads; the second
 //       window's loads are issued before the first one is parsed
 //    2. each lane parses its record from LDS (template-ID dispatch per lane) and writes the
@@ -68,8 +68,12 @@ constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWin
 #ifndef SBE_DEC_MID_AVG
 #define SBE_DEC_MID_AVG 204
 #endif
+// 15 KiB: config 3 (1 M mixed TM / Ack records, 200 B on average) decodes in 56.6 us against 60.0
+// at 14 KiB, 60.5 at 16 KiB and 64.1 at 13 KiB (A/B in one process, profiles/r05_ab_decmid.log,
+// profiles/r04_ab_decmid.log): a CU then holds 10 workgroups instead of 11, but the tiles a 14 KiB
+// window cannot hold whole no longer pay a second window.
 #ifndef SBE_DEC_WIN_MID  // A/B builds only
-#define SBE_DEC_WIN_MID 14336
+#define SBE_DEC_WIN_MID 15360
 #endif
 constexpr uint32_t kWinMid = SBE_DEC_WIN_MID, kWinSmall = 8192;
 constexpr uint64_t kMidAvg = SBE_DEC_MID_AVG, kSmallAvg = SBE_DEC_SMALL_AVG;
