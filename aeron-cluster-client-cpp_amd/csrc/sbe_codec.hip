@@ -76,6 +76,18 @@ constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWin
 #define SBE_DEC_WIN_MID 15360
 #endif
 constexpr uint32_t kWinMid = SBE_DEC_WIN_MID, kWinSmall = 8192;
+// Batches of records over kLargeAvg bytes on average (config 4: 387 B) take a 13 KiB window: a
+// 64-record tile of ~24.8 KB then fits two windows (12 KiB windows hold ~24.2 KB in two, so most
+// tiles paid a third).  Config 4 decode 422.4 -> 405.8 us at 4 M records; session frames (280 B)
+// stay on 12 KiB, where 13 KiB read 69.5 -> 72.0 us (profiles/r05_ab_decwide.log).
+#ifndef SBE_DEC_WIN_LARGE  // A/B builds only
+#define SBE_DEC_WIN_LARGE 13312
+#endif
+#ifndef SBE_DEC_LARGE_AVG
+#define SBE_DEC_LARGE_AVG 320
+#endif
+constexpr uint32_t kWinLarge = SBE_DEC_WIN_LARGE;
+constexpr uint64_t kLargeAvg = SBE_DEC_LARGE_AVG;
 constexpr uint64_t kMidAvg = SBE_DEC_MID_AVG, kSmallAvg = SBE_DEC_SMALL_AVG;
 
 // ------------------------------------------------------------------------------------------
@@ -3057,7 +3069,7 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
 #define SBE_DEC_MINW_WIDE SBE_DEC_MINW
 #endif
 template <uint32_t kMode, uint32_t kWin>
-__global__ __launch_bounds__(kWave, kWin == kWinWide ? SBE_DEC_MINW_WIDE : SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
+__global__ __launch_bounds__(kWave, (kWin == kWinWide || kWin == kWinLarge) ? SBE_DEC_MINW_WIDE : SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
     __shared__ uint32_t win[kWin / 4];
     dec_tile<kMode, kWin>(a, blockIdx.x, win);
 }
@@ -3398,6 +3410,18 @@ __device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
 #define SBE_FC_U 4
 #endif
 constexpr int kFcU = SBE_FC_U;
+// One unaligned 16-byte load per output chunk (a single global_load_dwordx4 at any byte address)
+// instead of the two aligned blocks it spans joined with v_alignbyte: reassembly row 188.4 ->
+// 185.3 us (profiles/r05_ab_fragcopy.log); SBE_FC_UA=0 builds the joined form.
+#ifndef SBE_FC_UA
+#define SBE_FC_UA 1
+#endif
+typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4_a1 g_u32x4_a1;
+__device__ __forceinline__ uint4 gload128_ua(uintptr_t addr) {  // any byte address (one global_load_dwordx4)
+    const u32x4 v = *reinterpret_cast<g_u32x4_a1*>(addr);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
     if (len == 0) return;
     uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
@@ -3405,9 +3429,26 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
     if ((uint64_t)lane < head) dst[lane] = src[lane];
     const uint64_t nc = (len - head) >> 4;
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(src) + head;
+    uint4* d16 = reinterpret_cast<uint4*>(dst + head);
+#if SBE_FC_UA
+    // the chunk's 16 source bytes in one load at their own (unaligned) address: no join, half the
+    // loads (every byte read lies inside the source)
+    for (uint64_t c0 = 0; c0 < nc; c0 += kFcU * kWave) {
+        uint4 x[kFcU];
+#pragma unroll
+        for (int u = 0; u < kFcU; ++u) {
+            const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
+            x[u] = gload128_ua(p0 + 16 * (c < nc ? c : nc - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < kFcU; ++u) {
+            const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
+            if (c < nc) d16[c] = x[u];
+        }
+    }
+#else
     const uint32_t sh = (uint32_t)(p0 & 15u);
     const uintptr_t q0 = p0 & ~(uintptr_t)15;
-    uint4* d16 = reinterpret_cast<uint4*>(dst + head);
     for (uint64_t c0 = 0; c0 < nc; c0 += kFcU * kWave) {
         uint4 x[kFcU], y[kFcU];
 #pragma unroll
@@ -3423,6 +3464,7 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
             if (c < nc) d16[c] = sh ? join16(x[u], y[u], sh) : x[u];
         }
     }
+#endif
     const uint64_t t0 = head + 16 * nc;
     if ((uint64_t)lane < len - t0) dst[t0 + lane] = src[t0 + lane];
 }
@@ -3432,22 +3474,47 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
 // complete groups: the common case) form runs, each copied as one block; a message with a single
 // inside its group is copied fragment by fragment.
 constexpr int kFragGroup = 64;
+#ifndef SBE_FC_PF  // A/B builds: prefetch the next group's message metadata during the copy
+#define SBE_FC_PF 0
+#endif
 __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
     const uint64_t m = a.counts[0];
-    for (uint64_t base = ((uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * kFragGroup; base <= m;
-         base += waves * kFragGroup) {
+    const uint64_t base0 = ((uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * kFragGroup;
+    const uint64_t step = waves * kFragGroup;
+#if SBE_FC_PF
+    // the next group's metadata is loaded while this group is copied (clamped index, loaded
+    // unconditionally: no wait on it before the copy)
+    auto meta = [&](uint64_t b, uint64_t& len_, uint64_t& first_, uint64_t& mlast_, uint64_t& dst_) {
+        uint64_t jj = b + (uint64_t)lane;
+        jj = jj <= m ? jj : m;
+        len_ = a.msize[jj];
+        first_ = a.mfirst[jj];
+        mlast_ = a.mlast[jj];
+        dst_ = a.msg_off[jj];
+    };
+    uint64_t nlen, nfirst, nmlast, ndst;
+    meta(base0, nlen, nfirst, nmlast, ndst);
+#endif
+    for (uint64_t base = base0; base <= m; base += step) {
         const uint64_t j = base + (uint64_t)lane;
+        const bool valid = lane < kFragGroup && j <= m;
+#if SBE_FC_PF
+        uint64_t len = nlen, first = nfirst, mlast = nmlast, dst = ndst;
+        uint64_t src = a.frag_off[first];
+        if (!valid) len = src = dst = mlast = first = 0;
+        meta(base + step, nlen, nfirst, nmlast, ndst);
+#else
         uint64_t len = 0, src = 0, dst = 0, mlast = 0, first = 0;
-        if (lane < kFragGroup && j <= m) {
+        if (valid) {
             len = a.msize[j];
             first = a.mfirst[j];
             mlast = a.mlast[j];
             dst = a.msg_off[j];
             src = a.frag_off[first];
         }
-        const bool valid = lane < kFragGroup && j <= m;
+#endif
         const bool gap = valid && (mlast >> 63);
         // run membership: this message's source follows the previous one's (and neither is gapped)
         const uint64_t pend = __shfl_up(src + len, 1, kWave);
@@ -4115,14 +4182,17 @@ int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t 
     hipEvent_t e0, e1;
     prof_slot(1, &e0, &e1);
     // kernel shape by the average record size (in_bytes = 0: unknown, the 16 KiB window)
-    const int shape = in_bytes > (uint64_t)kWideAvg * n   ? 1
+    const int shape = in_bytes > (uint64_t)kLargeAvg * n  ? 4
+                      : in_bytes > (uint64_t)kWideAvg * n   ? 1
                       : in_bytes == 0                     ? 0
                       : in_bytes <= (uint64_t)kSmallAvg * n ? 3
                       : in_bytes <= (uint64_t)kMidAvg * n   ? 2
                                                           : 0;
 #define SBE_DEC_LAUNCH(M)                                                                                  \
     do {                                                                                                   \
-        if (shape == 1)                                                                                    \
+        if (shape == 4)                                                                                    \
+            hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinLarge>), grid, block, 0, s, e0, e1, 0, a);     \
+        else if (shape == 1)                                                                               \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinWide>), grid, block, 0, s, e0, e1, 0, a);      \
         else if (shape == 2)                                                                               \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinMid>), grid, block, 0, s, e0, e1, 0, a);       \

@@ -1844,6 +1844,182 @@ void MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* r
     run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE, &fill);
 }
 
+// ---- BatchingParser -------------------------------------------------------------------------
+// Two batches: one fills on the caller's thread while the other is decoded by the decode thread
+// (its own device context) or waits, decoded, for the caller's next poll() to deliver it.
+struct BatchingParser::Impl {
+    using clk = std::chrono::steady_clock;
+    enum State { kFilling, kDecoding, kReady };
+    struct Batch {
+        // page-locked (a block of the library's pool, so a new parser reuses the blocks of earlier
+        // ones instead of pinning fresh memory): the one-chunk decode reads it in place
+        std::shared_ptr<void> blk;
+        size_t cap = 0;
+        size_t bytes = 0;
+        uint8_t* b() const { return static_cast<uint8_t*>(blk.get()); }
+        std::vector<uint64_t> off{0};
+        ParsedBatch pb;  // the device descriptors; ParseResults are built at delivery
+        State state = kFilling;
+        uint64_t seq = 0;
+        clk::time_point first{};
+        std::exception_ptr err;
+        size_t n() const { return off.size() - 1; }
+        void reset() {
+            bytes = 0;
+            off.resize(1);
+            state = kFilling;
+            err = nullptr;
+        }
+    };
+    Handler handler;
+    Options opt;
+    Batch b[2];
+    ParseResult cur;  // the result handed to the handler (rewritten in place per record)
+    int fill = 0;
+    uint64_t next_seq = 0;
+    uint64_t n_delivered = 0;
+    mutable std::mutex m;
+    std::condition_variable cv;
+    bool stop = false;
+    std::thread worker;
+
+    Impl(Handler h, Options o) : handler(std::move(h)), opt(o) {
+        if (sbe_device_ready() != 1) fail("no gfx950 device visible");  // as every mirror entry point
+        if (opt.max_records == 0) opt.max_records = 1;
+        for (Batch& x : b) x.off.reserve(opt.max_records + 1);
+        worker = std::thread([this] { run(); });
+    }
+    ~Impl() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        worker.join();
+    }
+    void run() {  // the decode thread
+        std::unique_lock<std::mutex> g(m);
+        for (;;) {
+            cv.wait(g, [&] { return stop || b[0].state == kDecoding || b[1].state == kDecoding; });
+            Batch* x = nullptr;
+            for (Batch& y : b)
+                if (y.state == kDecoding && (!x || y.seq < x->seq)) x = &y;
+            if (!x) return;  // stop, nothing left to decode
+            g.unlock();
+            try {
+                x->pb = MessageParser::decode_batch(x->b(), x->off.data(), x->n());
+            } catch (...) {
+                x->err = std::current_exception();
+            }
+            g.lock();
+            x->state = kReady;
+            cv.notify_all();
+        }
+    }
+    // the filling batch to the decode thread; the other batch (older) is delivered first if it is
+    // decoded, or waited for and then delivered: at most one batch decodes while the next fills
+    size_t hand_off() {
+        Batch& f = b[fill];
+        Batch& o = b[1 - fill];
+        size_t got = 0;
+        if (state(o) != kFilling) got = deliver_wait(o);
+        {
+            std::lock_guard<std::mutex> g(m);
+            f.state = kDecoding;
+            f.seq = next_seq++;
+        }
+        cv.notify_all();
+        fill = 1 - fill;
+        return got;
+    }
+    size_t deliver_wait(Batch& x) {
+        {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return x.state == kReady; });
+        }
+        return deliver(x);
+    }
+    size_t deliver(Batch& x) {  // caller's thread; x is kReady
+        const size_t n = x.n();
+        std::exception_ptr e = x.err;
+        if (e) {
+            x.reset();
+            std::rethrow_exception(e);
+        }
+        // each result built on this thread into one reused ParseResult right before its handler
+        // (the record and the result stay in this core's cache; the reference's handler likewise
+        // receives a ParseResult that lives for the call, src/cluster_client.cpp:1185-1190)
+        for (size_t i = 0; i < n; ++i) {
+            x.pb.result_into(i, cur);
+            handler(cur);
+        }
+        x.pb = ParsedBatch();
+        n_delivered += n;
+        x.reset();
+        return n;
+    }
+    State state(const Batch& x) const {
+        std::lock_guard<std::mutex> g(m);
+        return x.state;
+    }
+};
+
+BatchingParser::BatchingParser(Handler handler) : BatchingParser(std::move(handler), Options{}) {}
+BatchingParser::BatchingParser(Handler handler, Options options)
+    : impl_(std::make_unique<Impl>(std::move(handler), options)) {}
+BatchingParser::~BatchingParser() {
+    try {
+        flush();
+    } catch (...) {
+    }
+}
+
+void BatchingParser::on_fragment(const std::uint8_t* data, std::size_t length) {
+    Impl& I = *impl_;
+    if (I.b[I.fill].n() > 0 &&
+        (I.b[I.fill].n() + 1 > I.opt.max_records || I.b[I.fill].bytes + length > I.opt.max_bytes))
+        I.hand_off();
+    Impl::Batch& f = I.b[I.fill];
+    if (f.bytes + length > f.cap) {  // grow, keeping the bytes already copied
+        const size_t want = std::max(f.bytes + length, std::max(I.opt.max_bytes, (size_t)4096));
+        std::shared_ptr<void> nb = PinnedPool::get().take(want);
+        if (f.bytes) std::memcpy(nb.get(), f.blk.get(), f.bytes);
+        f.blk = std::move(nb);
+        f.cap = want;
+    }
+    if (f.n() == 0) f.first = Impl::clk::now();
+    if (length) copy_small(f.b() + f.bytes, data, length);
+    f.bytes += length;
+    f.off.push_back(f.bytes);
+}
+
+std::size_t BatchingParser::poll() {
+    Impl& I = *impl_;
+    size_t got = 0;
+    Impl::Batch& o = I.b[1 - I.fill];
+    if (I.state(o) == Impl::kReady) got += I.deliver(o);
+    Impl::Batch& f = I.b[I.fill];
+    if (f.n() > 0 && Impl::clk::now() - f.first >= I.opt.max_delay) got += I.hand_off();
+    return got;
+}
+
+std::size_t BatchingParser::flush() {
+    Impl& I = *impl_;
+    size_t got = 0;
+    if (I.b[I.fill].n() > 0) got += I.hand_off();
+    Impl::Batch& o = I.b[1 - I.fill];  // the batch just handed off (or an older one)
+    if (I.state(o) != Impl::kFilling) got += I.deliver_wait(o);
+    return got;
+}
+
+std::size_t BatchingParser::pending() const {
+    const Impl& I = *impl_;
+    std::lock_guard<std::mutex> g(I.m);
+    return I.b[0].n() + I.b[1].n();
+}
+
+std::uint64_t BatchingParser::delivered() const { return impl_->n_delivered; }
+
 ParsedBatch MessageParser::decode_batch(const std::uint8_t* data, const std::uint64_t* rec_off, std::size_t n) {
     ParsedBatch b;
     b.desc_ = run_decode(data, rec_off, n, SBE_DEC_PARSE_MESSAGE);
@@ -1854,6 +2030,9 @@ ParsedBatch MessageParser::decode_batch(const std::uint8_t* data, const std::uin
 }
 
 ParseResult ParsedBatch::result(std::size_t i) const { return materialize(data_ + rec_off_[i], *desc_, i); }
+void ParsedBatch::result_into(std::size_t i, ParseResult& out) const {
+    materialize_into(out, data_ + rec_off_[i], *desc_, i);
+}
 bool ParsedBatch::success(std::size_t i) const { return desc_->status(i) < SBE_ST_ERR_NULL_EMPTY; }
 std::uint8_t ParsedBatch::status(std::size_t i) const { return desc_->status(i); }
 std::uint16_t ParsedBatch::template_id(std::size_t i) const {

@@ -33,6 +33,7 @@
 #pragma once
 
 #include <cstdint>
+#include <chrono>
 #include <functional>
 #include <memory>
 #include <optional>
@@ -304,6 +305,8 @@ public:
     std::size_t size() const { return n_; }
     ParseResult result(std::size_t i) const;
     ParseResult operator[](std::size_t i) const { return result(i); }
+    // result(i) written into `out`, which keeps its string buffers (no allocation once they have grown)
+    void result_into(std::size_t i, ParseResult& out) const;
     bool success(std::size_t i) const;
     std::uint8_t status(std::size_t i) const;  // SBE_ST_* of include/sbecodec.h
     std::uint16_t template_id(std::size_t i) const;
@@ -326,6 +329,48 @@ private:
 };
 
 std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len);
+
+// MessageParser::parse_message at the reference's call granularity, batched across polls.  The
+// reference parses one fragment per call from its poll handler (handle_incoming_message,
+// src/cluster_client.cpp:1185) in polls of up to 100 fragments
+// (include/aeron_cluster/performance_config.hpp:17); one GPU call per fragment costs a launch or
+// a serve round trip, far more than the parse.  A BatchingParser takes the fragments of many
+// polls: on_fragment copies each one (the fragment is only valid during the poll callback) into
+// a page-locked batch; when the batch holds max_records records or max_bytes bytes, or at a poll()
+// whose oldest pending record has waited max_delay, the batch goes to a decode thread
+// (MessageParser::parse_batch into a reused vector) and filling continues in a second batch.
+// Handlers run on the caller's thread, in arrival order, inside poll() / flush() (never inside
+// on_fragment unless both batches are busy: then on_fragment waits for the older one and delivers
+// it first), with handler(result) == handler(MessageParser::parse_message(fragment)).
+// Added latency per record: at most max_delay + one batch decode after the poll that follows it
+// (a caller polling continuously), or whatever the caller waits between polls.
+class BatchingParser {
+public:
+    struct Options {
+        std::size_t max_records = 8192;
+        std::size_t max_bytes = std::size_t(4) << 20;
+        std::chrono::microseconds max_delay{200};
+    };
+    using Handler = std::function<void(const ParseResult&)>;
+    explicit BatchingParser(Handler handler);
+    BatchingParser(Handler handler, Options options);
+    ~BatchingParser();  // flush(): every record given is delivered
+    BatchingParser(const BatchingParser&) = delete;
+    BatchingParser& operator=(const BatchingParser&) = delete;
+
+    void on_fragment(const std::uint8_t* data, std::size_t length);
+    // After each poll: delivers every decoded batch; hands the filling batch to the decoder if its
+    // oldest record has waited max_delay.  Returns the records delivered.
+    std::size_t poll();
+    // Decodes everything given so far and delivers it.  Returns the records delivered.
+    std::size_t flush();
+    std::size_t pending() const;  // given but not yet delivered
+    std::uint64_t delivered() const;
+
+private:
+    struct Impl;
+    std::unique_ptr<Impl> impl_;
+};
 
 using TopicMessageCallback = std::function<void(std::string_view topic, std::string_view msg_type,
                                                 std::string_view uuid, std::string_view payload,

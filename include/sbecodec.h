@@ -269,8 +269,9 @@ int sbe_decode_batch(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uin
 
 /* sbe_decode_batch with the batch's total record bytes (rec_off[n] - rec_off[0]) as the caller
  * knows them, used only to pick the kernel shape (the LDS window of a 64-record tile, which caps
- * the workgroups per CU): records over 256 B on average (session frames, long payloads) 12 KiB
- * windows (a tile takes two or more); up to 112 B 8 KiB; up to 204 B 15 KiB; others 16 KiB.
+ * the workgroups per CU): records over 320 B on average (long payloads) 13 KiB windows, over 256 B
+ * (session frames) 12 KiB (a tile takes two or more); up to 112 B 8 KiB; up to 204 B 15 KiB;
+ * others 16 KiB.
  * in_bytes = 0: the 16 KiB kernel.  Outputs are identical either way. */
 int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t n, uint64_t in_bytes, uint32_t mode,
                            const sbe_decoded* out, void* stream);

@@ -205,9 +205,12 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
     const auto batch = MessageParser::parse_batch(all.data(), off.data(), cases.size());
     const ParsedBatch pb = MessageParser::decode_batch(all.data(), off.data(), cases.size());
     CHECK(batch.size() == cases.size() && pb.size() == cases.size());
+    ParseResult into;  // one object rewritten record after record (every kind over every other)
     for (size_t i = 0; i < cases.size(); ++i) {
         CHECK(same(batch[i], single[i]));
         CHECK(same(pb.result(i), single[i]));
+        pb.result_into(i, into);
+        CHECK(same(into, single[i]));
         CHECK(pb.success(i) == single[i].success && pb.template_id(i) == single[i].template_id &&
               pb.schema_id(i) == single[i].schema_id && pb.timestamp(i) == single[i].timestamp &&
               pb.sequence_number(i) == single[i].sequence_number);
@@ -246,6 +249,51 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
         ++visited;
     });
     CHECK(visited == cases.size());
+
+    // BatchingParser: the cases repeated, fed in polls of 1-100 fragments (the reference's
+    // per-poll limit), delivered in order with results equal to parse_message's, under small
+    // batches (many hand-offs, on_fragment waiting for the older batch), the byte limit, the
+    // deadline, an explicit flush and the destructor's flush
+    {
+        const size_t N = 5000;
+        struct Setting {
+            size_t max_records, max_bytes;
+            int delay_us;
+        };
+        for (const Setting st : {Setting{7, 1u << 20, 1000000}, Setting{4096, 1u << 20, 200},
+                                 Setting{8192, 3000, 1000000}, Setting{1, 1u << 20, 0}}) {
+            size_t got = 0;
+            bool ok = true;
+            {
+                BatchingParser::Options o;
+                o.max_records = st.max_records;
+                o.max_bytes = st.max_bytes;
+                o.max_delay = std::chrono::microseconds(st.delay_us);
+                BatchingParser bp([&](const ParseResult& r) { ok = ok && same(r, single[got++ % cases.size()]); }, o);
+                uint64_t seed = 12345;
+                size_t fed = 0;
+                while (fed < N) {
+                    seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
+                    const size_t poll = 1 + (size_t)((seed >> 33) % 100);
+                    for (size_t k = 0; k < poll && fed < N; ++k, ++fed) {
+                        const Case& c = cases[fed % cases.size()];
+                        bp.on_fragment(c.rec.empty() ? nullptr : c.rec.data(), c.rec.size());
+                    }
+                    (void)bp.poll();
+                    CHECK(got + bp.pending() == fed);
+                }
+                if (st.max_records != 7) {
+                    const size_t before = got;
+                    CHECK(bp.flush() == N - before);
+                    CHECK(got == N && bp.pending() == 0 && bp.delivered() == N);
+                }
+            }  // destructor: flush
+            CHECK(ok && got == N);
+            if (!(ok && got == N))
+                std::fprintf(stderr, "  BatchingParser max_records %zu: %zu of %zu delivered, ok %d\n", st.max_records,
+                             got, N, (int)ok);
+        }
+    }
 
     // MessageParser's other public statics (sbe_messages.hpp:423-450, sbe_encoder.cpp:554-616)
     CHECK(same(MessageParser::decode_topic_message_with_sbe(wire.data(), wire.size()),

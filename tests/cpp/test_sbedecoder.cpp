@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -213,6 +214,17 @@ int main() {
     }
     cmp_session({}, 0);
     cmp_ack({}, 0);
+    // BatchingParser without a device (this binary runs on the CPU): refused at construction with
+    // the mirror's exception, as every entry point of the mirror is
+    if (!gpu_codec_available()) {
+        bool threw = false;
+        try {
+            BatchingParser bp([](const ParseResult&) {});
+        } catch (const std::runtime_error& e) {
+            threw = std::strstr(e.what(), "gfx950") != nullptr;
+        }
+        CHECK(threw);
+    }
     std::printf("sbedecoder test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }
