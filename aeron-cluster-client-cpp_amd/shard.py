@@ -41,6 +41,16 @@ class RcclGather:
         return self._codec.gather_encoded(self.comm, out, out_off, n, root=root, dst=dst, dst_off=dst_off,
                                           stream=stream)
 
+    def gather_sized(self, sizes, out, out_off, root: int = 0, dst=None, dst_off=None, dst_capacity: int = 0,
+                     dst_off_capacity: int = 0, stream=None):
+        """The same for callers that know every rank's shard size (sizes = [(bytes, records)] per
+        group rank, identical on every rank; fixed-size records, or a host size plan): no size
+        all-gather and no host wait (sbe_gather_encoded_sized), so the next shard's encode can be
+        enqueued while this one travels.  Every rank passes the root's capacities."""
+        return self._codec.gather_encoded_sized(self.comm, sizes, out, out_off, root=root, dst=dst, dst_off=dst_off,
+                                                dst_capacity=dst_capacity, dst_off_capacity=dst_off_capacity,
+                                                stream=stream)
+
     def close(self):
         self.comm.close()
 

@@ -290,6 +290,35 @@ def config5(args, world, rank, dev):
                                 "collective": "sbe_gather_encoded (ncclAllGather of sizes + grouped ncclSend/ncclRecv)"}
         if rank == 0:
             res["encode_gather"]["verify"] = verify
+        # fixed-256 shards have known sizes: the sized gather (no size all-gather, no host wait per
+        # gather), every rank's encode and transfers enqueued back to back
+        sizes = [(256 * (b - a), b - a) for a, b in (shard.shard_range(N, world, r) for r in range(world))]
+        cap, off_cap = sbecodec.output_bound(N, 222 * N), N + 1  # the root's buffers, known to every rank
+        g.gather_sized(sizes, out, out_off, root=0, dst=dst, dst_off=dst_off, dst_capacity=cap,
+                       dst_off_capacity=off_cap)
+        torch.cuda.synchronize()
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            enc()
+            g.gather_sized(sizes, out, out_off, root=0, dst=dst, dst_off=dst_off, dst_capacity=cap,
+                           dst_off_capacity=off_cap)
+        torch.cuda.synchronize()
+        barrier(world)
+        t_egs = max_over_ranks((time.perf_counter() - t0) / reps, world)
+        verify_s = None
+        if rank == 0:
+            verify_s = verify_gathered(dst, dst_off, N, dev, ws)
+            ok = ok and verify_s["mismatched_chunks"] == 0
+        res["encode_gather_sized"] = {"seconds": t_egs, "records_per_s": N / t_egs,
+                                      "gather_seconds": max(t_egs - t_enc, 0.0),
+                                      "GBps_into_root": into_root / max(t_egs - t_enc, 1e-9) / 1e9,
+                                      "frac_of_xgmi_root_ingress":
+                                          into_root / max(t_egs - t_enc, 1e-9) / 1e9 / XGMI_ROOT_GBS,
+                                      "collective": "sbe_gather_encoded_sized (grouped ncclSend/ncclRecv only)"}
+        if rank == 0:
+            res["encode_gather_sized"]["verify"] = verify_s
         g.close()
         del dst, dst_off
     else:

@@ -19,13 +19,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("libs", nargs="+")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--clean", action="store_true",
+                help="no whole message inside a group (every group's bytes in input order: the flat copy)")
 args = ap.parse_args()
 
 sbecodec.use_library(os.path.abspath(args.libs[0]))
 sbecodec.require_device()
 dev = torch.device("cuda:0")
 n = 1_000_000
-data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512, p_group=0.1)
+data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512, p_group=0.1, p_inner=0.0 if args.clean else 0.1)
 d = torch.from_numpy(data).to(dev)
 o = torch.from_numpy(off.view(np.int64)).to(dev)
 f = torch.from_numpy(flags).to(dev)
@@ -56,5 +58,5 @@ for rnd in range(args.rounds):
         res[p].append(e0.elapsed_time(e1) / args.steps)
 for p in args.libs:
     v = np.array(res[p])
-    print(f"reassemble {os.path.basename(p):24s} med {np.median(v) * 1e3:8.1f} us  min {v.min() * 1e3:8.1f} us  "
+    print(f"reassemble{'(clean)' if args.clean else ''} {os.path.basename(p):24s} med {np.median(v) * 1e3:8.1f} us  min {v.min() * 1e3:8.1f} us  "
           f"{nbytes / (np.median(v) * 1e-3) / 1e12:5.2f} TB/s (all launches)", flush=True)

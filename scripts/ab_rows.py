@@ -52,6 +52,14 @@ def prep(kind):
         data, off = T.mixed_records(1_000_000)
         return dict(n=1_000_000, data=torch.from_numpy(data).to(dev),
                     off=torch.from_numpy(off.view(np.int64)).to(dev), enc=False)
+    if kind.startswith("fixedp"):  # fixed-size TopicMessages with a P-byte payload, random printable bytes
+        P = int(kind[6:])
+        rec = 34 + 6 + 12 + 29 + P + 32
+        n = (4_000_000 * 387) // rec
+        lens = torch.tensor([6, 12, 29, P, 32], dtype=torch.int32, device=dev).repeat(n, 1)
+        a = torch.randint(32, 127, (n * (rec - 34),), dtype=torch.uint8, device=dev)
+        t = torch.arange(n, dtype=torch.int64, device=dev) + 1_760_000_000_000_000_000
+        return dict(n=n, a=a, l=lens, t=t, enc=True, session=False)
     if kind.startswith("lite"):
         t_id, n = int(kind[4:]), 1_000_000
         arena, L, tid, seq = T.lite_records(n, t_id)
@@ -134,5 +142,8 @@ for k in works:
     for p in args.libs:
         r = res[(p, k)]
         pk = f"pack med {np.median(r['pack']) * 1e3:8.1f} us" if r["pack"] else " " * 21
+        if r["pack"] and "lite" not in works[k] and not works[k]["session"]:  # algorithmic TB/s
+            alg = 2 * int(works[k]["l"].sum()) + (18 + 34) * works[k]["n"]
+            pk += f" {alg / (np.median(r['pack']) * 1e-3) / 1e12:5.2f} TB/s"
         print(f"{k:8s} {os.path.basename(p):22s} {pk} | decode med {np.median(r['dec']) * 1e3:8.1f} us "
               f"(min {np.min(r['dec']) * 1e3:8.1f})", flush=True)

@@ -157,11 +157,11 @@ def oracle_reassemble(data, frag_off, flags):
     return msgs, carry
 
 
-def fragment_stream(n, seed, p_single=0.6, maxlen=300, p_group=None):
+def fragment_stream(n, seed, p_single=0.6, maxlen=300, p_group=None, p_inner=0.1):
     """Random Aeron fragment stream: lengths 0..maxlen, flags drawn from whole messages
     (BEGIN|END, probability p_single), BEGIN … END sequences of 2-5 fragments (p_group, default
-    0.9 - p_single; a middle fragment is a whole message with probability 0.1), and stray middle /
-    END / BEGIN fragments (the rest)."""
+    0.9 - p_single; a middle fragment is a whole message with probability p_inner), and stray
+    middle / END / BEGIN fragments (the rest)."""
     rng = np.random.default_rng(seed)
     flags = np.zeros(n, np.uint8)
     p_grp_end = p_single + (0.9 - p_single if p_group is None else p_group)
@@ -177,7 +177,7 @@ def fragment_stream(n, seed, p_single=0.6, maxlen=300, p_group=None):
                 if i >= n:
                     break
                 flags[i] = 0x80 if t == 0 else (0x40 if t == k - 1 else 0x00)
-                if 0 < t < k - 1 and rng.random() < 0.1:
+                if 0 < t < k - 1 and rng.random() < p_inner:
                     flags[i] = 0xC0  # a whole message inside a group
                 i += 1
         else:

@@ -87,6 +87,26 @@ def test_gpu_random(codec, n, seed, p_single):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,seed,cut", [(200000, 21, 0), (200000, 22, 3), (5000, 23, 1), (64, 24, 0)])
+def test_gpu_in_order_streams(codec, n, seed, cut):
+    """Streams whose output is their input (whole messages and complete groups, no message inside
+    a group, nothing dropped): every 64-message group of frag_copy is one run.  cut > 0 ends the
+    batch inside a group (the carry is the tail of the input, still in order); seed 23 drops one
+    pending group (a BEGIN over it), which splits the run there."""
+    data, off, flags = T.fragment_stream(n, seed, p_single=0.9, maxlen=400, p_group=0.1, p_inner=0.0)
+    if cut:  # the last group open: drop its END
+        k = int(np.nonzero(flags == 0x40)[0][-1])
+        flags = flags[:k].copy()
+        off = off[:k + 1].copy()
+        data = data[:int(off[-1])].copy()
+    if seed == 23:  # a BEGIN over a pending group: its bytes are dropped
+        g = int(np.nonzero(flags == 0x80)[0][0])
+        flags = flags.copy()
+        flags[g + 1] = 0x80
+    assert gpu_reassemble(codec, data, off, flags) == T.oracle_reassemble(data, off, flags)
+
+
+@pytest.mark.gpu
 def test_gpu_carry_continues_the_next_batch(codec):
     data, off, flags = T.fragment_stream(20000, 7, 0.3)
     exp_msgs, exp_carry = T.oracle_reassemble(data, off, flags)
