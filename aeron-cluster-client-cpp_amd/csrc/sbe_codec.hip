@@ -3535,15 +3535,32 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
             const int k = __builtin_ctzll(mk);
             const uint64_t D = uniform64(__shfl(dst, (int)k, kWave));
             const uint64_t ML = uniform64(__shfl(mlast, (int)k, kWave));
-            {  // a single inside the group: fragment by fragment, skipping singles
-                const uint64_t F = uniform64(__shfl(first, (int)k, kWave)), last = ML & ~(1ull << 63);
-                uint64_t at = 0;
-                for (uint64_t f = F; f <= last; ++f) {
-                    if (frag_single(a.flags[f])) continue;
-                    const uint64_t l = a.frag_off[f + 1] - a.frag_off[f];
-                    wave_copy16(a.out + D + at, a.in + a.frag_off[f], l, lane);
-                    at += l;
+            // a single inside the group: the group's fragments 64 at a time, one a lane (flags and
+            // offsets loaded at once, not one dependent round trip per fragment), singles skipped,
+            // consecutive kept fragments (back to back in the input) copied as one run
+            const uint64_t F = uniform64(__shfl(first, (int)k, kWave)), last = ML & ~(1ull << 63);
+            uint64_t at = 0;
+            for (uint64_t f0 = F; f0 <= last; f0 += kWave) {
+                const uint64_t f = f0 + (uint64_t)lane;
+                bool take = false;
+                uint64_t fo = 0, fl = 0;
+                if (f <= last) {
+                    take = !frag_single(a.flags[f]);
+                    fo = a.frag_off[f];
+                    fl = take ? a.frag_off[f + 1] - fo : 0;
                 }
+                const uint64_t incl = wave_incl_scan64(fl, lane), excl = incl - fl;  // bytes before it
+                const bool prev = __shfl_up(take ? 1 : 0, 1, kWave) != 0;
+                const uint64_t kept = __ballot(take);
+                for (uint64_t rm = __ballot(take && (lane == 0 || !prev)); rm; rm &= rm - 1) {
+                    const int r0 = __builtin_ctzll(rm);
+                    const uint64_t after = ~kept & ~((2ull << r0) - 1);  // first lane past the run
+                    const int r1 = after ? __builtin_ctzll(after) : kWave;
+                    const uint64_t d0 = uniform64(__shfl(excl, r0, kWave));
+                    const uint64_t d1 = uniform64(__shfl(incl, r1 - 1, kWave));
+                    wave_copy16(a.out + D + at + d0, a.in + uniform64(__shfl(fo, r0, kWave)), d1 - d0, lane);
+                }
+                at += lane_u64(incl, kWave - 1);
             }
         }
     }
