@@ -179,7 +179,7 @@ __device__ inline uint32_t zero_bytes(uint32_t x) {  // 0x80 in exactly the zero
 __device__ inline uint32_t special4(uint32_t w) {  // 4-bit mask of w's special bytes
     const uint32_t ctl = ~((w & 0x7f7f7f7fu) + 0x60606060u) & 0x80808080u;  // low 7 bits < 0x20
     const uint32_t m = (w & 0x80808080u) | ctl | zero_bytes(w ^ 0x22222222u) | zero_bytes(w ^ 0x5c5c5c5cu);
-    return (((m >> 7) * 0x00204081u) >> 21) & 0xfu;
+    return __builtin_amdgcn_udot4(m >> 7, 0x08040201u, 0u, false);  // flags as bits 0-3 (one v_dot4)
 }
 __device__ inline uint32_t special16(const uint4& v) {
     return special4(v.x) | (special4(v.y) << 4) | (special4(v.z) << 8) | (special4(v.w) << 12);

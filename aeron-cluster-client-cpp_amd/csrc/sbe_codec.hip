@@ -2514,7 +2514,7 @@ __device__ __forceinline__ uint64_t printable_mask64(const R_t& R, uint32_t p, u
         const uint32_t w = R.adw(q0 + 4 * (k < kmax ? k : kmax));
         const uint32_t lo7 = w & 0x7f7f7f7fu;
         const uint32_t pr = (lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u;
-        const uint32_t c = (((pr >> 7) * 0x00204081u) >> 21) & 0xfu;
+        const uint32_t c = __builtin_amdgcn_udot4(pr >> 7, 0x08040201u, 0u, false);  // the four flags as bits 0-3
         if (k < 16) m |= (uint64_t)c << (4 * k);
         else extra = c;
     }
@@ -2528,7 +2528,9 @@ __device__ __forceinline__ uint64_t printable_mask64(const R_t& R, uint32_t p, u
 __device__ __forceinline__ uint32_t printable4(uint32_t w) {  // bit k: byte k of w is printable
     const uint32_t lo7 = w & 0x7f7f7f7fu;
     const uint32_t pr = (lo7 + 0x60606060u) & ~(lo7 + 0x01010101u) & ~w & 0x80808080u;
-    return (((pr >> 7) * 0x00204081u) >> 21) & 0xfu;
+    // the four byte flags (bits 7, 15, 23, 31) gathered as bits 0-3 by one v_dot4_u32_u8 (weights
+    // 1, 2, 4, 8) instead of a quarter-rate multiply and two shifts
+    return __builtin_amdgcn_udot4(pr >> 7, 0x08040201u, 0u, false);
 }
 template <>
 __device__ __forceinline__ uint64_t printable_mask64<LdsRec>(const LdsRec& R, uint32_t p, uint32_t nbytes) {
