@@ -57,6 +57,11 @@ void snippet_parse_batch() {
 #include "snip_parse_batch.inc"
 }
 
+void snippet_batching_parser() {
+    auto message_callback_ = [](const aeron_cluster::ParseResult&) {};
+#include "snip_batching_parser.inc"
+}
+
 void snippet_gather() {
     int rank = 0, world = 1;
     sbe_tm_batch shard{};
