@@ -184,6 +184,10 @@ __device__ inline uint32_t special4(uint32_t w) {  // 4-bit mask of w's special 
 __device__ inline uint32_t special16(const uint4& v) {
     return special4(v.x) | (special4(v.y) << 4) | (special4(v.z) << 8) | (special4(v.w) << 12);
 }
+__device__ inline uint32_t nul4(uint32_t w) { return __builtin_amdgcn_udot4(zero_bytes(w) >> 7, 0x08040201u, 0u, false); }
+__device__ inline uint32_t nul16(const uint4& v) {  // bit k set iff byte k of the block is 0
+    return nul4(v.x) | (nul4(v.y) << 4) | (nul4(v.z) << 8) | (nul4(v.w) << 12);
+}
 
 // jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
 // Out-of-line helpers take the sink by value and return it: a sink passed by reference lives in
@@ -241,15 +245,61 @@ __device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
     return s;
 }
 
+// ---- decimal text in registers ----------------------------------------------------------------
+// A private digit array indexed by a running count lives in scratch (every digit a scratch store
+// and load); these helpers keep the digits as packed ASCII words and append them with the sink's
+// run(), so the common path touches no scratch.
+
+// The four ASCII digits of v < 10000, most significant in byte 0.
+__device__ inline uint32_t asc4(uint32_t v) {
+    const uint32_t a = v / 100u, b = v - 100u * a;
+    const uint32_t a1 = a / 10u, b1 = b / 10u;
+    return 0x30303030u | a1 | (a - 10u * a1) << 8 | b1 << 16 | (b - 10u * b1) << 24;
+}
+
+// Twenty ASCII digits of v, zero padded, most significant first: bytes 0-15 in a, 16-19 in b.
+struct Dec20 {
+    uint4 a;
+    uint32_t b;
+};
+__device__ inline Dec20 dec20(uint64_t v) {
+    constexpr uint64_t kE16 = 10000000000000000ull;
+    const uint64_t hi = v / kE16;  // <= 1844
+    const uint64_t r = v - hi * kE16;
+    const uint32_t mid = (uint32_t)(r / 100000000u), lo = (uint32_t)(r - (uint64_t)mid * 100000000u);
+    Dec20 d;
+    d.a.x = asc4((uint32_t)hi);
+    d.a.y = asc4(mid / 10000u);
+    d.a.z = asc4(mid % 10000u);
+    d.a.w = asc4(lo / 10000u);
+    d.b = asc4(lo % 10000u);
+    return d;
+}
+
+// Appends bytes [o, o + m) of the twenty digits.
 template <class S>
-__device__ void dec_u64(S& s, uint64_t v) {
-    char b[20];
-    int n = 0;
-    do {
-        b[n++] = (char)('0' + v % 10);
-        v /= 10;
-    } while (v);
-    while (n) s.put((uint8_t)b[--n]);
+__device__ inline void dec_run(S& s, const Dec20& d, uint32_t o, uint32_t m) {
+    if (o < 16) {
+        const uint32_t m1 = m < 16 - o ? m : 16 - o;
+        s.run(d.a, o, m1);
+        m -= m1;
+        o = 16;
+    }
+    if (m) s.run(make_uint4(d.b, 0u, 0u, 0u), o - 16, m);
+}
+
+__device__ inline uint32_t ndig64(uint64_t v) {  // decimal digits of v (1 for 0)
+    uint32_t d = 1;
+    uint64_t p = 10;
+#pragma unroll
+    for (int k = 1; k < 20; ++k, p *= 10) d += v >= p ? 1u : 0u;
+    return d;
+}
+
+template <class S>
+__device__ inline void dec_u64(S& s, uint64_t v) {
+    const uint32_t nd = ndig64(v);
+    dec_run(s, dec20(v), 20 - nd, nd);
 }
 
 template <class S>
@@ -422,6 +472,71 @@ __device__ inline void put_digits(S& s, uint32_t v, int w) {
         if (q >= 9 - w) s.put((uint8_t)('0' + dg[q]));
 }
 
+// ---- the register path for price-like values ----
+// |v| = I + F / 2^k with k <= 64 and I < 1e17 (what Exact's register mode covers): I, F, k.
+__device__ inline bool small_parts(double v, uint64_t& I, uint64_t& F, uint32_t& k) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v) & ~(1ull << 63);
+    const uint32_t ex = (uint32_t)(bits >> 52);
+    uint64_t m = bits & ((1ull << 52) - 1);
+    int e;
+    if (ex == 0) e = -1074;
+    else m |= 1ull << 52, e = (int)ex - 1075;
+    const int t = __builtin_ctzll(m);
+    m >>= t;
+    e += t;
+    if (e < 0 && e >= -64) {
+        k = (uint32_t)-e;
+        F = k >= 64 ? m : (m & ((1ull << k) - 1));
+        I = k >= 64 ? 0 : (m >> k);
+        return true;
+    }
+    if (e >= 0 && e <= 10 && (m << e) < 100000000000000000ull) {
+        k = 0;
+        F = 0;
+        I = m << e;
+        return true;
+    }
+    return false;
+}
+
+typedef unsigned __int128 u128;
+__device__ inline u128 low_bits(uint32_t k) { return (((u128)1) << k) - 1; }  // k <= 64
+
+__constant__ uint64_t kPow10[20] = {1ull,
+                                    10ull,
+                                    100ull,
+                                    1000ull,
+                                    10000ull,
+                                    100000ull,
+                                    1000000ull,
+                                    10000000ull,
+                                    100000000ull,
+                                    1000000000ull,
+                                    10000000000ull,
+                                    100000000000ull,
+                                    1000000000000ull,
+                                    10000000000000ull,
+                                    100000000000000ull,
+                                    1000000000000000ull,
+                                    10000000000000000ull,
+                                    100000000000000000ull,
+                                    1000000000000000000ull,
+                                    10000000000000000000ull};
+
+__device__ inline uint32_t tz_dec(uint32_t v) {  // trailing decimal zeros of 0 < v < 1e9
+    uint32_t z = 0;
+    if (v % 100000000u == 0) z += 8, v /= 100000000u;
+    if (v % 10000u == 0) z += 4, v /= 10000u;
+    if (v % 100u == 0) z += 2, v /= 100u;
+    if (v % 10u == 0) z += 1;
+    return z;
+}
+
+template <class S>
+__device__ __noinline__ S fmt_fixed6_slow(S s, double v);
+template <class S>
+__device__ __noinline__ S fmt_g17_slow(S s, double v);
+
 // "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
 // round half to even on the exact value; inf / nan as glibc prints them.
 template <class S>
@@ -442,6 +557,25 @@ __device__ __noinline__ S fmt_fixed6(S s, double v) {
         lit(s, "0.000000");
         return s;
     }
+    uint64_t I, F;
+    uint32_t k;
+    if (!small_parts(v, I, F, k)) return fmt_fixed6_slow(s, v);
+    uint32_t kept = 0;  // the six decimals, rounded half to even on the exact remainder
+    if (k) {
+        const u128 t = (u128)F * 1000000u;
+        kept = (uint32_t)(t >> k);
+        const u128 rem = t & low_bits(k), half = ((u128)1) << (k - 1);
+        if (rem > half || (rem == half && (kept & 1)))
+            if (++kept == 1000000u) kept = 0, ++I;
+    }
+    dec_u64(s, I);
+    s.put('.');
+    s.run(make_uint4(asc4(kept / 10000u), asc4(kept % 10000u), 0u, 0u), 2, 6);
+    return s;
+}
+
+template <class S>
+__device__ __noinline__ S fmt_fixed6_slow(S s, double v) {  // |v| outside the register path (sign printed)
     Exact x;
     x.init(v);
     const uint32_t c1 = x.frac_next9();
@@ -496,6 +630,77 @@ __device__ __noinline__ S fmt_g17(S s, double v) {
         lit(s, "0.0");
         return s;
     }
+    uint64_t I, F;
+    uint32_t k;
+    if (!small_parts(v, I, F, k)) return fmt_g17_slow(s, v);
+    // D: the first 18 significant digits, X: the decimal exponent of the first, sticky: any
+    // nonzero digit past them
+    uint64_t D;
+    int X;
+    bool sticky;
+    if (I) {
+        const uint32_t nd = ndig64(I);  // 1..17
+        const uint64_t p = kPow10[18 - nd];
+        const u128 t = (u128)F * p;
+        D = I * p + (k ? (uint64_t)(t >> k) : 0ull);
+        sticky = k && (t & low_bits(k)) != 0;
+        X = (int)nd - 1;
+    } else {  // 0 < F / 2^k < 1: nine-digit chunks until the first nonzero one
+        X = -1;
+        uint32_t c;
+        for (;;) {
+            const u128 t = (u128)F * kE9;
+            c = (uint32_t)(t >> k);
+            F = (uint64_t)(t & low_bits(k));
+            if (c) break;
+            X -= 9;
+        }
+        const uint32_t w0 = ndig64(c);
+        X -= 9 - (int)w0;
+        const uint64_t p = kPow10[18 - w0];
+        const u128 t = (u128)F * p;
+        D = (uint64_t)c * p + (uint64_t)(t >> k);
+        sticky = (t & low_bits(k)) != 0;
+    }
+    // round to 17 digits, half to even
+    uint64_t M = D / 10;
+    const uint32_t r = (uint32_t)(D - 10 * M);
+    M += (r > 5 || (r == 5 && (sticky || (M & 1)))) ? 1 : 0;
+    if (M == 100000000000000000ull) M = 10000000000000000ull, ++X;
+    const uint32_t mhi = (uint32_t)(M / 100000000u), mlo = (uint32_t)(M - (uint64_t)mhi * 100000000u);
+    const int last = 16 - (int)(mlo ? tz_dec(mlo) : 8 + tz_dec(mhi));  // trailing zeros dropped
+    const Dec20 dg = dec20(M);  // digit j of the 17 at byte 3 + j
+    if (X < -4 || X >= 17) {
+        dec_run(s, dg, 3, 1);
+        if (last > 0) {
+            s.put('.');
+            dec_run(s, dg, 4, (uint32_t)last);
+        }
+        s.put('e');
+        int ax = X;
+        if (ax < 0) s.put('-'), ax = -ax;
+        else s.put('+');
+        if (ax < 10) s.put('0');
+        dec_u64(s, (uint64_t)ax);
+    } else if (X >= 0) {
+        dec_run(s, dg, 3, (uint32_t)X + 1);
+        if (last > X) {
+            s.put('.');
+            dec_run(s, dg, 4 + (uint32_t)X, (uint32_t)(last - X));
+        } else {
+            lit(s, ".0");
+        }
+    } else {
+        s.put('0');
+        s.put('.');
+        for (int j = 0; j < -X - 1; ++j) s.put('0');
+        dec_run(s, dg, 3, (uint32_t)last + 1);
+    }
+    return s;
+}
+
+template <class S>
+__device__ __noinline__ S fmt_g17_slow(S s, double v) {  // |v| outside the register path (sign printed)
     Exact x;
     x.init(v);
     // first 18 significant digits of the expansion, the decimal exponent X of the first, sticky
@@ -594,13 +799,21 @@ __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFi
         return;
     }
     const double q = a.quantity[i];
-    uint32_t id_len = l[1];  // headers["origin_id"] = identifier.c_str()
-    BlockReader rd;
-    for (uint32_t j = 0; j < id_len; ++j)
-        if (rd.at(f[1] + j) == 0) {
-            id_len = j;
-            break;
+    uint32_t id_len = l[1];  // headers["origin_id"] = identifier.c_str(): up to the first NUL
+    {
+        BlockReader rd;
+        for (uint32_t j = 0; j < id_len;) {  // one SWAR test per 16-byte block
+            (void)rd.at(f[1] + j);
+            const uint32_t o = (uint32_t)((uintptr_t)(f[1] + j) & 15);
+            const uint32_t nul = (nul16(rd.v) >> o) & ((1u << (16 - o)) - 1);
+            if (nul) {
+                const uint32_t at = j + (uint32_t)__builtin_ctz(nul);
+                id_len = at < id_len ? at : id_len;
+                break;
+            }
+            j += 16 - o;
         }
+    }
     lit(s, "{\"message\":{\"headers\":{\"auth_token\":\"Bearer xxx\",\"connection_uuid\":\"130032\",\"create_ts\":\"");
     dec_i64(s, a.timestamp[i] / 1000000);
     lit(s, "\",\"customer_id\":\"");
