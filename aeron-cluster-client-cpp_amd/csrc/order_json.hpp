@@ -915,30 +915,21 @@ __device__ inline uint64_t wave_max(uint64_t v) {
     return v;
 }
 
+// The staging and storing half of the writing launch: every live lane knows its text's output
+// range [o, e) and its fields; the wave's texts go through the LDS window `win`.
 template <uint32_t kWhat>
-__global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+__device__ __forceinline__ void write_texts(const JsonArgs& a, lw8* win, uint32_t lane, uint64_t i, bool live,
+                                            uint64_t o, uint64_t e, gu8* const f[kFields], const uint32_t l[kFields]) {
     constexpr uint32_t kWin = WShape<kWhat>::kWinB;
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWin];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * WShape<kWhat>::kOpw + lane;
-    const bool live = lane < WShape<kWhat>::kOpw && i < a.n;
-    uint64_t o = 0, e = 0;
     bool done = true;
-    gu8* f[kFields];
-    uint32_t l[kFields];
     if (live) {
-        o = a.out_off[i];
-        e = a.out_off[i + 1];
         const bool fits = e <= a.cap;
         if (a.status) a.status[i] = fits ? SBE_JSON_OK : SBE_JSON_OVERFLOW;
         done = !fits;
-        if (fits) {
-            fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-            if (e - o > kWin - 16) {  // larger than any window: straight to HBM
-                HbmSink w((gw8*)(a.out + o));
-                order_text<kWhat>(w, a, i, f, l);
-                done = true;
-            }
+        if (fits && e - o > kWin - 16) {  // larger than any window: straight to HBM
+            HbmSink w((gw8*)(a.out + o));
+            order_text<kWhat>(w, a, i, f, l);
+            done = true;
         }
     }
     uint64_t start = ~0ull;  // output coordinate of the first record still to stage
@@ -955,7 +946,7 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         const uint64_t wbase = start - (uint64_t)((uintptr_t)(a.out + start) & 15);  // win[0] ≡ out + wbase (mod 16)
         uint64_t my_end = 0;
         if (!done && e - wbase <= kWin) {
-            LdsSink w((lw8*)(win + (o - wbase)), (uint32_t)(e - o));
+            LdsSink w(win + (o - wbase), (uint32_t)(e - o));
             order_text<kWhat>(w, a, i, f, l);
             done = true;
             my_end = e;
@@ -966,7 +957,9 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         for (uint64_t c = lane; c < nch; c += kWWave) {
             const uint64_t x0 = wbase + 16 * c;  // output coordinate of this 16-byte chunk
             if (x0 >= start && x0 + 16 <= cend) {
-                const uint4 v = *reinterpret_cast<const uint4*>(win + 16 * c);
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                typedef const __attribute__((address_space(3))) u32x4 lu128;
+                const u32x4 v = *(lu128*)(win + 16 * c);
                 __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(a.out + x0));
                 __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(a.out + x0) + 1);
                 __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(a.out + x0) + 2);
@@ -983,6 +976,23 @@ __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
         }
         start = nx;
     }
+}
+
+template <uint32_t kWhat>
+__global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[WShape<kWhat>::kWinB];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * WShape<kWhat>::kOpw + lane;
+    const bool live = lane < WShape<kWhat>::kOpw && i < a.n;
+    uint64_t o = 0, e = 0;
+    gu8* f[kFields];
+    uint32_t l[kFields];
+    if (live) {
+        o = a.out_off[i];
+        e = a.out_off[i + 1];
+        fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
+    }
+    write_texts<kWhat>(a, (lw8*)win, lane, i, live, o, e, f, l);
 }
 
 inline size_t scan_temp(uint64_t n) {

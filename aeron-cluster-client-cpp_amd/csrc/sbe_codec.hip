@@ -4567,10 +4567,10 @@ int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what
     w = al(w + 8 * (n + 1));
     void* tmp = reinterpret_cast<void*>(w);
     size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
+    hipError_t e = hipSuccess;
     oj::JsonArgs a{in->arena, in->str_off, in->str_len, in->customer_id, in->timestamp, in->quantity, n, what,
                    out,       out_capacity, out_off,    status,          sz,             tot,           base};
     const uint32_t blocks = (uint32_t)((n + 1 + oj::kBlock - 1) / oj::kBlock);
-    hipError_t e = hipSuccess;
     if (!in->str_off) {
         hipLaunchKernelGGL(oj::order_json_totals, dim3(blocks), dim3(oj::kBlock), 0, s, a);
         e = hipGetLastError();

@@ -166,3 +166,30 @@ def test_gpu_side_stream_regrow(codec):
     assert np.array_equal(off, exp_off)
     assert (r.status.cpu().numpy()[:n] == 0).all()
     assert r.out[: int(off[-1])].cpu().numpy().tobytes() == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", [0, 1])
+def test_gpu_window_edges(codec, what):
+    """Texts of every size class in one batch: most fit a tile's LDS window, some only a window of
+    their own (several passes), some exceed any window (written straight to HBM); with a capacity
+    that cuts the batch in the middle of a large text."""
+    n = 700
+    fields, cid, ts, q = T.order_batch(n, 31, True)
+    big = {0: b"\x01" * 3500, 6: b"\x01" * 3500}  # payload prints field 0 twice; headers print field 6
+    fields = [tuple((big[j] * (1 + (i % 3))) if (i % 37 == 5 and j in big) else
+                    ((b"\x02" * 600) if (i % 11 == 3 and j in big) else f) for j, f in enumerate(rec))
+              for i, rec in enumerate(fields)]
+    arena, str_len = T.pack_order_fields(fields)
+    exp, exp_off = T.oracle_order_json(arena, str_len, cid, ts, q, what, nthreads=8)
+    sizes = np.diff(exp_off.astype(np.int64))
+    assert sizes.max() > 20000 and (sizes > 3000).sum() > 20  # both size classes are present
+    for cap in (None, int(exp_off[400]) - 7):
+        out, off, st = gpu_json(codec, fields, cid, ts, q, what, out_capacity=cap)
+        assert np.array_equal(off, exp_off)
+        limit = int(off[-1]) if cap is None else cap
+        fits = exp_off[1:] <= limit
+        assert (st[fits] == 0).all() and (st[~fits] == 6).all()
+        for i in np.nonzero(fits)[0]:
+            a, b = int(off[i]), int(off[i + 1])
+            assert out[a:b].tobytes() == exp[a:b], i
