@@ -23,6 +23,7 @@ constexpr uint32_t kFields = SBE_ORDER_FIELDS;
 // make every byte access a flat instruction (which waits on both the LDS and the vector-memory
 // counters).  Strings are read from HBM (global), texts are written to LDS or HBM.
 typedef const __attribute__((address_space(1))) uint8_t gu8;
+typedef const __attribute__((address_space(3))) uint8_t lr8;  // strings staged in LDS (sizing launch)
 typedef __attribute__((address_space(1))) uint8_t gw8;
 typedef __attribute__((address_space(3))) uint8_t lw8;
 constexpr uint32_t kBlock = 256;
@@ -38,17 +39,28 @@ struct JsonArgs {
     uint32_t what;
     uint8_t* out;
     uint64_t cap;
-    uint64_t* out_off;  // n + 1 text offsets (scan of sz)
+    uint64_t* out_off;   // n + 1 text offsets
     uint8_t* status;
-    uint64_t* sz;       // n + 1 text lengths (sz[n] = 0)
-    uint64_t* str_tot;  // n + 1 packed-arena string totals (str_tot[n] = 0)
-    uint64_t* str_base; // n + 1 their scan
+    uint64_t* sz;        // n text lengths (sizing launch)
+    uint64_t* str_base;  // n packed-arena string bases (sizing launch)
+    uint64_t* blk_str;   // per block of kBlock Orders: packed-arena string bytes, then their exclusive scan
+    uint64_t* blk_txt;   // per block: text bytes, then their exclusive scan
 };
 
 // ---- byte sinks: counting (sizing launch) and writing (8-byte buffered, byte-exact edges) ----
+// Byte o of a 16-byte block and the block shifted down by o bytes, by 64-bit shifts: a select
+// chain over the four words is turned by the compiler into a private array (a scratch store and
+// a scratch load per byte).
 __device__ inline uint32_t block_byte(const uint4& v, uint32_t o) {
-    const uint32_t w = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);
-    return (w >> (8 * (o & 3))) & 0xFF;
+    const uint64_t h = (o & 8) ? ((uint64_t)v.w << 32 | v.z) : ((uint64_t)v.y << 32 | v.x);
+    return (uint32_t)(h >> (8 * (o & 7))) & 0xFF;
+}
+__device__ inline uint4 block_shift(const uint4& v, uint32_t o) {  // bytes [o, 16) of v, then zeros
+    const uint64_t lo = (uint64_t)v.y << 32 | v.x, hi = (uint64_t)v.w << 32 | v.z;
+    const uint32_t sh = 8 * (o & 7);
+    const uint64_t a = (o & 8) ? hi : lo, b = (o & 8) ? 0ull : hi;
+    const uint64_t rlo = sh ? (a >> sh) | (b << (64 - sh)) : a, rhi = b >> sh;
+    return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
 }
 
 // put(b) appends one byte; run(v, o, m) appends bytes [o, o + m) of the loaded 16-byte block v
@@ -73,16 +85,12 @@ struct LdsSink {
         if (n + 16 <= lim) {
             typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
             typedef __attribute__((address_space(3))) u32x4u lw128u;
-            const uint32_t j = o >> 2, sh = o & 3u;
-            const uint32_t w0 = j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
-            const uint32_t w1 = j == 0 ? v.y : j == 1 ? v.z : j == 2 ? v.w : 0u;
-            const uint32_t w2 = j == 0 ? v.z : j == 1 ? v.w : 0u;
-            const uint32_t w3 = j == 0 ? v.w : 0u;
+            const uint4 r = block_shift(v, o);
             u32x4u x;
-            x.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            x.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            x.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            x.w = __builtin_amdgcn_alignbyte(0u, w3, sh);
+            x.x = r.x;
+            x.y = r.y;
+            x.z = r.z;
+            x.w = r.w;
             *reinterpret_cast<lw128u*>(p + n) = x;
             n += m;
         } else {
@@ -140,23 +148,32 @@ __device__ inline uint32_t utf8_cp(uint32_t b, uint32_t b1, uint32_t b2, uint32_
 // Reads a string through aligned 16-byte loads, so a lane's walk over its string issues one
 // load per 16 bytes instead of one dependent load per byte.  A block holding a byte of the
 // string lies inside the allocation's page, so the over-read is harmless.
+template <class P>
+struct W32;  // the dword pointer of the same address space
+template <>
+struct W32<gu8*> {
+    typedef const __attribute__((address_space(1))) uint32_t* T;
+};
+template <>
+struct W32<lr8*> {
+    typedef const __attribute__((address_space(3))) uint32_t* T;
+};
+
+template <class P>  // P: gu8* (HBM) or lr8* (LDS)
 struct BlockReader {
     uintptr_t blk = ~(uintptr_t)0;
     uint4 v;
-    __device__ uint32_t at(gu8* p) {
+    __device__ uint32_t at(P p) {
         const uintptr_t a = (uintptr_t)p, b = a & ~(uintptr_t)15;
         if (b != blk) {
             blk = b;
-            typedef const __attribute__((address_space(1))) uint32_t gu32;
-            gu32* q = reinterpret_cast<gu32*>(b);
+            const typename W32<P>::T q = (typename W32<P>::T)b;
             v.x = q[0];
             v.y = q[1];
             v.z = q[2];
             v.w = q[3];
         }
-        const uint32_t o = (uint32_t)(a & 15);
-        const uint32_t w = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);
-        return (w >> (8 * (o & 3))) & 0xFF;
+        return block_byte(v, (uint32_t)(a & 15));
     }
 };
 
@@ -189,13 +206,22 @@ __device__ inline uint32_t nul16(const uint4& v) {  // bit k set iff byte k of t
     return nul4(v.x) | (nul4(v.y) << 4) | (nul4(v.z) << 8) | (nul4(v.w) << 12);
 }
 
+#ifndef SBE_OJ_INLINE  // A/B builds: 1 = the string and number helpers inlined into the kernels
+#define SBE_OJ_INLINE 0
+#endif
+#if SBE_OJ_INLINE
+#define OJ_HELPER __forceinline__
+#else
+#define OJ_HELPER __noinline__
+#endif
+
 // jsoncpp valueToQuotedStringN(str, len, emitUTF8 = false)
 // Out-of-line helpers take the sink by value and return it: a sink passed by reference lives in
 // scratch and every put would load and store its count.
-template <class S>
-__device__ __noinline__ S quoted(S s, gu8* p, uint64_t len) {
+template <class S, class P>
+__device__ OJ_HELPER S quoted(S s, P p, uint64_t len) {
     s.put('"');
-    BlockReader rd;
+    BlockReader<P> rd;
     uint64_t i = 0;
     while (i < len) {
         {  // the common case: a run of plain bytes inside the current 16-byte block, found with
@@ -540,7 +566,7 @@ __device__ __noinline__ S fmt_g17_slow(S s, double v);
 // "%f" (std::to_string(double), src/order_types.cpp:164): all integer digits, six decimals,
 // round half to even on the exact value; inf / nan as glibc prints them.
 template <class S>
-__device__ __noinline__ S fmt_fixed6(S s, double v) {
+__device__ OJ_HELPER S fmt_fixed6(S s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     const bool neg = (bits >> 63) != 0;
     if (__builtin_isnan(v)) {
@@ -613,7 +639,7 @@ __device__ __noinline__ S fmt_fixed6_slow(S s, double v) {  // |v| outside the r
 // jsoncpp valueToString(double, false, 17, significantDigits): "%.17g" then ".0" when the text
 // has neither '.' nor 'e'; NaN → null, ±inf → ±1e+9999.
 template <class S>
-__device__ __noinline__ S fmt_g17(S s, double v) {
+__device__ OJ_HELPER S fmt_g17(S s, double v) {
     const uint64_t bits = (uint64_t)__double_as_longlong(v);
     if (__builtin_isnan(v)) {
         lit(s, "null");
@@ -776,8 +802,9 @@ __device__ __noinline__ S fmt_g17_slow(S s, double v) {  // |v| outside the regi
     return s;
 }
 
-__device__ inline bool eq_lit(gu8* p, uint64_t n, const char* t) {
-    BlockReader rd;
+template <class P>
+__device__ inline bool eq_lit(P p, uint64_t n, const char* t) {
+    BlockReader<P> rd;
     uint64_t i = 0;
     for (; t[i]; ++i)
         if (i >= n || rd.at(p + i) != (uint8_t)t[i]) return false;
@@ -785,8 +812,8 @@ __device__ inline bool eq_lit(gu8* p, uint64_t n, const char* t) {
 }
 
 // One Order's text (src/order_types.cpp:122-181, src/cluster_client.cpp:308-323).
-template <uint32_t kWhat, class S>
-__device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFields],
+template <uint32_t kWhat, class S, class P>
+__device__ __forceinline__ void order_text(S& s, const JsonArgs& a, uint64_t i, P const f[kFields],
                            const uint32_t l[kFields]) {
     if (kWhat == SBE_JSON_PUBLISH_HEADERS) {
         const bool upd = eq_lit(f[7], l[7], "UPDATED") || eq_lit(f[7], l[7], "CANCELLED");
@@ -801,7 +828,7 @@ __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFi
     const double q = a.quantity[i];
     uint32_t id_len = l[1];  // headers["origin_id"] = identifier.c_str(): up to the first NUL
     {
-        BlockReader rd;
+        BlockReader<P> rd;
         for (uint32_t j = 0; j < id_len;) {  // one SWAR test per 16-byte block
             (void)rd.at(f[1] + j);
             const uint32_t o = (uint32_t)((uintptr_t)(f[1] + j) & 15);
@@ -839,44 +866,156 @@ __device__ void order_text(S& s, const JsonArgs& a, uint64_t i, gu8* const f[kFi
     s.put('}');
 }
 
-__device__ inline void fields_of(const JsonArgs& a, uint64_t i, uint64_t base, gu8* f[kFields],
-                                 uint32_t l[kFields]) {
-    for (uint32_t j = 0; j < kFields; ++j) {
-        l[j] = a.str_len[kFields * i + j];
-        if (a.str_off) {
-            f[j] = (gu8*)(a.arena + a.str_off[kFields * i + j]);
-        } else {
-            f[j] = (gu8*)(a.arena + base);
-            base += l[j];
-        }
+
+// ---- offsets without a device-wide scan library call ----
+// Orders are taken in blocks of kBlock: a block's string bytes (packed arena) and text bytes are
+// summed per block, the block sums scanned by one small launch, and each Order's offset is its
+// block's prefix plus a scan inside the block (sizing launch: string bases; writing launch: text
+// offsets, from the sizes of the block's earlier Orders).
+
+// exclusive scan of v over the block (every thread calls it); total = the block's sum
+__device__ inline uint64_t block_excl_scan(uint64_t v, uint64_t* wtot, uint32_t lane, uint32_t wv, uint64_t& total) {
+    const uint64_t incl = wave_incl_scan64(v, (int)lane);
+    if (lane == kWave - 1) wtot[wv] = incl;
+    __syncthreads();
+    uint64_t before = 0;
+    total = 0;
+    for (uint32_t w = 0; w < kBlock / kWave; ++w) {
+        const uint64_t t = wtot[w];
+        before += w < wv ? t : 0;
+        total += t;
     }
+    __syncthreads();
+    return before + incl - v;
 }
 
-// Packed arena: each record's string total (scan → its base).
+// Packed arena: each block's string bytes into blk_str.
 __global__ __launch_bounds__(kBlock) void order_json_totals(JsonArgs a) {
+    __shared__ uint64_t wtot[kBlock / kWave];
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i > a.n) return;
     uint64_t t = 0;
     if (i < a.n)
         for (uint32_t j = 0; j < kFields; ++j) t += a.str_len[kFields * i + j];
-    a.str_tot[i] = t;
+    uint64_t total;
+    (void)block_excl_scan(t, wtot, threadIdx.x % kWave, threadIdx.x / kWave, total);
+    if (threadIdx.x == 0) a.blk_str[blockIdx.x] = total;
 }
 
-// Sizing launch: the text length of record i into sz[i] (sz[n] = 0).
+// Exclusive scan of v[0, m) in place: one block of 1024 threads, 4096 values per step.
+constexpr uint32_t kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void order_json_scan_blocks(uint64_t* v, uint64_t m) {
+    __shared__ uint64_t wt[kScanThreads / kWave];
+    const uint32_t lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < m; c0 += 4 * kScanThreads) {
+        const uint64_t k0 = c0 + 4 * (uint64_t)threadIdx.x;
+        uint64_t x[4], sum = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            x[r] = k0 + r < m ? v[k0 + r] : 0;
+            sum += x[r];
+        }
+        const uint64_t incl = wave_incl_scan64(sum, (int)lane);
+        if (lane == kWave - 1) wt[wv] = incl;
+        __syncthreads();
+        uint64_t before = carry, tot = 0;
+        for (uint32_t w = 0; w < kScanThreads / kWave; ++w) {
+            const uint64_t t = wt[w];
+            before += w < wv ? t : 0;
+            tot += t;
+        }
+        __syncthreads();
+        uint64_t run = before + incl - sum;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (k0 + r < m) v[k0 + r] = run;
+            run += x[r];
+        }
+        carry += tot;
+    }
+}
+
+// Sizing launch: the text length of record i into sz[i], the block's text bytes into blk_txt
+// (and, packed arena, the string base of record i into str_base[i]).  With a packed arena the
+// strings of a wave's 64 Orders are one contiguous range: the wave copies it into LDS with
+// coalesced 16-byte loads issued back to back, and sizes the texts from there, instead of each
+// lane walking its strings with a chain of dependent HBM loads (the launch's latency bound).  A
+// range larger than the wave's LDS share is read from HBM as before.
+#ifndef SBE_OJ_MSTR  // LDS bytes per wave for the staged strings (0: never staged)
+#define SBE_OJ_MSTR 10240
+#endif
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
+    __shared__ uint64_t wtot[kBlock / kWave];
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i > a.n) return;
-    if (i == a.n) {
-        a.sz[i] = 0;
-        return;
-    }
-    gu8* f[kFields];
+    const bool live = i < a.n;
+    const uint32_t lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
     uint32_t l[kFields];
-    fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
-    CountSink c;
-    order_text<kWhat>(c, a, i, f, l);
-    a.sz[i] = c.n;
+    uint64_t tot = 0;
+    if (live)
+        for (uint32_t j = 0; j < kFields; ++j) {
+            l[j] = a.str_len[kFields * i + j];
+            tot += l[j];
+        }
+    uint64_t len = 0, total;
+    bool done = false;
+    if (!a.str_off) {  // uniform over the launch
+        const uint64_t base = a.blk_str[blockIdx.x] + block_excl_scan(tot, wtot, lane, wv, total);
+        if (live) a.str_base[i] = base;
+#if SBE_OJ_MSTR > 0
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        __shared__ __attribute__((aligned(16))) uint8_t sbuf[kBlock / kWave][SBE_OJ_MSTR];
+        const uint64_t i0 = i - lane;
+        bool staged = false;
+        uint64_t g0 = 0;
+        if (i0 < a.n) {  // uniform per wave
+            g0 = lane_u64(base, 0) & ~15ull;
+            const uint64_t last = a.n - 1 - i0 < kWave - 1 ? a.n - 1 - i0 : kWave - 1;
+            const uint64_t end = lane_u64(base + tot, (int)last);
+            staged = end - g0 <= SBE_OJ_MSTR;
+            if (staged) {
+                typedef const __attribute__((address_space(1))) u32x4 g128;
+                typedef __attribute__((address_space(3))) u32x4 l128;
+                const uint64_t nb = (end - g0 + 15) / 16;
+                for (uint64_t c = lane; c < nb; c += kWave)
+                    *(l128*)(sbuf[wv] + 16 * c) = *(g128*)(a.arena + g0 + 16 * c);
+            }
+        }
+        __syncthreads();
+        if (staged && live) {
+            lr8* f[kFields];
+            uint64_t at = base - g0;
+            for (uint32_t j = 0; j < kFields; ++j) {
+                f[j] = (lr8*)(sbuf[wv] + at);
+                at += l[j];
+            }
+            CountSink c;
+            order_text<kWhat>(c, a, i, f, l);
+            len = c.n;
+        }
+        done = staged;
+#endif
+        if (!done && live) {
+            gu8* f[kFields];
+            uint64_t at = base;
+            for (uint32_t j = 0; j < kFields; ++j) {
+                f[j] = (gu8*)(a.arena + at);
+                at += l[j];
+            }
+            CountSink c;
+            order_text<kWhat>(c, a, i, f, l);
+            len = c.n;
+        }
+    } else if (live) {
+        gu8* f[kFields];
+        for (uint32_t j = 0; j < kFields; ++j) f[j] = (gu8*)(a.arena + a.str_off[kFields * i + j]);
+        CountSink c;
+        order_text<kWhat>(c, a, i, f, l);
+        len = c.n;
+    }
+    if (live) a.sz[i] = len;
+    (void)block_excl_scan(len, wtot, lane, wv, total);
+    if (threadIdx.x == 0) a.blk_txt[blockIdx.x] = total;
 }
 
 // Writing launch: one wave per kOpw Orders (WShape).  Their texts are contiguous in `out`: the
@@ -917,9 +1056,9 @@ __device__ inline uint64_t wave_max(uint64_t v) {
 
 // The staging and storing half of the writing launch: every live lane knows its text's output
 // range [o, e) and its fields; the wave's texts go through the LDS window `win`.
-template <uint32_t kWhat>
+template <uint32_t kWhat, class P>
 __device__ __forceinline__ void write_texts(const JsonArgs& a, lw8* win, uint32_t lane, uint64_t i, bool live,
-                                            uint64_t o, uint64_t e, gu8* const f[kFields], const uint32_t l[kFields]) {
+                                            uint64_t o, uint64_t e, P const f[kFields], const uint32_t l[kFields]) {
     constexpr uint32_t kWin = WShape<kWhat>::kWinB;
     bool done = true;
     if (live) {
@@ -980,25 +1119,44 @@ __device__ __forceinline__ void write_texts(const JsonArgs& a, lw8* win, uint32_
 
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+    constexpr uint32_t kOpw = WShape<kWhat>::kOpw;
+    static_assert(kBlock % kOpw == 0, "a writing tile lies inside one sizing block");
     __shared__ __attribute__((aligned(16))) uint8_t win[WShape<kWhat>::kWinB];
     const uint32_t lane = threadIdx.x;
-    const uint64_t i = (uint64_t)blockIdx.x * WShape<kWhat>::kOpw + lane;
-    const bool live = lane < WShape<kWhat>::kOpw && i < a.n;
-    uint64_t o = 0, e = 0;
-    gu8* f[kFields];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kOpw, i = i0 + lane;
+    const bool live = lane < kOpw && i < a.n;
+    // text offsets: the block's prefix, the sizes of the block's Orders before the tile, the tile's scan
+    const uint64_t bs = i0 / kBlock * kBlock;
+    uint64_t pre = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kBlock / kWave; ++r) {
+        const uint64_t k = bs + lane + kWave * r;
+        if (k < i0) pre += a.sz[k];
+    }
+    pre = a.blk_txt[i0 / kBlock] + wave_sum64(pre);
+    const uint64_t len = live ? a.sz[i] : 0;
+    const uint64_t o = pre + wave_incl_scan64(len, (int)lane) - len, e = o + len;
     uint32_t l[kFields];
     if (live) {
-        o = a.out_off[i];
-        e = a.out_off[i + 1];
-        fields_of(a, i, a.str_off ? 0 : a.str_base[i], f, l);
+        a.out_off[i] = o;
+        if (i + 1 == a.n) a.out_off[a.n] = e;
+        for (uint32_t j = 0; j < kFields; ++j) l[j] = a.str_len[kFields * i + j];
+    }
+    gu8* f[kFields];
+    if (live) {
+        uint64_t at = a.str_off ? 0 : a.str_base[i];
+        for (uint32_t j = 0; j < kFields; ++j) {
+            if (a.str_off) {
+                f[j] = (gu8*)(a.arena + a.str_off[kFields * i + j]);
+            } else {
+                f[j] = (gu8*)(a.arena + at);
+                at += l[j];
+            }
+        }
     }
     write_texts<kWhat>(a, (lw8*)win, lane, i, live, o, e, f, l);
 }
 
-inline size_t scan_temp(uint64_t n) {
-    size_t t = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (uint64_t*)nullptr, (uint64_t*)nullptr, n + 1, nullptr);
-    return t + 256;
-}
+
 
 }  // namespace oj

@@ -4543,7 +4543,9 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
 }
 
 size_t sbe_order_json_workspace_size(uint64_t n) {
-    return (size_t)(3 * 8 * (n + 1) + 4 * 16) + oj::scan_temp(n);
+    // text sizes and string bases (n each), two block-sum arrays, alignment
+    const uint64_t nblk = (n + oj::kBlock - 1) / oj::kBlock;
+    return (size_t)(16 * n + 16 * nblk + 4 * 16);
 }
 
 int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what, uint8_t* out,
@@ -4557,40 +4559,36 @@ int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what
     if (n >= (1ull << 40)) return SBE_EINVAL;
     if (workspace_bytes < sbe_order_json_workspace_size(n)) return SBE_ENOSPC;
     if (!out && out_capacity) return SBE_EINVAL;
+    const uint64_t nblk = (n + oj::kBlock - 1) / oj::kBlock;
     auto al = [](uintptr_t x) { return (x + 15) & ~(uintptr_t)15; };
     uintptr_t w = al(reinterpret_cast<uintptr_t>(workspace));
     uint64_t* sz = reinterpret_cast<uint64_t*>(w);
-    w = al(w + 8 * (n + 1));
-    uint64_t* tot = reinterpret_cast<uint64_t*>(w);
-    w = al(w + 8 * (n + 1));
+    w = al(w + 8 * n);
     uint64_t* base = reinterpret_cast<uint64_t*>(w);
-    w = al(w + 8 * (n + 1));
-    void* tmp = reinterpret_cast<void*>(w);
-    size_t tmp_bytes = reinterpret_cast<uintptr_t>(workspace) + workspace_bytes - w;
-    hipError_t e = hipSuccess;
+    w = al(w + 8 * n);
+    uint64_t* blk_str = reinterpret_cast<uint64_t*>(w);
+    w = al(w + 8 * nblk);
+    uint64_t* blk_txt = reinterpret_cast<uint64_t*>(w);
     oj::JsonArgs a{in->arena, in->str_off, in->str_len, in->customer_id, in->timestamp, in->quantity, n, what,
-                   out,       out_capacity, out_off,    status,          sz,             tot,           base};
-    const uint32_t blocks = (uint32_t)((n + 1 + oj::kBlock - 1) / oj::kBlock);
+                   out,       out_capacity, out_off,  status,  sz,  base,  blk_str,  blk_txt};
+    // sizing (per-block sums), one small scan of the block sums per chain, writing
+    const uint32_t blocks = (uint32_t)nblk;
     if (!in->str_off) {
         hipLaunchKernelGGL(oj::order_json_totals, dim3(blocks), dim3(oj::kBlock), 0, s, a);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, tot, base, n + 1, s);
-        if (e != hipSuccess) return record_hip(e);
+        hipLaunchKernelGGL(oj::order_json_scan_blocks, dim3(1), dim3(oj::kScanThreads), 0, s, blk_str, nblk);
     }
     if (what == SBE_JSON_PUBLISH_HEADERS)
         hipLaunchKernelGGL(oj::order_json_measure<SBE_JSON_PUBLISH_HEADERS>, dim3(blocks), dim3(oj::kBlock), 0, s, a);
     else
         hipLaunchKernelGGL(oj::order_json_measure<SBE_JSON_ORDER_PAYLOAD>, dim3(blocks), dim3(oj::kBlock), 0, s, a);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, sz, out_off, n + 1, s);
-    if (e != hipSuccess) return record_hip(e);
+    hipLaunchKernelGGL(oj::order_json_scan_blocks, dim3(1), dim3(oj::kScanThreads), 0, s, blk_txt, nblk);
     if (what == SBE_JSON_PUBLISH_HEADERS) {
-        constexpr uint64_t w = oj::WShape<SBE_JSON_PUBLISH_HEADERS>::kOpw;
-        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_PUBLISH_HEADERS>, dim3((uint32_t)((n + w - 1) / w)),
+        constexpr uint64_t t = oj::WShape<SBE_JSON_PUBLISH_HEADERS>::kOpw;
+        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_PUBLISH_HEADERS>, dim3((uint32_t)((n + t - 1) / t)),
                            dim3(oj::kWWave), 0, s, a);
     } else {
-        constexpr uint64_t w = oj::WShape<SBE_JSON_ORDER_PAYLOAD>::kOpw;
-        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_ORDER_PAYLOAD>, dim3((uint32_t)((n + w - 1) / w)),
+        constexpr uint64_t t = oj::WShape<SBE_JSON_ORDER_PAYLOAD>::kOpw;
+        hipLaunchKernelGGL(oj::order_json_write<SBE_JSON_ORDER_PAYLOAD>, dim3((uint32_t)((n + t - 1) / t)),
                            dim3(oj::kWWave), 0, s, a);
     }
     return record_hip(hipGetLastError());

@@ -345,8 +345,9 @@ size_t sbe_order_json_workspace_size(uint64_t n);
 
 /* Write the JSON text of n Orders back to back: record i = out[out_off[i] .. out_off[i+1]).
  * out_off (n + 1 device u64) always holds the full sizes; a record past out_capacity is not
- * written and gets status SBE_JSON_OVERFLOW (status: n device u8 or NULL).  Two launches and a
- * device scan on `stream`. */
+ * written and gets status SBE_JSON_OVERFLOW (status: n device u8 or NULL).  On `stream`: a
+ * sizing launch, a one-block scan of its per-block sums and the writing launch (packed arena:
+ * first a per-block string-bytes launch and its scan). */
 int sbe_order_to_json_batch(const sbe_order_batch* in, uint64_t n, uint32_t what, uint8_t* out,
                             uint64_t out_capacity, uint64_t* out_off, uint8_t* status, void* workspace,
                             size_t workspace_bytes, void* stream);
