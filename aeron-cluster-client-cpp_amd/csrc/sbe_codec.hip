@@ -2849,7 +2849,11 @@ __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint6
         if (ch < nch) lds_write_chunk(win, ch, I[k]);
     }
     uint32_t sm = 0;
+#ifdef SBE_ABL_NOCLASS  // ablation builds only (wrong flags on payloads with a key or a backslash)
+    if (false) {
+#else
     if (kMode == SBE_DEC_PARSE_MESSAGE && wide) {
+#endif
         // rows of chunks past the window are skipped (a tile's later window is often part full);
         // zero chunks of the last row are never suspect
         const uint32_t nrow = (nch + kWave - 1) / kWave;
