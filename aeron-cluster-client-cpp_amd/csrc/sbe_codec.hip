@@ -2940,6 +2940,82 @@ __device__ uint64_t g_serve_prof[16];
 #else
 #define SBE_SVP(k, t) do { } while (0)
 #endif
+// The windows after a tile's first one (which is parsed): the second window's loads go out first
+// when its start is known; then windows from the first record still to parse; records no window
+// can hold are parsed from HBM.  I: free staging registers.
+template <uint32_t kMode, uint32_t kWin>
+__device__ __forceinline__ void dec_rest(const DecArgs& a, uint32_t* win, uint64_t T0, uint64_t end, uint64_t rs,
+                                         uint64_t rl, bool wide, bool& done, Desc& d, int lane,
+                                         uint4 (&I)[dec_regs<kWin>()]) {
+    for (;;) {
+        bool again = false;
+        uint64_t wb = 0;
+        for (;;) {
+            const uint64_t m = __ballot(!done);
+            if (m == 0) break;
+            const int f = __builtin_ctzll(m);
+            const uint64_t rsf = uniform64(__shfl(rs, f, kWave));
+            const uint64_t rlf = uniform64(__shfl(rl, f, kWave));
+            if ((rsf & 15) + rlf <= kWin && rsf + rlf <= end && rsf >= (T0 & ~15ull)) {
+                wb = rsf & ~15ull;
+                again = true;
+                break;
+            }
+            if (lane == f) {
+                d = dec_record_glb<kMode>(a.in, rs, (uint32_t)rl);
+                done = true;
+            }
+        }
+        if (!again) break;
+        const uint64_t we = wb + kWin < end ? wb + kWin : end;
+        wsync();
+        dec_issue<kWin>(a, wb, we, lane, I);
+        const uint32_t sm = dec_commit<kMode, kWin>(win, wb, we, wide, lane, I);
+        wsync();
+        dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
+    }
+}
+
+// The descriptor SoA of record r, and ParseResult.sequence_number of flagged TopicMessages (rare:
+// payloads with the key or a backslash), evaluated from HBM by the lanes that hold one.
+template <uint32_t kMode, bool kServe>
+__device__ __forceinline__ void dec_outputs(const DecArgs& a, uint64_t r, bool valid, uint64_t rs, const Desc& d) {
+    if (valid) {
+        dst_store(a.status + r, (uint8_t)d.status);
+        dst_store(a.flags + r, (uint8_t)d.flags);
+        dst_store(reinterpret_cast<uint64_t*>(a.hdr + 4 * r),
+                  (uint64_t)((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16)) |
+                      ((uint64_t)((uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16)) << 32));
+        dst_store(a.ts + r, d.ts);
+    }
+    // views [n][5]: each lane stores its record's 20 contiguous bytes per array (a dwordx4 and a
+    // dword; the wave's stores cover 1280 contiguous bytes), no LDS transpose
+    if (valid) {
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        u32x4a4 o4, l4;
+        o4.x = d.off[0]; o4.y = d.off[1]; o4.z = d.off[2]; o4.w = d.off[3];
+        l4.x = d.len[0]; l4.y = d.len[1]; l4.z = d.len[2]; l4.w = d.len[3];
+        __builtin_nontemporal_store(o4, reinterpret_cast<u32x4a4*>(a.view_off + 5 * r));
+        __builtin_nontemporal_store(d.off[4], a.view_off + 5 * r + 4);
+        __builtin_nontemporal_store(l4, reinterpret_cast<u32x4a4*>(a.view_len + 5 * r));
+        __builtin_nontemporal_store(d.len[4], a.view_len + 5 * r + 4);
+    }
+    if (kMode == SBE_DEC_PARSE_MESSAGE && a.seq) {
+        const bool cand = valid && d.status == SBE_ST_TM && (d.flags & kSeqCand);
+        if (__ballot(cand) && cand)
+            a.seq[r] = kServe ? json_seq_eval_call_serve(a.in + rs + d.off[3], d.len[3])
+                              : json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
+    }
+}
+
+// A record beyond 32-bit sizes is not an SBE frame we bound-check
+template <uint32_t kMode>
+__device__ __forceinline__ void dec_oversize(Desc& d) {
+    d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE
+             : kMode == SBE_DEC_LITE    ? SBE_ST_LITE_E100
+                                        : SBE_ST_ERR_TM_E100;
+}
+
 template <uint32_t kMode, uint32_t kWin, bool kServe = false>
 __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32_t* win) {
 #ifdef SBE_SERVE_PROF
@@ -2960,10 +3036,8 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
     Desc d;
     d.clear();
     bool done = !valid;
-    if (valid && rl > 0xffffffffull) {  // beyond 32-bit record sizes: not an SBE frame we bound-check
-        d.status = kMode == SBE_DEC_ON_EGRESS ? SBE_ST_EG_NONE
-                 : kMode == SBE_DEC_LITE    ? SBE_ST_LITE_E100
-                                            : SBE_ST_ERR_TM_E100;
+    if (valid && rl > 0xffffffffull) {
+        dec_oversize<kMode>(d);
         done = true;
     }
     // first window: the whole tile when its records are at most 256 B on average
@@ -3005,66 +3079,10 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
         wsync();
         dec_window<kMode>(win, wb2, we2, rs, rl, wide, sm, done, d, lane);
     }
-    if (__ballot(!done)) {
-        // later windows start at the first record still to parse; records no window can hold are
-        // parsed from HBM
-#pragma nounroll
-        for (;;) {
-            bool again = false;
-            for (;;) {
-                const uint64_t m = __ballot(!done);
-                if (m == 0) break;
-                const int f = __builtin_ctzll(m);
-                const uint64_t rsf = uniform64(__shfl(rs, f, kWave));
-                const uint64_t rlf = uniform64(__shfl(rl, f, kWave));
-                if ((rsf & 15) + rlf <= kWin && rsf + rlf <= end && rsf >= (T0 & ~15ull)) {
-                    wb = rsf & ~15ull;
-                    again = true;
-                    break;
-                }
-                if (lane == f) {
-                    d = dec_record_glb<kMode>(a.in, rs, (uint32_t)rl);
-                    done = true;
-                }
-            }
-            if (!again) break;
-            we = wb + kWin < end ? wb + kWin : end;
-            wsync();
-            sm = dec_stage<kMode, kWin>(a, win, wb, we, wide, lane);
-            wsync();
-            dec_window<kMode>(win, wb, we, rs, rl, wide, sm, done, d, lane);
-        }
-    }
+    if (__ballot(!done)) dec_rest<kMode, kWin>(a, win, T0, end, rs, rl, wide, done, d, lane, I);
     SBE_SVP(7, tp0);  // parsed
-    if (valid) {
-        dst_store(a.status + r, (uint8_t)d.status);
-        dst_store(a.flags + r, (uint8_t)d.flags);
-        dst_store(reinterpret_cast<uint64_t*>(a.hdr + 4 * r),
-                  (uint64_t)((uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16)) |
-                      ((uint64_t)((uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16)) << 32));
-        dst_store(a.ts + r, d.ts);
-    }
-    // views [n][5]: each lane stores its record's 20 contiguous bytes per array (a dwordx4 and a
-    // dword; the wave's stores cover 1280 contiguous bytes), no LDS transpose
-    if (valid) {
-        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-        u32x4a4 o4, l4;
-        o4.x = d.off[0]; o4.y = d.off[1]; o4.z = d.off[2]; o4.w = d.off[3];
-        l4.x = d.len[0]; l4.y = d.len[1]; l4.z = d.len[2]; l4.w = d.len[3];
-        __builtin_nontemporal_store(o4, reinterpret_cast<u32x4a4*>(a.view_off + 5 * r));
-        __builtin_nontemporal_store(d.off[4], a.view_off + 5 * r + 4);
-        __builtin_nontemporal_store(l4, reinterpret_cast<u32x4a4*>(a.view_len + 5 * r));
-        __builtin_nontemporal_store(d.len[4], a.view_len + 5 * r + 4);
-    }
-    // ParseResult.sequence_number of flagged TopicMessages (rare: payloads with the key or a
-    // backslash), evaluated from HBM by the lanes that hold one
+    dec_outputs<kMode, kServe>(a, r, valid, rs, d);
     SBE_SVP(8, tp0);  // descriptor stores issued
-    if (kMode == SBE_DEC_PARSE_MESSAGE && a.seq) {
-        const bool cand = valid && d.status == SBE_ST_TM && (d.flags & kSeqCand);
-        if (__ballot(cand) && cand)
-            a.seq[r] = kServe ? json_seq_eval_call_serve(a.in + rs + d.off[3], d.len[3])
-                              : json_seq_eval_call(a.in + rs + d.off[3], d.len[3]);
-    }
 #ifdef SBE_SERVE_PROF
     if (kServe && lane == 0)
         for (int k = 0; k < 4; ++k) g_serve_prof[5 + k] += tpk[k] - tp0;
@@ -3097,7 +3115,7 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
         int dev;
         uint64_t g;
     };
-    static thread_local Entry cache[8] = {};
+    static thread_local Entry cache[32] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     uint64_t g = 0;
