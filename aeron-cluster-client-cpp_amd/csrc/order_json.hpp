@@ -1099,10 +1099,8 @@ __device__ __forceinline__ void write_texts(const JsonArgs& a, lw8* win, uint32_
                 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                 typedef const __attribute__((address_space(3))) u32x4 lu128;
                 const u32x4 v = *(lu128*)(win + 16 * c);
-                __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t*>(a.out + x0));
-                __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t*>(a.out + x0) + 1);
-                __builtin_nontemporal_store(v.z, reinterpret_cast<uint32_t*>(a.out + x0) + 2);
-                __builtin_nontemporal_store(v.w, reinterpret_cast<uint32_t*>(a.out + x0) + 3);
+                // out + x0 is 16-byte aligned (wbase's choice): one dwordx4 store a chunk
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.out + x0));
             } else {
                 for (uint64_t x = x0 < start ? start : x0; x < x0 + 16 && x < cend; ++x) a.out[x] = win[x - wbase];
             }
