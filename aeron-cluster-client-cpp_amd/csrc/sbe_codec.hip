@@ -3415,6 +3415,86 @@ __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
     }
 }
 
+// frag_scan and frag_messages in one launch (the default): the block's inclusive scan stays in
+// registers (and the singles counts in LDS) instead of a 32-B element per fragment written to HBM
+// and read back.  A group that starts before the block finds the singles before its start from
+// the block's exclusive prefix minus the singles between its start and the block (few fragments:
+// groups are short).
+#ifndef SBE_FRAG_FUSED  // A/B builds: 0 = frag_scan + frag_messages
+#define SBE_FRAG_FUSED 1
+#endif
+__global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const FragScan* pre) {
+    __shared__ FragScan wt[kFsThreads / kWave];
+    __shared__ uint32_t sgl[kFsBlk];  // inclusive singles count at every fragment of the block
+    const uint64_t b = blockIdx.x;
+    FragScan e[kFsPer], before;
+    (void)fs_block(a, b, e, wt, before);
+    const FragScan P = pre[b];  // the scan at the fragment before the block
+    const FragScan base = FragScanOp{}(P, before);
+    const int tid = threadIdx.x;
+    const uint64_t blk0 = b * kFsBlk, i0 = blk0 + (uint64_t)tid * kFsPer;
+    FragScan v[kFsPer];
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k) {
+        v[k] = FragScanOp{}(base, e[k]);
+        sgl[tid * kFsPer + k] = fs_sg(v[k]);
+    }
+    __syncthreads();
+    auto sg_at = [&](uint64_t x) -> uint32_t {  // singles among fragments [0, x]
+        if (x >= blk0) return sgl[x - blk0];
+        uint32_t c = fs_sg(P);
+        for (uint64_t y = x + 1; y < blk0; ++y) c -= frag_single(a.flags[y]) ? 1u : 0u;
+        return c;
+    };
+    auto group = [&](const FragScan& x, int64_t le_before, uint64_t& s0, bool& gap) {  // frag_group
+        int64_t st = (int64_t)x.lb > le_before + 1 ? (int64_t)x.lb : le_before + 1;
+        if (st < 0) st = 0;
+        s0 = (uint64_t)st;
+        const uint32_t sg0 = s0 ? sg_at(s0 - 1) : 0u;
+        gap = fs_sg(x) != sg0;
+    };
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k) {
+        const uint64_t i = i0 + k;
+        if (i >= a.n) break;
+        const FragScan& x = v[k];
+        const FragScan& prev = k ? v[k - 1] : base;  // the scan at fragment i - 1 (identity before 0)
+        const uint8_t f = a.flags[i];
+        const uint64_t E0 = i ? prev.E : 0ull;
+        const bool single = frag_single(f);
+        const uint32_t dp = fs_dp(x);
+        if ((single || (f & SBE_FRAG_END)) && dp >= 1 && dp <= a.n) {
+            const uint64_t j = dp - 1;
+            a.msize[j] = x.E - E0;
+            a.msg_off[j] = E0;
+            if (single) {
+                a.mfirst[j] = i;
+                a.mlast[j] = i;
+            } else {
+                uint64_t s0;
+                bool gap;
+                group(x, i ? (int64_t)prev.le : -1, s0, gap);
+                a.mfirst[j] = s0;
+                a.mlast[j] = i | (gap ? (1ull << 63) : 0ull);
+            }
+        }
+        if (i == a.n - 1) {  // the open accumulator after the last fragment: the carry
+            const uint64_t m = dp <= a.n ? dp : a.n;
+            uint64_t s0;
+            bool gap;
+            group(x, x.le, s0, gap);
+            const uint64_t bytes = x.B;
+            const bool open = (int64_t)s0 <= (int64_t)i && bytes > 0;
+            a.msize[m] = open ? bytes : 0u;
+            a.msg_off[m] = x.E;
+            a.mfirst[m] = s0;
+            a.mlast[m] = i | (gap ? (1ull << 63) : 0ull);
+            a.counts[0] = m;
+            a.counts[1] = open ? bytes : 0u;
+        }
+    }
+}
+
 // the 16 bytes at src + 16c + sh from the aligned blocks b0 (at 16c) and b1 (the next one)
 __device__ __forceinline__ uint4 join16(uint4 b0, uint4 b1, uint32_t sh) {
     const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -4550,12 +4630,19 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     const uint64_t nb = (n + kFsBlk - 1) / kFsBlk;
     hipLaunchKernelGGL(frag_reduce, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, el);
     hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsbThreads), 0, s, el, nb);
-    hipLaunchKernelGGL(frag_scan, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return record_hip(e);
-    hipLaunchKernelGGL(frag_messages, dim3(blocks), dim3(256), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return record_hip(e);
+    hipError_t e = hipSuccess;
+    if (SBE_FRAG_FUSED) {
+        hipLaunchKernelGGL(frag_scan_msgs, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
+        e = hipGetLastError();
+        if (e != hipSuccess) return record_hip(e);
+    } else {
+        hipLaunchKernelGGL(frag_scan, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
+        e = hipGetLastError();
+        if (e != hipSuccess) return record_hip(e);
+        hipLaunchKernelGGL(frag_messages, dim3(blocks), dim3(256), 0, s, a);
+        e = hipGetLastError();
+        if (e != hipSuccess) return record_hip(e);
+    }
     const uint64_t cb = (n + 1 + 4 * kFragGroup - 1) / (4 * kFragGroup);  // four waves per block
 #ifndef SBE_FC_MAXB  // A/B builds: the copy's grid cap (blocks of four waves; they loop over the groups)
 #define SBE_FC_MAXB 4096

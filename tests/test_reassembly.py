@@ -107,6 +107,37 @@ def test_gpu_in_order_streams(codec, n, seed, cut):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["one_long", "many_long", "cross_every_block"])
+def test_gpu_long_groups(codec, layout):
+    """Groups that span the scan's 1024-fragment blocks: one BEGIN..END group over several blocks
+    with whole messages inside it (the group's start is blocks behind its END), many such groups,
+    and short groups placed across every block boundary."""
+    rng = np.random.default_rng({"one_long": 31, "many_long": 32, "cross_every_block": 33}[layout])
+    if layout == "cross_every_block":
+        n = 20 * 1024
+        flags = np.full(n, 0xC0, np.uint8)
+        for b in range(1024, n, 1024):  # BEGIN 2 before the boundary, middle(s), END 2 after it
+            flags[b - 2], flags[b - 1], flags[b], flags[b + 1] = 0x80, 0x00, 0xC0, 0x40
+    else:
+        parts = []
+        for _ in range(1 if layout == "one_long" else 6):
+            parts.append(np.full(int(rng.integers(100, 700)), 0xC0, np.uint8))
+            g = np.zeros(int(rng.integers(2500, 5000)), np.uint8)
+            g[0], g[-1] = 0x80, 0x40
+            inner = rng.choice(np.arange(1, g.size - 1), size=40, replace=False)
+            g[inner] = 0xC0  # whole messages inside the group
+            parts.append(g)
+        parts.append(np.full(300, 0xC0, np.uint8))
+        flags = np.concatenate(parts)
+        n = flags.size
+    lens = rng.integers(0, 200, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+    assert gpu_reassemble(codec, data, off, flags) == T.oracle_reassemble(data, off, flags)
+
+
+@pytest.mark.gpu
 def test_gpu_carry_continues_the_next_batch(codec):
     data, off, flags = T.fragment_stream(20000, 7, 0.3)
     exp_msgs, exp_carry = T.oracle_reassemble(data, off, flags)
