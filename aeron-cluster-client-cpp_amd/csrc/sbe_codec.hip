@@ -3520,6 +3520,9 @@ constexpr int kFcU = SBE_FC_U;
 #ifndef SBE_FC_UA
 #define SBE_FC_UA 1
 #endif
+#ifndef SBE_FC_NT
+#define SBE_FC_NT 1
+#endif
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4_a1 g_u32x4_a1;
 __device__ __forceinline__ uint4 gload128_ua(uintptr_t addr) {  // any byte address (one global_load_dwordx4)
@@ -3547,7 +3550,15 @@ __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, ui
 #pragma unroll
         for (int u = 0; u < kFcU; ++u) {
             const uint64_t c = c0 + (uint64_t)lane + (uint64_t)kWave * u;
+#if SBE_FC_NT  // nontemporal (streamed) stores, as the pack and decode kernels' outputs
+            if (c < nc) {
+                u32x4 v;
+                v.x = x[u].x, v.y = x[u].y, v.z = x[u].z, v.w = x[u].w;
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(d16 + c));
+            }
+#else
             if (c < nc) d16[c] = x[u];
+#endif
         }
     }
 #else
