@@ -3525,8 +3525,15 @@ constexpr int kFcU = SBE_FC_U;
 #endif
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4_a1 g_u32x4_a1;
+#ifndef SBE_FC_NTL  // A/B builds: 1 = the copy's source loads nontemporal
+#define SBE_FC_NTL 0
+#endif
 __device__ __forceinline__ uint4 gload128_ua(uintptr_t addr) {  // any byte address (one global_load_dwordx4)
+#if SBE_FC_NTL
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<g_u32x4_a1*>(addr));
+#else
     const u32x4 v = *reinterpret_cast<g_u32x4_a1*>(addr);
+#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void wave_copy16(uint8_t* dst, const uint8_t* src, uint64_t len, int lane) {
