@@ -262,6 +262,13 @@ struct Lay {
     static constexpr int32_t kBlk = kBlk_;
     static constexpr int kNF = kNF_;
     static constexpr bool kTM = kTM_;                 // TopicMessage block (timestamp default, truncation)
+    // staged-input loads nontemporal: TopicMessage and OrderRequestLite records (fixed-256 pack
+    // 99.3 -> 95.5 us, config 4 724.7 -> 707.3, OrderRequestLite 145.9 -> 144.1); not for session
+    // frames (134.3 -> 135.3) or CommitOffsetLite (40.7 -> 43.4), profiles/r05_ab_packntl.log
+#ifndef SBE_PACK_NTL  // A/B builds: 0 = never, 2 = always
+#define SBE_PACK_NTL 1
+#endif
+    static constexpr bool kNtIn = SBE_PACK_NTL == 2 || (SBE_PACK_NTL == 1 && (kTM_ ? kPre_ == 0 : kNF_ == 3));
     static constexpr int32_t kLit = kPre + 8 + kBlk;  // literal prefix bytes (multiple of 4)
     static constexpr int32_t kS0 = kLit + 2;          // first string byte
     static constexpr int32_t kOvh = kLit + 2 * kNF;   // wire overhead
@@ -783,13 +790,17 @@ __device__ __forceinline__ void stage_range(const TileSt& S, int32_t wrel, int l
 // Always kStageRegs loads (all lanes, offsets clamped into [swb, swb + nbytes); swb must be
 // readable for 16 bytes when nbytes == 0): the loop body's vector-memory operations are then
 // straight-line, so the compiler's vmcnt waits count them exactly instead of draining all.
+// kNt: nontemporal loads (Lay::kNtIn: the input is read once and not from this kernel's caches again)
+template <bool kNt>
 __device__ __forceinline__ void stage_issue(uintptr_t swb, int32_t nbytes, int lane, uint4 (&I)[kStageRegs]) {
     g_u32x4* const base = reinterpret_cast<g_u32x4*>(swb);  // uniform base + 32-bit lane offsets
     const uint32_t last = nbytes >= 16 ? (uint32_t)(nbytes - 16) >> 4 : 0u;
 #pragma unroll
     for (int k = 0; k < kStageRegs; ++k) {
         const uint32_t ch = lane + kWave * k;
-        const u32x4 v = base[ch < last ? ch : last];
+        u32x4 v;
+        if constexpr (kNt) v = __builtin_nontemporal_load(base + (ch < last ? ch : last));
+        else v = base[ch < last ? ch : last];
         I[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -1797,7 +1808,7 @@ __device__ __forceinline__ void enc_pack_run(const EncArgs& a, uint64_t first, u
     bool fast = kPacked && !S.wrapped && !tile_big<LY>(S, lane);
     if (fast) W = tile_window<LY>(S, 0, lane, sink);
     if (kPacked) {
-        stage_issue(W.swb, W.nb, lane, I);
+        stage_issue<LY::kNtIn>(W.swb, W.nb, lane, I);
         stage_write(win_in, W.nb, lane, I);
     }
     uint64_t tn = t + G;
@@ -1824,7 +1835,7 @@ __device__ __forceinline__ void enc_pack_run(const EncArgs& a, uint64_t first, u
             fast_n = kPacked && !Sn.wrapped && !tile_big<LY>(Sn, lane);
             if (fast_n) Wn = tile_window<LY>(Sn, 0, lane, sink);
         }
-        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
+        if (have_next && kPacked) stage_issue<LY::kNtIn>(Wn.swb, Wn.nb, lane, I);
         ph.lap(0);
         // current window (fast) or the whole tile window by window
         if (fast) {
@@ -2037,7 +2048,7 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
 #endif
     rn += advance(S, W, fast);
     if (kPacked) {
-        stage_issue(W.swb, W.nb, lane, I);
+        stage_issue<LY::kNtIn>(W.swb, W.nb, lane, I);
         stage_write(win_in, W.nb, lane, I);
     }
     // the next step: the rest of this chunk, or the workgroup's next chunk (its base from the
@@ -2080,7 +2091,7 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
                 x = vt_load<LY, kPacked>(a, rnn, lane);
             }
         }
-        if (have_next && kPacked) stage_issue(Wn.swb, Wn.nb, lane, I);
+        if (have_next && kPacked) stage_issue<LY::kNtIn>(Wn.swb, Wn.nb, lane, I);
         ph.lap(0);
         if (fast) {
             if (!compose_records<LY>(a, wout, win_in, rt, S, W.wrel, W.wlen, W.swb, W.nb, lane, W.ra, W.rb, ph, spread)) {
