@@ -11,8 +11,10 @@
 // yields nine digits per multiply.  Values with short binary fractions (prices, quantities) touch
 // one or two words; the full range (subnormals, 1e308) takes more words, never a different path.
 //
-// One lane per Order; a sizing launch (text length + packed-arena string total), two device scans,
-// then the writing launch, which stages each wave's texts in LDS and stores them coalesced.
+// One lane per Order; per-block string totals (packed arena) and their one-block scan, a sizing
+// launch (text lengths, string bases, per-block text totals) and its one-block scan, then the
+// writing launch, which finds each text's offset from the block sums, stages each wave's texts in
+// LDS and stores them coalesced.
 #pragma once
 
 namespace oj {

@@ -27,7 +27,6 @@
 //       descriptor SoA; records no window can hold are parsed from HBM.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
-#include <hipcub/device/device_scan.hpp>
 #include <dlfcn.h>
 #include <rccl/rccl.h>  // types only: the library is dlopen-ed (rccl_api)
 
