@@ -261,11 +261,12 @@ struct Lay {
     static constexpr int32_t kBlk = kBlk_;
     static constexpr int kNF = kNF_;
     static constexpr bool kTM = kTM_;                 // TopicMessage block (timestamp default, truncation)
-    // staged-input loads nontemporal: TopicMessage and OrderRequestLite records (fixed-256 pack
-    // 99.3 -> 95.5 us, config 4 724.7 -> 707.3, OrderRequestLite 145.9 -> 144.1); not for session
-    // frames (134.3 -> 135.3) or CommitOffsetLite (40.7 -> 43.4), profiles/r05_ab_packntl.log
-#ifndef SBE_PACK_NTL  // A/B builds: 0 = never, 2 = always
-#define SBE_PACK_NTL 1
+    // staged-input loads nontemporal (A/B builds only): in scripts/ab_rows.py they took the
+    // fixed-256 pack 98.3 -> 93.7 us and config 4 721.7 -> 704.3 us, but the headline bench, whose
+    // repeated 250 MB input stays in the 256 MB MALL under the default policy, ran 86.3 -> 94.9 us
+    // (profiles/r05_ab_packntl.log): default loads
+#ifndef SBE_PACK_NTL  // 0 = never, 1 = TopicMessage / OrderRequestLite, 2 = always
+#define SBE_PACK_NTL 0
 #endif
     static constexpr bool kNtIn = SBE_PACK_NTL == 2 || (SBE_PACK_NTL == 1 && (kTM_ ? kPre_ == 0 : kNF_ == 3));
     static constexpr int32_t kLit = kPre + 8 + kBlk;  // literal prefix bytes (multiple of 4)
