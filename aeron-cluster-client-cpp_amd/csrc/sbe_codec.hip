@@ -3434,12 +3434,24 @@ __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
 #ifndef SBE_FRAG_FUSED  // A/B builds: 0 = frag_scan + frag_messages
 #define SBE_FRAG_FUSED 1
 #endif
+// The block's messages are the consecutive indices [dp before the block, dp after it): their four
+// table entries go through LDS, one array at a time, and leave as contiguous 8-B stores per lane
+// (stored straight from each fragment's lane, a wave's 64 stores land 32 B apart and the table
+// cost 56.6 MB of HBM writes for 32 MB of entries, profiles/r05_reasm2_summary.txt).
+#ifndef SBE_FRAG_STAGE
+#define SBE_FRAG_STAGE 1
+#endif
 __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const FragScan* pre) {
     __shared__ FragScan wt[kFsThreads / kWave];
     __shared__ uint32_t sgl[kFsBlk];  // inclusive singles count at every fragment of the block
+#if SBE_FRAG_STAGE
+    __shared__ uint64_t stg[kFsBlk];  // one table array of the block's messages
+    uint64_t tv[kFsPer][4];
+    uint32_t tj[kFsPer];              // message index - j0, or ~0u (no message at this fragment)
+#endif
     const uint64_t b = blockIdx.x;
     FragScan e[kFsPer], before;
-    (void)fs_block(a, b, e, wt, before);
+    const FragScan tot = fs_block(a, b, e, wt, before);
     const FragScan P = pre[b];  // the scan at the fragment before the block
     const FragScan base = FragScanOp{}(P, before);
     const int tid = threadIdx.x;
@@ -3464,6 +3476,11 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
         const uint32_t sg0 = s0 ? sg_at(s0 - 1) : 0u;
         gap = fs_sg(x) != sg0;
     };
+#if SBE_FRAG_STAGE
+    const uint32_t j0 = fs_dp(P), nj = fs_dp(tot);  // the block's messages: [j0, j0 + nj)
+#pragma unroll
+    for (int k = 0; k < kFsPer; ++k) tj[k] = ~0u;
+#endif
 #pragma unroll
     for (int k = 0; k < kFsPer; ++k) {
         const uint64_t i = i0 + k;
@@ -3476,18 +3493,26 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
         const uint32_t dp = fs_dp(x);
         if ((single || (f & SBE_FRAG_END)) && dp >= 1 && dp <= a.n) {
             const uint64_t j = dp - 1;
-            a.msize[j] = x.E - E0;
-            a.msg_off[j] = E0;
-            if (single) {
-                a.mfirst[j] = i;
-                a.mlast[j] = i;
-            } else {
+            uint64_t first = i, last = i;
+            if (!single) {
                 uint64_t s0;
                 bool gap;
                 group(x, i ? (int64_t)prev.le : -1, s0, gap);
-                a.mfirst[j] = s0;
-                a.mlast[j] = i | (gap ? (1ull << 63) : 0ull);
+                first = s0;
+                last = i | (gap ? (1ull << 63) : 0ull);
             }
+#if SBE_FRAG_STAGE
+            tj[k] = (uint32_t)(j - j0);
+            tv[k][0] = x.E - E0;
+            tv[k][1] = E0;
+            tv[k][2] = first;
+            tv[k][3] = last;
+#else
+            a.msize[j] = x.E - E0;
+            a.msg_off[j] = E0;
+            a.mfirst[j] = first;
+            a.mlast[j] = last;
+#endif
         }
         if (i == a.n - 1) {  // the open accumulator after the last fragment: the carry
             const uint64_t m = dp <= a.n ? dp : a.n;
@@ -3504,6 +3529,18 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
             a.counts[1] = open ? bytes : 0u;
         }
     }
+#if SBE_FRAG_STAGE
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int k = 0; k < kFsPer; ++k)
+            if (tj[k] != ~0u) stg[tj[k]] = tv[k][r];
+        __syncthreads();
+        uint64_t* dst = (r == 0 ? a.msize : r == 1 ? a.msg_off : r == 2 ? a.mfirst : a.mlast) + j0;
+        for (uint32_t t = tid; t < nj; t += kFsThreads) dst[t] = stg[t];
+        __syncthreads();
+    }
+#endif
 }
 
 // the 16 bytes at src + 16c + sh from the aligned blocks b0 (at 16c) and b1 (the next one)
