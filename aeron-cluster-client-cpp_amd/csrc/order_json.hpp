@@ -961,6 +961,11 @@ __global__ __launch_bounds__(kScanThreads) void order_json_scan_blocks(uint64_t*
 #ifndef SBE_OJ_MSTR  // LDS bytes per wave for the staged strings (0: never staged)
 #define SBE_OJ_MSTR 10240
 #endif
+// A/B builds: 0 = headers texts (3 of the 8 strings) sized from HBM, not staged: measured slower
+// (row 0.560 -> 0.580 ms, profiles/r05_ab_ojhstage.log), so the headers launch stages all 8 as well
+#ifndef SBE_OJ_HSTAGE
+#define SBE_OJ_HSTAGE 1
+#endif
 template <uint32_t kWhat>
 __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
     __shared__ uint64_t wtot[kBlock / kWave];
@@ -981,15 +986,16 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
         if (live) a.str_base[i] = base;
 #if SBE_OJ_MSTR > 0
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        __shared__ __attribute__((aligned(16))) uint8_t sbuf[kBlock / kWave][SBE_OJ_MSTR];
+        constexpr bool kStage = kWhat != SBE_JSON_PUBLISH_HEADERS || SBE_OJ_HSTAGE;
+        __shared__ __attribute__((aligned(16))) uint8_t sbuf[kBlock / kWave][kStage ? SBE_OJ_MSTR : 16];
         const uint64_t i0 = i - lane;
         bool staged = false;
         uint64_t g0 = 0;
-        if (i0 < a.n) {  // uniform per wave
+        if (kStage && i0 < a.n) {  // uniform per wave
             g0 = lane_u64(base, 0) & ~15ull;
             const uint64_t last = a.n - 1 - i0 < kWave - 1 ? a.n - 1 - i0 : kWave - 1;
             const uint64_t end = lane_u64(base + tot, (int)last);
-            staged = end - g0 <= SBE_OJ_MSTR;
+            staged = end - g0 <= (kStage ? SBE_OJ_MSTR : 0);
             if (staged) {
                 typedef const __attribute__((address_space(1))) u32x4 g128;
                 typedef __attribute__((address_space(3))) u32x4 l128;
