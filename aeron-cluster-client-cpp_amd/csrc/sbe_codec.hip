@@ -3260,7 +3260,10 @@ __device__ __forceinline__ bool frag_single(uint8_t f) {
 // 1024-fragment block on the fly and writes the block's aggregate; frag_scan_blocks turns the
 // aggregates into exclusive block prefixes (one workgroup, 1024 at a time with a carry);
 // frag_scan re-classifies and writes the inclusive scan.  Elements are never materialised.
-constexpr int kFsPer = 4, kFsThreads = 256, kFsBlk = kFsPer * kFsThreads;
+#ifndef SBE_FS_PER  // A/B builds: fragments per thread of the scan launches
+#define SBE_FS_PER 4
+#endif
+constexpr int kFsPer = SBE_FS_PER, kFsThreads = 256, kFsBlk = kFsPer * kFsThreads;
 __device__ __forceinline__ FragScan fs_identity() { return FragScan{0u, 0x80000000u, -1, -1, 0ull, 0ull}; }
 __device__ __forceinline__ FragScan fs_elem(const FragArgs& a, uint64_t i) {
     if (i >= a.n) return fs_identity();
