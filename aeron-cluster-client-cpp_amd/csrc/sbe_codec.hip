@@ -261,12 +261,13 @@ struct Lay {
     static constexpr int32_t kBlk = kBlk_;
     static constexpr int kNF = kNF_;
     static constexpr bool kTM = kTM_;                 // TopicMessage block (timestamp default, truncation)
-    // staged-input loads nontemporal (A/B builds only): in scripts/ab_rows.py they took the
-    // fixed-256 pack 98.3 -> 93.7 us and config 4 721.7 -> 704.3 us, but the headline bench, whose
-    // repeated 250 MB input stays in the 256 MB MALL under the default policy, ran 86.3 -> 94.9 us
-    // (profiles/r05_ab_packntl.log): default loads
-#ifndef SBE_PACK_NTL  // 0 = never, 1 = TopicMessage / OrderRequestLite, 2 = always
-#define SBE_PACK_NTL 0
+    // staged-input loads nontemporal: the input is read once.  On inputs that rotate over three
+    // buffer sets (no step finds its input in the 256 MB MALL, as streaming data would not) they
+    // read fixed-256 96.0 -> 94.2 us, config 4 723.3 -> 716.6, OrderRequestLite 146.3 -> 143.8,
+    // session frames 137.7 -> 137.2 (profiles/r06_ab_ntl_rot.log); only a batch re-read every step
+    // (rounds 1-5's bench) prefers the default policy, whose lines the MALL keeps (86.6 vs 93.9 us)
+#ifndef SBE_PACK_NTL  // A/B builds: 0 = never, 1 = TopicMessage / OrderRequestLite, 2 = always
+#define SBE_PACK_NTL 2
 #endif
     static constexpr bool kNtIn = SBE_PACK_NTL == 2 || (SBE_PACK_NTL == 1 && (kTM_ ? kPre_ == 0 : kNF_ == 3));
     static constexpr int32_t kLit = kPre + 8 + kBlk;  // literal prefix bytes (multiple of 4)
@@ -3468,8 +3469,26 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
     __syncthreads();
     auto sg_at = [&](uint64_t x) -> uint32_t {  // singles among fragments [0, x]
         if (x >= blk0) return sgl[x - blk0];
-        uint32_t c = fs_sg(P);
-        for (uint64_t y = x + 1; y < blk0; ++y) c -= frag_single(a.flags[y]) ? 1u : 0u;
+        // x lies in an earlier block: that block's exclusive prefix plus the singles from its first
+        // fragment through x, counted from 16-byte aligned flag loads (at most kFsBlk / 16 + 1
+        // independent loads; an aligned 16-B block holding a flag byte never crosses a page).
+        // Walking one flag at a time from x up to this block cost thousands of loads for a group
+        // of thousands of fragments.
+        const uint64_t s = x / kFsBlk * kFsBlk;
+        uint32_t c = fs_sg(pre[x / kFsBlk]);
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(a.flags + s), hi = reinterpret_cast<uintptr_t>(a.flags + x);
+        for (uintptr_t q = lo & ~(uintptr_t)15; q <= hi; q += 16) {
+            const uint4 w4 = gload128(q);
+            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uintptr_t b0 = q + 4 * t;  // address of byte 0 of this dword
+                uint32_t m = (w[t] >> 1) & w[t] & 0x40404040u;  // bit 6 of a byte: BEGIN and END both set
+                if (b0 < lo) m &= lo - b0 >= 4 ? 0u : ~0u << (8 * (lo - b0));
+                if (b0 + 3 > hi) m &= b0 > hi ? 0u : byte_mask_bits((uint32_t)(hi - b0 + 1));
+                c += __builtin_popcount(m);
+            }
+        }
         return c;
     };
     auto group = [&](const FragScan& x, int64_t le_before, uint64_t& s0, bool& gap) {  // frag_group
@@ -5015,7 +5034,7 @@ int sbe_gather_encoded(sbe_comm* c, int root, const uint8_t* out, const uint64_t
 int sbe_gather_encoded_sized(sbe_comm* c, int root, const uint64_t* sizes, const uint8_t* out,
                              const uint64_t* out_off, uint8_t* dst, uint64_t dst_capacity, uint64_t* dst_off,
                              uint64_t dst_off_capacity, uint64_t* totals, void* stream) {
-    if (!c || !sizes || !out_off || root < 0 || root >= c->world) return SBE_EINVAL;
+    if (!c || !sizes || !out_off || root < 0 || root >= c->world || dst_off_capacity == 0) return SBE_EINVAL;
     const bool am_root = c->rank == root;
     if (am_root && !dst_off) return SBE_EINVAL;
     // the plan from the caller's sizes, with the root's capacities every rank was given

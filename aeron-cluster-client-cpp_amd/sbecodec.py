@@ -651,25 +651,42 @@ def gather_encoded_sized(comm: Comm, sizes, out, out_off, root: int = 0, dst=Non
     """Collective, for callers that know every shard's size: sizes = [(bytes, records)] per rank,
     identical on every rank.  No size all-gather and no host wait (sbe_gather_encoded_sized): the
     transfers and the root's rebase are enqueued on `stream`.  Every rank passes the ROOT's
-    capacities (the root's own default to its dst / dst_off sizes); returns as gather_encoded."""
+    capacities (dst_capacity bytes, dst_off_capacity offsets; both required, on every rank: a rank
+    that decided ENOSPC alone would leave the others blocked in their transfers); returns as
+    gather_encoded.
+
+    Checked before anything is enqueued: both capacities non-zero; on the root, that
+    they do not exceed dst / dst_off; on every rank, that out / out_off hold this rank's
+    sizes[rank] bytes / records (RCCL reads and writes exactly the planned counts)."""
     world = comm.world
     if len(sizes) != world:
         raise SbeError(f"sizes has {len(sizes)} entries for a world of {world}")
+    dst_capacity, dst_off_capacity = int(dst_capacity), int(dst_off_capacity)
+    if dst_capacity <= 0 or dst_off_capacity <= 0:
+        raise SbeError("gather_encoded_sized: every rank passes the root's dst_capacity and dst_off_capacity "
+                       f"(got {dst_capacity}, {dst_off_capacity})")
+    my_bytes, my_recs = (int(v) for v in sizes[comm.rank])
     out = _dev(out, torch.uint8, "out")
     out_off = _dev(out_off, torch.int64, "out_off")
+    if out is None or out_off is None:
+        raise SbeError("gather_encoded_sized: every rank passes its shard's out and out_off")
+    if out.numel() < my_bytes or out_off.numel() < my_recs:
+        raise SbeError(f"rank {comm.rank}: shard buffers hold {out.numel()} bytes / {out_off.numel()} offsets, "
+                       f"sizes[{comm.rank}] says {my_bytes} / {my_recs}")
     am_root = comm.rank == root
     if am_root:
         dst = _dev(dst, torch.uint8, "dst")
         dst_off = _dev(dst_off, torch.int64, "dst_off")
         if dst is None or dst_off is None:
             raise SbeError("the root passes dst and dst_off")
-        dst_capacity = dst_capacity or int(dst.numel())
-        dst_off_capacity = dst_off_capacity or int(dst_off.numel())
+        if dst_capacity > dst.numel() or dst_off_capacity > dst_off.numel():
+            raise SbeError(f"root capacities {dst_capacity} / {dst_off_capacity} exceed dst ({dst.numel()}) / "
+                           f"dst_off ({dst_off.numel()})")
     flat = (ctypes.c_uint64 * (2 * world))(*[int(v) for sz in sizes for v in sz])
     totals = (ctypes.c_uint64 * 2)()
     rc = lib().sbe_gather_encoded_sized(comm._h, int(root), flat, _ptr(out), _ptr(out_off),
-                                        _ptr(dst) if am_root else None, int(dst_capacity),
-                                        _ptr(dst_off) if am_root else None, int(dst_off_capacity),
+                                        _ptr(dst) if am_root else None, dst_capacity,
+                                        _ptr(dst_off) if am_root else None, dst_off_capacity,
                                         totals, _stream(stream))
     _check(rc, "sbe_gather_encoded_sized")
     nbytes, nrec = int(totals[0]), int(totals[1])

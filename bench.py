@@ -7,7 +7,10 @@ One step = one round trip of the hot path over one batch resident in HBM:
     workload's payloads carry no "_sequence_number" and no escapes, as the Order JSON of the
     reference has none, so nothing is evaluated; --separate-seq uses the standalone launch).
 Workload (BASELINE.json configs[1] extended to the metric's encode+decode): 1,000,000 fixed-256 B
-Order TopicMessages per GPU (seed 0x5EED0002 + rank), synthetic.
+Order TopicMessages per GPU (seed 0x5EED0002 + rank), synthetic.  The
+steps rotate over --sets (3) distinct sets of inputs and outputs, so that no step reads what the
+previous one left in the 256 MB MALL (a 1 M-record set is ~0.58 GB); the roofline comes from the
+rotated steps, and the one-set (warm-cache) figure rides beside it as `frac_warm`.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  `--gpus N` outside a launcher starts
 N ranks through torch.distributed.run before touching the GPU.  The headline shards records by
@@ -60,6 +63,10 @@ def parse_args():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--records", type=int, default=1_000_000, help="records per GPU (headline)")
+    p.add_argument("--sets", type=int, default=3,
+                   help="distinct input / output buffer sets the steps rotate over (step k uses set k mod S). "
+                        "Three 1 M-record sets put ~1.7 GB of other traffic between two reads of one set, so no "
+                        "step finds its inputs in the 256 MB MALL; --sets 1 is the old warm-cache workload")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="host threads of the CPU baseline (0: the cores this process may use, capped by "
@@ -361,45 +368,56 @@ def main():
     sbecodec.require_device()
     dev = torch.device("cuda", local)
     n = args.records
-    arena, L, ts = make_inputs(n, rank, dev)
-    cap = sbecodec.output_bound(n, int(arena.numel()))
-    out = torch.empty(cap, dtype=torch.uint8, device=dev)
-    out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    nsets = max(1, args.sets)
+    # S distinct sets of inputs and outputs (step k uses set k mod S): every set has its own arena,
+    # lengths, timestamps, encoded stream, offsets, status and descriptors, so a step reads nothing
+    # that the previous step left in the caches (MI355X_MICROARCH.md: 256 MB MALL)
+    sets = []
+    for k in range(nsets):
+        arena, L, ts = make_inputs(n, rank + (k << 16), dev)
+        cap = sbecodec.output_bound(n, int(arena.numel()))
+        sets.append(dict(arena=arena, L=L, ts=ts, out=torch.empty(cap, dtype=torch.uint8, device=dev),
+                         out_off=torch.empty(n + 1, dtype=torch.int64, device=dev),
+                         status=torch.empty(n, dtype=torch.uint8, device=dev),
+                         dec=sbecodec.alloc_decoded(n, dev), seq=torch.zeros(n, dtype=torch.int64, device=dev)))
     ws = sbecodec.alloc_workspace(n, dev)
-    dec = sbecodec.alloc_decoded(n, dev)
-    seq = torch.zeros(n, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
 
     ev_enc = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     ev_dec = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    rot = {"i": 0, "only": None}  # next set; "only": pin every step to one set (the warm-cache pass)
 
     def step(k=None):
         # k is not None: the untimed pass that brackets the whole encode / decode calls with
         # torch events (the timed steps carry only the library's kernel events)
+        b = sets[rot["only"] if rot["only"] is not None else rot["i"] % nsets]
+        rot["i"] += 1
         if k is not None:
             ev_enc[k][0].record(stream)
-        sbecodec.encode_topic_batch(arena, L, ts, out=out, out_off=out_off, status=status, workspace=ws,
-                                    stream=stream)
+        sbecodec.encode_topic_batch(b["arena"], b["L"], b["ts"], out=b["out"], out_off=b["out_off"],
+                                    status=b["status"], workspace=ws, stream=stream)
         if k is not None:
             ev_enc[k][1].record(stream)
             ev_dec[k][0].record(stream)
         if args.separate_seq:
-            sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream)
-            sbecodec.eval_sequence_numbers(out, out_off, dec, seq=seq, stream=stream)
+            sbecodec.decode_batch(b["out"], b["out_off"], mode=sbecodec.DEC_PARSE_MESSAGE, out=b["dec"], stream=stream)
+            sbecodec.eval_sequence_numbers(b["out"], b["out_off"], b["dec"], seq=b["seq"], stream=stream)
         else:
-            sbecodec.decode_batch(out, out_off, mode=sbecodec.DEC_PARSE_MESSAGE, out=dec, stream=stream, seq=seq)
+            sbecodec.decode_batch(b["out"], b["out_off"], mode=sbecodec.DEC_PARSE_MESSAGE, out=b["dec"],
+                                  stream=stream, seq=b["seq"])
         if k is not None:
             ev_dec[k][1].record(stream)
 
     if args.verify:
-        step()
-        torch.cuda.synchronize()
         import sbe_testlib as T
-        eo, eoff, _ = T.oracle_encode(arena.cpu().numpy(), L.cpu().numpy().view(np.uint32),
-                                      ts.cpu().numpy().view(np.uint64))
-        assert np.array_equal(out_off.cpu().numpy().view(np.uint64), eoff)
-        assert np.array_equal(out[: int(eoff[-1])].cpu().numpy(), eo)
+        for _ in range(nsets):
+            b = sets[rot["i"] % nsets]
+            step()
+            torch.cuda.synchronize()
+            eo, eoff, _ = T.oracle_encode(b["arena"].cpu().numpy(), b["L"].cpu().numpy().view(np.uint32),
+                                          b["ts"].cpu().numpy().view(np.uint64))
+            assert np.array_equal(b["out_off"].cpu().numpy().view(np.uint64), eoff)
+            assert np.array_equal(b["out"][: int(eoff[-1])].cpu().numpy(), eo)
     # host-side setup before the warmup, so the GPU goes from the warmup steps straight into the
     # timed ones: creating the profiling events takes ~1 ms of host time, during which an idle GPU
     # lowers its clocks
@@ -439,6 +457,18 @@ def main():
     deck_samples = sbecodec.profile_read(sbecodec.PROF_DECODE)
     pack_ms = float(np.mean(pack_samples))
     deck_ms = float(np.mean(deck_samples))
+    # the warm-cache figure (rounds 1-5's workload): the same number of steps on set 0 alone, so
+    # each step re-reads what the previous one left in the MALL; reported beside, never the roofline
+    rot["only"] = 0
+    for _ in range(10):
+        step()
+    sbecodec.profile_enable(1)
+    for _ in range(args.sample_steps):
+        step()
+    torch.cuda.synchronize()
+    pack_warm = float(np.mean(sbecodec.profile_read(sbecodec.PROF_PACK)))
+    deck_warm = float(np.mean(sbecodec.profile_read(sbecodec.PROF_DECODE)))
+    rot["only"] = None
     sbecodec.profile_enable(0)
 
     # informational, untimed: whole-call encode (sums + pack) and decode times
@@ -452,7 +482,7 @@ def main():
 
     c5 = None
     if not args.no_config5:
-        del arena, L, ts, out, dec, seq
+        sets.clear()
         torch.cuda.empty_cache()
         try:
             c5 = config5(args, world, rank, dev)
@@ -465,10 +495,10 @@ def main():
 
         if pack_ms >= deck_ms:
             dom = dict(kernel="sbe_enc_pack<packed,wire>", bytes_per_record=ENC_BYTES, bytes_all=ENC_BYTES_ALL,
-                       ms=pack_ms, samples=pack_samples, inreg=inreg_pack)
+                       ms=pack_ms, samples=pack_samples, inreg=inreg_pack, warm=pack_warm)
         else:
             dom = dict(kernel="sbe_decode_kernel<parse_message>", bytes_per_record=DEC_BYTES,
-                       bytes_all=DEC_BYTES_ALL, ms=deck_ms, samples=deck_samples, inreg=inreg_deck)
+                       bytes_all=DEC_BYTES_ALL, ms=deck_ms, samples=deck_samples, inreg=inreg_deck, warm=deck_warm)
         traffic = measured_traffic(dom["kernel"], n)
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # rank 0 at N=1 only
@@ -481,7 +511,10 @@ def main():
             "config": {"workload": "roundtrip_fixed256_orders", "records_per_gpu": n, "record_bytes": 256,
                        "encode": "wire-correct TopicMessage, packed SoA input",
                        "decode": "parse_message descriptors (views) + sequence_number evaluation",
-                       "parallelism": f"shard{world}", "settle": {"ms": args.settle_ms, "steps": settle_steps}},
+                       "parallelism": f"shard{world}", "settle": {"ms": args.settle_ms, "steps": settle_steps},
+                       "input_sets": nsets,
+                       "rotation": (f"step k encodes set k mod {nsets} and decodes that set's stream; every set has "
+                                    f"its own inputs and outputs ({nsets} x ~{(n * (250 + 256 + 58 + 17)) / 1e9:.2f} GB)")},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom["kernel"],
                          "kernel_ms": dom["ms"], "bytes_per_record": dom["bytes_per_record"],
@@ -497,9 +530,14 @@ def main():
                          "kernel_ms_in_region": float(np.mean(dom["inreg"])) if dom["inreg"] else None,
                          "kernel_ms_min": float(np.min(dom["samples"])),
                          "kernel_ms_median": float(np.median(dom["samples"])),
-                         "kernel_ms_max": float(np.max(dom["samples"]))},
+                         "kernel_ms_max": float(np.max(dom["samples"])),
+                         "cache": (f"inputs rotated over {nsets} sets (cache-cold for the MALL)" if nsets > 1 else
+                                   "one input set re-read every step (warm: part of it is served by the MALL)"),
+                         "kernel_ms_warm": dom["warm"], "achieved_warm": gbs(dom["bytes_per_record"], dom["warm"]),
+                         "frac_warm": gbs(dom["bytes_per_record"], dom["warm"]) / HBM_PEAK_GBS},
             "kernels": {"encode_ms": enc_ms, "decode_ms": dec_ms, "pack_ms": pack_ms,
                         "pack_gbs": gbs(ENC_BYTES, pack_ms), "decode_kernel_ms": deck_ms,
+                        "pack_ms_warm": pack_warm, "decode_kernel_ms_warm": deck_warm,
                         "decode_kernel_gbs": gbs(DEC_BYTES, deck_ms),
                         "roundtrip_gbs": n * (ENC_BYTES + DEC_BYTES) / ((enc_ms + dec_ms) * 1e-3) / 1e9},
             "cpu_baseline": cpu,

@@ -393,7 +393,9 @@ int sbe_gather_encoded(sbe_comm* comm, int root, const uint8_t* out, const uint6
  * the root's rebase on `stream` and returns, so a rank can go on to encode its next shard while
  * this one travels.  dst_capacity / dst_off_capacity are the ROOT's capacities, passed on every
  * rank (non-roots pass dst = dst_off = NULL), so every rank reaches the same SBE_ENOSPC verdict
- * before anything is sent.  The sizes are trusted as a planned encode's tile sums are: they must
+ * before anything is sent; dst_off_capacity 0 is SBE_EINVAL (N + 1 >= 1 offsets are always
+ * written), and a rank that passes other capacities than the root's can leave the root blocked in
+ * its receives, so the Python binding refuses zero capacities on every rank.  The sizes are trusted as a planned encode's tile sums are: they must
  * equal out_off[n] and n of the shard each rank encoded (a wrong plan moves the wrong bytes; it
  * never writes past the root's capacities). */
 int sbe_gather_encoded_sized(sbe_comm* comm, int root, const uint64_t* sizes, const uint8_t* out,

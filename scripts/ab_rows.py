@@ -28,6 +28,9 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--steps", type=int, default=10)
 ap.add_argument("--var-records", type=int, default=4_000_000)
 ap.add_argument("--no-check", action="store_true", help="ablation builds (wrong bytes by design): skip the check")
+ap.add_argument("--rotate", type=int, default=1,
+                help="distinct copies of every workload's inputs and outputs the steps rotate over (R > 1: no "
+                     "step finds its inputs in the 256 MB MALL; 1: the same buffers every step)")
 ap.add_argument("--phases", action="store_true", help="builds with -DSBE_PACK_PHASES: print the pack loop's phase shares")
 args = ap.parse_args()
 
@@ -81,6 +84,13 @@ for w in works.values():
         w["st"] = torch.empty(n, dtype=torch.uint8, device=dev)
     w["seq"] = torch.zeros(n, dtype=torch.int64, device=dev)
 
+# rotation: R copies of every tensor a step reads or writes (clones: the same bytes at other addresses)
+for w in works.values():
+    w["sets"] = [{k: v for k, v in w.items() if torch.is_tensor(v)}]
+    for _ in range(1, args.rotate):
+        w["sets"].append({k: v.clone() for k, v in w["sets"][0].items()})
+    w["cur"] = 0
+
 res = {(p, k): {"pack": [], "dec": []} for p in args.libs for k in works}
 ref = {}
 for rnd in range(args.rounds):
@@ -89,9 +99,13 @@ for rnd in range(args.rounds):
         for k, w in works.items():
             n = w["n"]
             ws = sbecodec.alloc_workspace(n, dev) if w["enc"] else None
-            dec = sbecodec.alloc_decoded(n, dev)
+            decs = [sbecodec.alloc_decoded(n, dev) for _ in w["sets"]]
 
             def step():
+                j = w["cur"] % len(w["sets"])
+                w["cur"] += 1
+                w.update(w["sets"][j])
+                dec = decs[j]
                 if "lite" in w:
                     sbecodec.encode_lite_batch(w["lite"], w["a"], w["l"], w["ti"], w["sq"], out=w["out"],
                                                out_off=w["off_o"], status=w["st"], workspace=ws)
@@ -111,6 +125,7 @@ for rnd in range(args.rounds):
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
+            dec = decs[(w["cur"] - 1) % len(w["sets"])]
             if rnd == 0 and not args.no_check:  # every build must produce the same bytes and descriptors
                 h = (int(dec.status.to(torch.int64).sum()), int(dec.view_off.to(torch.int64).sum()),
                      int(dec.view_len.to(torch.int64).sum()), int(dec.ts.sum()))
@@ -137,7 +152,7 @@ for rnd in range(args.rounds):
                 print(f"phases {k:8s} {os.path.basename(p):18s} waves {int(live.sum())} mean wave clk "
                       f"{ph[live].sum(1).mean():.0f}: " + " ".join(f"{nm} {v / tot.sum():.3f}" for nm, v in zip(names, tot)),
                       flush=True)
-            del ws, dec
+            del ws, dec, decs
 for k in works:
     for p in args.libs:
         r = res[(p, k)]

@@ -23,7 +23,7 @@ constexpr int kIn = 7104, kOut = 8192;
 constexpr int kInCh = (kIn + 15) / 16;  // 444 chunks
 constexpr int kOutCh = kOut / 16;       // 512 chunks
 
-template <int kAux, int kTilesPerWave>
+template <int kAux, int kTilesPerWave, bool kNtl = false>
 __global__ __launch_bounds__(256) void copy_tiles(const uint8_t* in, uint8_t* out, long tiles, long stride_tiles) {
     const int lane = threadIdx.x & 63;
     const long wave = (long)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
@@ -37,7 +37,11 @@ __global__ __launch_bounds__(256) void copy_tiles(const uint8_t* in, uint8_t* ou
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int c = lane + 64 * k;
-                v[k] = c < kInCh ? src[c < kInCh - 1 ? c : kInCh - 1] : v[k > 0 ? k - 1 : 0];
+                const u32x4* p = src + (c < kInCh - 1 ? c : kInCh - 1);
+                u32x4 x;
+                if constexpr (kNtl) x = __builtin_nontemporal_load(p);
+                else x = *p;
+                v[k] = c < kInCh ? x : v[k > 0 ? k - 1 : 0];
             }
             uint8_t* dst = out + t * (long)kOut;
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, kOut, 0x00020000);
@@ -47,15 +51,24 @@ __global__ __launch_bounds__(256) void copy_tiles(const uint8_t* in, uint8_t* ou
     }
 }
 
-template <int kAux, int kTpw>
+// rotation (argv[2], default 1): R copies of the input and output, launch i uses copy i mod R, so
+// with R >= 3 no launch finds its input in the 256 MB MALL (bench.py's rotated headline)
+static int g_rot = 1;
+static long g_in_stride = 0, g_out_stride = 0;
+template <int kAux, int kTpw, bool kNtl = false>
 float run(const uint8_t* in, uint8_t* out, long tiles, int blocks, int threads, int reps) {
     const long waves = (long)blocks * threads / 64;
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((copy_tiles<kAux, kTpw>), dim3(blocks), dim3(threads), 0, 0, in, out, tiles, waves);
+    auto go = [&](int i) {
+        const int k = i % g_rot;
+        hipLaunchKernelGGL((copy_tiles<kAux, kTpw, kNtl>), dim3(blocks), dim3(threads), 0, 0, in + k * g_in_stride,
+                           out + k * g_out_stride, tiles, waves);
+    };
+    for (int i = 0; i < 3; ++i) go(i);
     CK(hipEventRecord(a));
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((copy_tiles<kAux, kTpw>), dim3(blocks), dim3(threads), 0, 0, in, out, tiles, waves);
+    for (int i = 0; i < reps; ++i) go(i);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -66,10 +79,14 @@ float run(const uint8_t* in, uint8_t* out, long tiles, int blocks, int threads, 
 int main(int argc, char** argv) {
     const long n = argc > 1 ? atol(argv[1]) : 1000000;
     const long tiles = (n + 31) / 32;
+    g_rot = argc > 2 ? atoi(argv[2]) : 1;
+    g_in_stride = (tiles * kIn + 64 + 4095) / 4096 * 4096;
+    g_out_stride = (tiles * kOut + 64 + 4095) / 4096 * 4096;
+    std::printf("records %ld, input/output sets rotated: %d\n", n, g_rot);
     uint8_t *in, *out;
-    CK(hipMalloc(&in, tiles * kIn + 64));
-    CK(hipMalloc(&out, tiles * kOut + 64));
-    CK(hipMemset(in, 1, tiles * kIn + 64));
+    CK(hipMalloc(&in, g_in_stride * g_rot));
+    CK(hipMalloc(&out, g_out_stride * g_rot));
+    CK(hipMemset(in, 1, g_in_stride * g_rot));
     const double bytes = (double)tiles * (kIn + kOut);
     auto rep = [&](const char* name, float ms) {
         std::printf("%-44s %8.1f us  %6.0f GB/s\n", name, ms * 1e3, bytes / (ms * 1e-3) / 1e9);
@@ -78,6 +95,8 @@ int main(int argc, char** argv) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "persistent 1-wave WGs G=%d nt", g);
         rep(nm, run<2, 1>(in, out, tiles, g, 64, 20));
+        std::snprintf(nm, sizeof nm, "persistent 1-wave WGs G=%d nt + nt loads", g);
+        rep(nm, run<2, 1, true>(in, out, tiles, g, 64, 20));
         std::snprintf(nm, sizeof nm, "persistent 1-wave WGs G=%d default", g);
         rep(nm, run<0, 1>(in, out, tiles, g, 64, 20));
     }

@@ -107,13 +107,20 @@ def test_gpu_in_order_streams(codec, n, seed, cut):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["one_long", "many_long", "cross_every_block"])
+@pytest.mark.parametrize("layout", ["one_long", "many_long", "cross_every_block", "huge_group"])
 def test_gpu_long_groups(codec, layout):
     """Groups that span the scan's 1024-fragment blocks: one BEGIN..END group over several blocks
     with whole messages inside it (the group's start is blocks behind its END), many such groups,
     and short groups placed across every block boundary."""
-    rng = np.random.default_rng({"one_long": 31, "many_long": 32, "cross_every_block": 33}[layout])
-    if layout == "cross_every_block":
+    rng = np.random.default_rng({"one_long": 31, "many_long": 32, "cross_every_block": 33, "huge_group": 34}[layout])
+    if layout == "huge_group":  # one message of 60 000 fragments (59 blocks), singles inside and around it
+        g = np.zeros(60000, np.uint8)
+        g[0], g[-1] = 0x80, 0x40
+        g[rng.choice(np.arange(1, g.size - 1), size=500, replace=False)] = 0xC0
+        flags = np.concatenate([np.full(777, 0xC0, np.uint8), g, np.full(1500, 0xC0, np.uint8),
+                                np.array([0x80, 0x00], np.uint8)])  # and an open carry
+        n = flags.size
+    elif layout == "cross_every_block":
         n = 20 * 1024
         flags = np.full(n, 0xC0, np.uint8)
         for b in range(1024, n, 1024):  # BEGIN 2 before the boundary, middle(s), END 2 after it
@@ -199,3 +206,53 @@ def test_gpu_empty_and_zero_length(codec):
     off = np.zeros(6, np.uint64)
     data = np.zeros(1, np.uint8)
     assert gpu_reassemble(codec, data, off, flags) == T.oracle_reassemble(data, off, flags)
+
+
+@pytest.mark.gpu
+def test_gpu_huge_group_not_slower(codec):
+    """the fused scan launch finds the singles before a group that starts blocks earlier
+    from the exclusive block prefixes plus at most one block's flags (16 per load), not by walking
+    every flag between the group's start and its END's block.  A 1 M-fragment batch holding one
+    message of 500 000 fragments must reassemble about as fast as one of short groups (bound 3x,
+    on the median of several runs; the walk made it milliseconds), and bit-exact."""
+    import time
+
+    import torch
+    n = 1 << 20
+    rng = np.random.default_rng(41)
+
+    def stream(huge):
+        flags = np.full(n, 0xC0, np.uint8)
+        if huge:
+            a, b = 1000, 501000
+            flags[a:b] = 0x00
+            flags[a], flags[b - 1] = 0x80, 0x40
+            flags[rng.choice(np.arange(a + 1, b - 1), size=2000, replace=False)] = 0xC0
+        else:
+            for s in range(1000, n - 8, 97):
+                flags[s], flags[s + 1], flags[s + 2] = 0x80, 0x00, 0x40
+        off = np.arange(n + 1, dtype=np.uint64) * 64
+        return flags, off
+
+    data = torch.randint(0, 256, (64 * n,), dtype=torch.uint8, device="cuda")
+    times = {}
+    for huge in (False, True):
+        flags, off = stream(huge)
+        fl = torch.from_numpy(flags).cuda()
+        of = torch.from_numpy(off.view(np.int64)).cuda()
+        r = codec.reassemble(data, of, fl)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(7):
+            t0 = time.perf_counter()
+            codec.reassemble(data, of, fl)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        times[huge] = float(np.median(ts))
+        if huge:  # parity on this batch: metadata vs the oracle on the host copy
+            exp_msgs, exp_carry = T.oracle_reassemble(data.cpu().numpy(), off, flags)
+            got = gpu_reassemble(codec, data.cpu().numpy(), off, flags)
+            assert got == (exp_msgs, exp_carry)
+    print(f"reassembly 1 M fragments: short groups {times[False] * 1e3:.3f} ms, one 500 k-fragment group "
+          f"{times[True] * 1e3:.3f} ms")
+    assert times[True] < 3 * times[False] + 2e-4, times
