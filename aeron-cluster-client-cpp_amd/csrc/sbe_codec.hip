@@ -1914,8 +1914,8 @@ __device__ __forceinline__ void enc_pack_run(const EncArgs& a, uint64_t first, u
 // slower, profiles/r04_ab_vt.log; chunks did not recover it, see SBE_PACK_VT).  A virtual tile
 // the fast path cannot take (a record longer than a window, gather mode, a PUBLISH_TOPIC length
 // wrap) is written whole, window by window.
-#ifndef SBE_VT_CHUNK  // tiles per chunk (0: one contiguous range per workgroup)
-#define SBE_VT_CHUNK 4
+#ifndef SBE_VT_CHUNK  // tiles per chunk (0: one contiguous range per workgroup, the batch kernel's)
+#define SBE_VT_CHUNK 0
 #endif
 template <class LY, bool kPacked>
 __device__ __forceinline__ TileIn vt_load(const EncArgs& a, uint64_t r0, int lane) {
@@ -2163,14 +2163,36 @@ __device__ __forceinline__ void enc_pack_run_vt(const EncArgs& a, uint64_t first
 // 160, CommitOffsetLite 41 → 40-44 over chunk sizes 1-8 and contiguous ranges;
 // profiles/r04_ab_vt_chunks.log).  The serve kernel uses the virtual-tile loop (running offsets,
 // no tile sums).  SBE_PACK_VT=1 selects it for the batch kernel (A/B).
-#ifndef SBE_PACK_VT
+#ifndef SBE_PACK_VT  // A/B builds: 1 = always the virtual-tile loop, 2 = never; 0 = chosen per launch
 #define SBE_PACK_VT 0
 #endif
+// Which loop pays is a matter of the windows a tile takes: a tile whose output ends in a part-full
+// window pays that window's fixed cost (staging issue, store rows, fix-up passes) for little, and
+// the virtual-tile loop (one contiguous record range per workgroup), whose windows are all full,
+// wins; a tile of whole windows keeps the tile loop, which re-prepares nothing.  Measured on
+// rotated inputs, pack us tile -> virtual tiles (profiles/r06_ab_vt.log; the tile's average output
+// and its last window's fill in brackets): config 4's variable-length records 729.9 -> 695.3
+// (12.4 KiB, 0.54), session frames 136.2 -> 130.4 (17.9 KiB, 0.23), 626-B records 648.4 -> 622.0
+// (20 KiB, 0.45); fixed-256 95.6 -> 105.3 (8 KiB, one window), 502-B records 578.5 -> 600.0 (16 KiB,
+// 0.96), OrderRequestLite 143.7 -> 156.1 (21.3 KiB, 0.65), CommitOffsetLite 43.6 -> 44.2 (one
+// window).  So the kernel takes the virtual-tile loop when the average tile of the first
+// superblock (sbe_enc_sums' totals: a uniform read, the same choice in every workgroup) needs more
+// than one window and its last one is under 60 % full.
+template <class LY>
+__device__ __forceinline__ bool vt_pays(const EncArgs& a) {
+    SBE_TILE_SHAPE(LY);
+    const uint64_t n0 = a.n < (uint64_t)kSbRec ? a.n : (uint64_t)kSbRec;
+    if (n0 < (uint64_t)kRpt) return false;
+    const uint64_t t = uniform64(a.bsum[0]) * kRpt / n0;  // average output bytes of a tile
+    if (t <= (uint64_t)kEW) return false;
+    const uint64_t last = t - (t - 1) / kEW * kEW;        // bytes in the tile's last window
+    return 10 * last < 6 * (uint64_t)kEW;
+}
 template <class LY, bool kPacked, int kLen>
 __global__ __launch_bounds__(kWave, SBE_PACK_MIN_WAVES) void sbe_enc_pack(EncArgs a) {
     __shared__ PackLds<LY, kPacked> lds;
-    if (SBE_PACK_VT)
-        enc_pack_run_vt<LY, kPacked, kLen>(a, blockIdx.x, gridDim.x, lds);
+    if (SBE_PACK_VT == 1 || (SBE_PACK_VT == 0 && kPacked && vt_pays<LY>(a)))
+        enc_pack_run_vt<LY, kPacked, kLen>(a, blockIdx.x, gridDim.x, lds, SBE_VT_CHUNK);
     else
         enc_pack_run<LY, kPacked, kLen>(a, blockIdx.x, gridDim.x, lds);
 }
@@ -3250,7 +3272,14 @@ struct FragArgs {
     uint64_t* msize;   // [n + 1]
     uint64_t* mfirst;  // [n + 1] first fragment of message j
     uint64_t* mlast;   // [n + 1] last fragment (bit 63: a single sits inside the group)
+    uint64_t* big;     // big[0]: count, big[1..]: messages of >= kFcBig bytes without a single inside
+                       // (copied by every wave of frag_copy together); nullptr: none singled out
 };
+// A message (or the carry) this large is not copied by the one wave that holds its table entry:
+// frag_scan_msgs lists it, and frag_copy's waves copy the listed messages together in 64 KiB
+// pieces after their own groups.  One wave copies a few GB/s, so one 32 MB message took 12 ms
+// alone while a 1 M-fragment batch of short messages takes 0.1 ms (tests/test_reassembly.py).
+constexpr uint64_t kFcBig = 64 * 1024, kFcPiece = 64 * 1024;
 
 __device__ __forceinline__ bool frag_single(uint8_t f) {
     return (f & (SBE_FRAG_BEGIN | SBE_FRAG_END)) == (SBE_FRAG_BEGIN | SBE_FRAG_END);
@@ -3335,9 +3364,10 @@ __global__ __launch_bounds__(kFsThreads) void frag_reduce(FragArgs a, FragScan* 
 // kFsPer consecutive aggregates a thread (a million fragments' 977 aggregates in one pass; at 1024
 // threads a pass the scan's registers spilled: 21 us instead of a few)
 constexpr int kFsbThreads = kFsThreads;
-__global__ __launch_bounds__(kFsbThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb) {
+__global__ __launch_bounds__(kFsbThreads) void frag_scan_blocks(FragScan* agg, uint64_t nb, uint64_t* big) {
     __shared__ FragScan wt[kFsbThreads / kWave];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    if (big && tid == 0) big[0] = 0;  // the big-message list of frag_scan_msgs (next launch)
     FragScan carry = fs_identity();
     for (uint64_t c0 = 0; c0 < nb; c0 += kFsBlk) {
         const uint64_t j0 = c0 + (uint64_t)tid * kFsPer;
@@ -3445,6 +3475,39 @@ __global__ __launch_bounds__(256) void frag_messages(FragArgs a) {
 #ifndef SBE_FRAG_STAGE
 #define SBE_FRAG_STAGE 1
 #endif
+// Singles among fragments [0, x] for an x in an earlier block than b (rare: the start of a group
+// that crosses into block b; out of line, so its registers stay out of frag_scan_msgs): from the
+// nearer block boundary, counting the singles between it and x from 16-byte aligned flag loads (at
+// most kFsBlk / 32 + 1 independent loads; an aligned 16-B block holding a flag byte never crosses
+// a page): x's own block's exclusive prefix plus the singles in [its start, x], or the prefix of
+// the block after x's minus the singles in (x, that block's start).  Walking one flag at a time
+// from x up to block b cost thousands of loads for a group of thousands of fragments;
+// always counting from x's block start made every short group across a block boundary read its
+// whole block (reassembly row 146 -> 172 us, profiles/r06_ab_reasm_big.log).
+__device__ __noinline__ uint32_t frag_singles_before(const FragArgs& a, const FragScan* pre, uint64_t x, uint64_t b) {
+    const uint64_t bx = x / kFsBlk, s = bx * kFsBlk;
+    const bool fwd = x - s < s + kFsBlk - 1 - x;
+    const uint32_t c = fs_sg(fwd ? pre[bx] : pre[bx + 1]);  // bx + 1 <= b: pre[b] is the block's own prefix
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(a.flags + (fwd ? s : x + 1)),
+                    hi = reinterpret_cast<uintptr_t>(a.flags + (fwd ? x : s + kFsBlk - 1));
+    uint32_t cnt = 0;
+    for (uintptr_t q = lo & ~(uintptr_t)15; q <= hi && lo <= hi; q += 16) {
+        const uint4 w4 = gload128(q);
+        const uint32_t w0 = w4.x, w1 = w4.y, w2 = w4.z, w3 = w4.w;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t w = t == 0 ? w0 : t == 1 ? w1 : t == 2 ? w2 : w3;
+            const uintptr_t b0 = q + 4 * t;  // address of byte 0 of this dword
+            uint32_t m = (w >> 1) & w & 0x40404040u;  // bit 6 of a byte: BEGIN and END both set
+            if (b0 < lo) m &= lo - b0 >= 4 ? 0u : ~0u << (8 * (lo - b0));
+            if (b0 + 3 > hi) m &= b0 > hi ? 0u : byte_mask_bits((uint32_t)(hi - b0 + 1));
+            cnt += __builtin_popcount(m);
+        }
+    }
+    (void)b;
+    return fwd ? c + cnt : c - cnt;
+}
+
 __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const FragScan* pre) {
     __shared__ FragScan wt[kFsThreads / kWave];
     __shared__ uint32_t sgl[kFsBlk];  // inclusive singles count at every fragment of the block
@@ -3468,28 +3531,7 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
     }
     __syncthreads();
     auto sg_at = [&](uint64_t x) -> uint32_t {  // singles among fragments [0, x]
-        if (x >= blk0) return sgl[x - blk0];
-        // x lies in an earlier block: that block's exclusive prefix plus the singles from its first
-        // fragment through x, counted from 16-byte aligned flag loads (at most kFsBlk / 16 + 1
-        // independent loads; an aligned 16-B block holding a flag byte never crosses a page).
-        // Walking one flag at a time from x up to this block cost thousands of loads for a group
-        // of thousands of fragments.
-        const uint64_t s = x / kFsBlk * kFsBlk;
-        uint32_t c = fs_sg(pre[x / kFsBlk]);
-        const uintptr_t lo = reinterpret_cast<uintptr_t>(a.flags + s), hi = reinterpret_cast<uintptr_t>(a.flags + x);
-        for (uintptr_t q = lo & ~(uintptr_t)15; q <= hi; q += 16) {
-            const uint4 w4 = gload128(q);
-            const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const uintptr_t b0 = q + 4 * t;  // address of byte 0 of this dword
-                uint32_t m = (w[t] >> 1) & w[t] & 0x40404040u;  // bit 6 of a byte: BEGIN and END both set
-                if (b0 < lo) m &= lo - b0 >= 4 ? 0u : ~0u << (8 * (lo - b0));
-                if (b0 + 3 > hi) m &= b0 > hi ? 0u : byte_mask_bits((uint32_t)(hi - b0 + 1));
-                c += __builtin_popcount(m);
-            }
-        }
-        return c;
+        return x >= blk0 ? sgl[x - blk0] : frag_singles_before(a, pre, x, b);
     };
     auto group = [&](const FragScan& x, int64_t le_before, uint64_t& s0, bool& gap) {  // frag_group
         int64_t st = (int64_t)x.lb > le_before + 1 ? (int64_t)x.lb : le_before + 1;
@@ -3523,6 +3565,8 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
                 first = s0;
                 last = i | (gap ? (1ull << 63) : 0ull);
             }
+            if (a.big && !(last >> 63) && x.E - E0 >= kFcBig)  // rare: a few per batch at most
+                a.big[1 + atomicAdd(reinterpret_cast<unsigned long long*>(a.big), 1ull)] = j;
 #if SBE_FRAG_STAGE
             tj[k] = (uint32_t)(j - j0);
             tv[k][0] = x.E - E0;
@@ -3549,6 +3593,8 @@ __global__ __launch_bounds__(kFsThreads) void frag_scan_msgs(FragArgs a, const F
             a.mlast[m] = i | (gap ? (1ull << 63) : 0ull);
             a.counts[0] = m;
             a.counts[1] = open ? bytes : 0u;
+            if (a.big && open && !gap && bytes >= kFcBig)
+                a.big[1 + atomicAdd(reinterpret_cast<unsigned long long*>(a.big), 1ull)] = m;
         }
     }
 #if SBE_FRAG_STAGE
@@ -3708,16 +3754,19 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
         }
 #endif
         const bool gap = valid && (mlast >> 63);
+        // a listed big message (frag_scan_msgs) is copied by all waves after the loop: it takes no
+        // part in a run here, as a gapped message does not
+        const bool brk = gap || (a.big && valid && len >= kFcBig);
         // run membership: this message's source follows the previous one's (and neither is gapped)
         const uint64_t pend = __shfl_up(src + len, 1, kWave);
-        const bool pgap = __shfl_up(gap ? 1 : 0, 1, kWave) != 0;
-        const bool cont = lane > 0 && valid && !gap && !pgap && src == pend;
-        const uint64_t starts = __ballot(valid && !gap && !cont);
+        const bool pgap = __shfl_up(brk ? 1 : 0, 1, kWave) != 0;
+        const bool cont = lane > 0 && valid && !brk && !pgap && src == pend;
+        const uint64_t starts = __ballot(valid && !brk && !cont);
         const uint64_t vmask = __ballot(valid);
         for (uint64_t mk = starts; mk; mk &= mk - 1) {
             const int k = __builtin_ctzll(mk);
             // the run ends before the next start, gapped message or invalid lane
-            const uint64_t stop = (starts | __ballot(gap) | ~vmask) & ~((2ull << k) - 1);
+            const uint64_t stop = (starts | __ballot(brk) | ~vmask) & ~((2ull << k) - 1);
             const int e = stop ? __builtin_ctzll(stop) : kWave;  // first lane after the run
             const uint64_t D = uniform64(__shfl(dst, k, kWave));
             const uint64_t De = uniform64(__shfl(dst + len, e - 1, kWave));
@@ -3755,6 +3804,22 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
                 at += lane_u64(incl, kWave - 1);
             }
         }
+    }
+    // the listed big messages, in kFcPiece pieces dealt round robin over every wave of the grid
+    // (the list's order is the atomics' order: each message's pieces are disjoint whatever it is)
+    const uint64_t nbig = a.big ? uniform64(a.big[0]) : 0ull;
+    const uint64_t me = (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    uint64_t pbase = 0;  // pieces of the listed messages before message q
+    for (uint64_t q = 0; q < nbig; ++q) {
+        const uint64_t j = uniform64(a.big[1 + q]);
+        const uint64_t len = uniform64(a.msize[j]);
+        const uint64_t np = (len + kFcPiece - 1) / kFcPiece;
+        const uint64_t src = uniform64(a.frag_off[uniform64(a.mfirst[j])]), dst = uniform64(a.msg_off[j]);
+        for (uint64_t p = (me + waves - pbase % waves) % waves; p < np; p += waves) {
+            const uint64_t o = p * kFcPiece;
+            wave_copy16(a.out + dst + o, a.in + src + o, len - o < kFcPiece ? len - o : kFcPiece, lane);
+        }
+        pbase += np;
     }
 }
 
@@ -4713,11 +4778,16 @@ int sbe_reassemble_fragments(const uint8_t* in, const uint64_t* frag_off, const 
     uint64_t* mfirst = reinterpret_cast<uint64_t*>(w);
     w = al(w + 8 * (n + 1));
     uint64_t* mlast = reinterpret_cast<uint64_t*>(w);
-    FragArgs a{in, frag_off, flags, n, out, msg_off, counts, el, sc, msize, mfirst, mlast};
+    // the big-message list lives in sc[], which the fused scan does not use (n + 2 <= 4n words)
+#ifndef SBE_FRAG_BIG  // A/B builds: 0 = no big-message list (every message copied by its own wave)
+#define SBE_FRAG_BIG 1
+#endif
+    FragArgs a{in, frag_off, flags, n, out, msg_off, counts, el, sc, msize, mfirst, mlast,
+               SBE_FRAG_FUSED && SBE_FRAG_BIG ? reinterpret_cast<uint64_t*>(sc) : nullptr};
     const uint32_t blocks = (uint32_t)((n + 1 + 255) / 256);
     const uint64_t nb = (n + kFsBlk - 1) / kFsBlk;
     hipLaunchKernelGGL(frag_reduce, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, el);
-    hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsbThreads), 0, s, el, nb);
+    hipLaunchKernelGGL(frag_scan_blocks, dim3(1), dim3(kFsbThreads), 0, s, el, nb, a.big);
     hipError_t e = hipSuccess;
     if (SBE_FRAG_FUSED) {
         hipLaunchKernelGGL(frag_scan_msgs, dim3((uint32_t)nb), dim3(kFsThreads), 0, s, a, static_cast<const FragScan*>(el));
