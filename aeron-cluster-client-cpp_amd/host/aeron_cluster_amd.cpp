@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <ctime>
 #include <iomanip>
 #include <iostream>
@@ -1845,11 +1846,19 @@ void MessageParser::parse_batch(const std::uint8_t* data, const std::uint64_t* r
 }
 
 // ---- BatchingParser -------------------------------------------------------------------------
-// Two batches: one fills on the caller's thread while the other is decoded by the decode thread
-// (its own device context) or waits, decoded, for the caller's next poll() to deliver it.
+// One batch fills on the caller's thread; handed-off batches queue for the decode thread (its own
+// device context), which decodes them in order, and wait, decoded, for the caller's next poll() /
+// flush() to deliver them in order.  Options::batches batches are kept (more are made when the
+// caller hands off faster than it polls), so a decode overlaps both the next fill and the previous
+// delivery: with two batches a 1024-record batch's decode (a serve round trip, ~20 us) could not,
+// and each hand-off paid two futex wake-ups (the decode thread's, then the caller's): 23 M rec/s,
+// below one CPU thread of the restatement (profiles/r05_host_latency.log).  Waits spin on an
+// atomic for a while before they block (states change under the mutex, so a waiter that blocks
+// cannot miss the notification).  Handlers run only inside poll() / flush(): on_fragment never
+// delivers, so it never throws a handler's exception and never drops the fragment it is given.
 struct BatchingParser::Impl {
     using clk = std::chrono::steady_clock;
-    enum State { kFilling, kDecoding, kReady };
+    enum State : int { kFilling, kDecoding, kReady };
     struct Batch {
         // page-locked (a block of the library's pool, so a new parser reuses the blocks of earlier
         // ones instead of pinning fresh memory): the one-chunk decode reads it in place
@@ -1859,108 +1868,159 @@ struct BatchingParser::Impl {
         uint8_t* b() const { return static_cast<uint8_t*>(blk.get()); }
         std::vector<uint64_t> off{0};
         ParsedBatch pb;  // the device descriptors; ParseResults are built at delivery
-        State state = kFilling;
-        uint64_t seq = 0;
+        std::atomic<int> state{kFilling};
+        size_t done = 0;  // records already handed to the handler (a throwing handler resumes here)
         clk::time_point first{};
         std::exception_ptr err;
         size_t n() const { return off.size() - 1; }
         void reset() {
             bytes = 0;
             off.resize(1);
-            state = kFilling;
+            done = 0;
             err = nullptr;
+            pb = ParsedBatch();
+            state.store(kFilling, std::memory_order_release);
         }
     };
     Handler handler;
     Options opt;
-    Batch b[2];
-    ParseResult cur;  // the result handed to the handler (rewritten in place per record)
-    int fill = 0;
-    uint64_t next_seq = 0;
+    std::vector<std::unique_ptr<Batch>> all;  // every batch (owner)
+    std::vector<Batch*> spare;                // free batches (caller's thread)
+    std::deque<Batch*> inflight;              // handed off, oldest first (caller's thread)
+    Batch* cur = nullptr;                     // the filling batch
+    ParseResult res;  // the result handed to the handler (rewritten in place per record)
     uint64_t n_delivered = 0;
     mutable std::mutex m;
     std::condition_variable cv;
-    bool stop = false;
+    std::deque<Batch*> todo;                  // the decode thread's queue (under m)
+    std::atomic<size_t> todo_n{0};
+    std::atomic<bool> stop{false};
     std::thread worker;
 
     Impl(Handler h, Options o) : handler(std::move(h)), opt(o) {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");  // as every mirror entry point
         if (opt.max_records == 0) opt.max_records = 1;
-        for (Batch& x : b) x.off.reserve(opt.max_records + 1);
+        opt.batches = std::max<size_t>(2, std::min<size_t>(opt.batches, 64));
+        for (size_t i = 0; i < opt.batches; ++i) spare.push_back(make_batch());
+        cur = take();
         worker = std::thread([this] { run(); });
     }
     ~Impl() {
         {
             std::lock_guard<std::mutex> g(m);
-            stop = true;
+            stop.store(true);
         }
         cv.notify_all();
         worker.join();
     }
-    void run() {  // the decode thread
+    Batch* make_batch() {
+        all.push_back(std::make_unique<Batch>());
+        all.back()->off.reserve(opt.max_records + 1);
+        return all.back().get();
+    }
+    Batch* take() {
+        if (spare.empty()) return make_batch();
+        Batch* x = spare.back();
+        spare.pop_back();
+        return x;
+    }
+    // spin (up to opt.spin) on pred, then block on the condition variable
+    template <class Pred>
+    void wait_for(Pred pred) {
+        if (pred()) return;
+        const auto until = clk::now() + opt.spin;
+        while (clk::now() < until) {
+            for (int k = 0; k < 64; ++k) {
+                if (pred()) return;
+#if defined(__x86_64__)
+                __builtin_ia32_pause();
+#endif
+            }
+        }
         std::unique_lock<std::mutex> g(m);
+        cv.wait(g, pred);
+    }
+    void run() {  // the decode thread: batches in hand-off order
         for (;;) {
-            cv.wait(g, [&] { return stop || b[0].state == kDecoding || b[1].state == kDecoding; });
+            wait_for([&] { return stop.load() || todo_n.load(std::memory_order_acquire) > 0; });
             Batch* x = nullptr;
-            for (Batch& y : b)
-                if (y.state == kDecoding && (!x || y.seq < x->seq)) x = &y;
-            if (!x) return;  // stop, nothing left to decode
-            g.unlock();
+            {
+                std::lock_guard<std::mutex> g(m);
+                if (todo.empty()) {
+                    if (stop.load()) return;
+                    continue;
+                }
+                x = todo.front();
+                todo.pop_front();
+                todo_n.fetch_sub(1, std::memory_order_relaxed);
+            }
             try {
                 x->pb = MessageParser::decode_batch(x->b(), x->off.data(), x->n());
             } catch (...) {
                 x->err = std::current_exception();
             }
-            g.lock();
-            x->state = kReady;
+            {
+                std::lock_guard<std::mutex> g(m);
+                x->state.store(kReady, std::memory_order_release);
+            }
             cv.notify_all();
         }
     }
-    // the filling batch to the decode thread; the other batch (older) is delivered first if it is
-    // decoded, or waited for and then delivered: at most one batch decodes while the next fills
-    size_t hand_off() {
-        Batch& f = b[fill];
-        Batch& o = b[1 - fill];
-        size_t got = 0;
-        if (state(o) != kFilling) got = deliver_wait(o);
+    void hand_off() {  // the filling batch to the decode thread; filling goes on in a free batch
+        Batch* x = cur;
+        x->state.store(kDecoding, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> g(m);
-            f.state = kDecoding;
-            f.seq = next_seq++;
+            todo.push_back(x);
+            todo_n.fetch_add(1, std::memory_order_release);
         }
         cv.notify_all();
-        fill = 1 - fill;
-        return got;
+        inflight.push_back(x);
+        cur = take();
     }
-    size_t deliver_wait(Batch& x) {
-        {
-            std::unique_lock<std::mutex> g(m);
-            cv.wait(g, [&] { return x.state == kReady; });
-        }
-        return deliver(x);
-    }
-    size_t deliver(Batch& x) {  // caller's thread; x is kReady
-        const size_t n = x.n();
-        std::exception_ptr e = x.err;
-        if (e) {
+    // the oldest in-flight batch, decoded; a handler that throws leaves it at the front with `done`
+    // past the record that threw, so the next call resumes after it
+    size_t deliver_front() {
+        Batch& x = *inflight.front();
+        size_t got = 0;
+        if (x.err) {
+            std::exception_ptr e = x.err;
+            n_delivered += x.n() - x.done;  // the batch's records are consumed by the error
+            inflight.pop_front();
             x.reset();
+            spare.push_back(&x);
             std::rethrow_exception(e);
         }
         // each result built on this thread into one reused ParseResult right before its handler
         // (the record and the result stay in this core's cache; the reference's handler likewise
         // receives a ParseResult that lives for the call, src/cluster_client.cpp:1185-1190)
-        for (size_t i = 0; i < n; ++i) {
-            x.pb.result_into(i, cur);
-            handler(cur);
+        const size_t n = x.n();
+        while (x.done < n) {
+            const size_t i = x.done++;
+            ++n_delivered;
+            ++got;
+            x.pb.result_into(i, res);
+            handler(res);
         }
-        x.pb = ParsedBatch();
-        n_delivered += n;
+        inflight.pop_front();
         x.reset();
-        return n;
+        spare.push_back(&x);
+        return got;
     }
-    State state(const Batch& x) const {
-        std::lock_guard<std::mutex> g(m);
-        return x.state;
+    size_t deliver_ready() {  // in order, up to the first batch still decoding
+        size_t got = 0;
+        while (!inflight.empty() && inflight.front()->state.load(std::memory_order_acquire) == kReady)
+            got += deliver_front();
+        return got;
+    }
+    size_t deliver_all() {
+        size_t got = 0;
+        while (!inflight.empty()) {
+            Batch* x = inflight.front();
+            wait_for([&] { return x->state.load(std::memory_order_acquire) == kReady; });
+            got += deliver_front();
+        }
+        return got;
     }
 };
 
@@ -1968,18 +2028,20 @@ BatchingParser::BatchingParser(Handler handler) : BatchingParser(std::move(handl
 BatchingParser::BatchingParser(Handler handler, Options options)
     : impl_(std::make_unique<Impl>(std::move(handler), options)) {}
 BatchingParser::~BatchingParser() {
-    try {
-        flush();
-    } catch (...) {
+    for (int k = 0; k < 1000000; ++k) {  // every record given is delivered (a throwing handler's
+        try {                            // exception is dropped here: a destructor cannot throw)
+            flush();
+            return;
+        } catch (...) {
+        }
     }
 }
 
 void BatchingParser::on_fragment(const std::uint8_t* data, std::size_t length) {
     Impl& I = *impl_;
-    if (I.b[I.fill].n() > 0 &&
-        (I.b[I.fill].n() + 1 > I.opt.max_records || I.b[I.fill].bytes + length > I.opt.max_bytes))
+    if (I.cur->n() > 0 && (I.cur->n() + 1 > I.opt.max_records || I.cur->bytes + length > I.opt.max_bytes))
         I.hand_off();
-    Impl::Batch& f = I.b[I.fill];
+    Impl::Batch& f = *I.cur;
     if (f.bytes + length > f.cap) {  // grow, keeping the bytes already copied
         const size_t want = std::max(f.bytes + length, std::max(I.opt.max_bytes, (size_t)4096));
         std::shared_ptr<void> nb = PinnedPool::get().take(want);
@@ -1995,27 +2057,23 @@ void BatchingParser::on_fragment(const std::uint8_t* data, std::size_t length) {
 
 std::size_t BatchingParser::poll() {
     Impl& I = *impl_;
-    size_t got = 0;
-    Impl::Batch& o = I.b[1 - I.fill];
-    if (I.state(o) == Impl::kReady) got += I.deliver(o);
-    Impl::Batch& f = I.b[I.fill];
-    if (f.n() > 0 && Impl::clk::now() - f.first >= I.opt.max_delay) got += I.hand_off();
-    return got;
+    // the filling batch goes first when its deadline has passed, so its decode overlaps the
+    // delivery of the older ones
+    if (I.cur->n() > 0 && Impl::clk::now() - I.cur->first >= I.opt.max_delay) I.hand_off();
+    return I.deliver_ready();
 }
 
 std::size_t BatchingParser::flush() {
     Impl& I = *impl_;
-    size_t got = 0;
-    if (I.b[I.fill].n() > 0) got += I.hand_off();
-    Impl::Batch& o = I.b[1 - I.fill];  // the batch just handed off (or an older one)
-    if (I.state(o) != Impl::kFilling) got += I.deliver_wait(o);
-    return got;
+    if (I.cur->n() > 0) I.hand_off();
+    return I.deliver_all();
 }
 
 std::size_t BatchingParser::pending() const {
     const Impl& I = *impl_;
-    std::lock_guard<std::mutex> g(I.m);
-    return I.b[0].n() + I.b[1].n();
+    size_t p = I.cur->n();
+    for (const Impl::Batch* x : I.inflight) p += x->n() - x->done;
+    return p;
 }
 
 std::uint64_t BatchingParser::delivered() const { return impl_->n_delivered; }

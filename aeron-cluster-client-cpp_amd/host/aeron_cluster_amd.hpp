@@ -338,10 +338,13 @@ std::optional<AckInfo> decode_ack(const std::uint8_t* data, std::size_t len);
 // polls: on_fragment copies each one (the fragment is only valid during the poll callback) into
 // a page-locked batch; when the batch holds max_records records or max_bytes bytes, or at a poll()
 // whose oldest pending record has waited max_delay, the batch goes to a decode thread
-// (MessageParser::parse_batch into a reused vector) and filling continues in a second batch.
-// Handlers run on the caller's thread, in arrival order, inside poll() / flush() (never inside
-// on_fragment unless both batches are busy: then on_fragment waits for the older one and delivers
-// it first), with handler(result) == handler(MessageParser::parse_message(fragment)).
+// (MessageParser::decode_batch) and filling continues in another batch (`batches` are kept; more
+// are made when the caller hands off faster than it polls).  Handlers run on the caller's thread,
+// in arrival order, only inside poll() / flush(), with handler(result) ==
+// handler(MessageParser::parse_message(fragment)); on_fragment never runs a handler.  Waits spin
+// for `spin` before they block.  A handler that throws propagates out of poll() / flush(); the
+// records after it are delivered by the next call, none twice.  Call poll() after every poll of
+// the subscription (the reference's loop), or flush().
 // Added latency per record: at most max_delay + one batch decode after the poll that follows it
 // (a caller polling continuously), or whatever the caller waits between polls.
 class BatchingParser {
@@ -350,6 +353,8 @@ public:
         std::size_t max_records = 8192;
         std::size_t max_bytes = std::size_t(4) << 20;
         std::chrono::microseconds max_delay{200};
+        std::size_t batches = 4;               // batches kept (2..64)
+        std::chrono::microseconds spin{200};   // spin before blocking in a wait (0: block at once)
     };
     using Handler = std::function<void(const ParseResult&)>;
     explicit BatchingParser(Handler handler);

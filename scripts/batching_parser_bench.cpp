@@ -81,9 +81,12 @@ int main(int argc, char** argv) {
     struct Setting {
         size_t max_records;
         int max_delay_us;
+        size_t batches;
+        int spin_us;
     };
-    for (const Setting s : {Setting{1024, 100}, Setting{4096, 200}, Setting{8192, 200}, Setting{16384, 500},
-                            Setting{65536, 2000}}) {
+    for (const Setting s : {Setting{1024, 100, 2, 0}, Setting{1024, 100, 4, 200}, Setting{1024, 100, 8, 200},
+                            Setting{512, 50, 8, 200}, Setting{2048, 100, 4, 200}, Setting{4096, 200, 4, 200},
+                            Setting{8192, 200, 4, 200}, Setting{16384, 500, 4, 200}, Setting{65536, 2000, 4, 200}}) {
         if (only && s.max_records != only) continue;
         // one parser per setting, as an application keeps one: a warm-up pass (the decode thread's
         // device context and serve kernel, the page-locked pool), then the timed pass
@@ -95,6 +98,8 @@ int main(int argc, char** argv) {
         BatchingParser::Options o;
         o.max_records = s.max_records;
         o.max_delay = std::chrono::microseconds(s.max_delay_us);
+        o.batches = s.batches;
+        o.spin = std::chrono::microseconds(s.spin_us);
         BatchingParser bp(
             [&](const ParseResult& r) {
                 const size_t k = got - base;
@@ -127,9 +132,9 @@ int main(int argc, char** argv) {
         std::sort(lat.begin(), lat.end());
         const auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, (size_t)(q * lat.size()))]; };
         std::printf("{\"op\": \"batching_parser\", \"records\": %zu, \"poll_fragments\": 100, \"max_records\": %zu, "
-                    "\"max_delay_us\": %d, \"rec_per_s\": %.4g, \"vs_oracle_1thread\": %.2f, \"latency_us_p50\": %.1f, "
+                    "\"max_delay_us\": %d, \"batches\": %zu, \"spin_us\": %d, \"rec_per_s\": %.4g, \"vs_oracle_1thread\": %.2f, \"latency_us_p50\": %.1f, "
                     "\"latency_us_p99\": %.1f, \"latency_us_max\": %.1f, \"on_fragment_share\": %.2f, \"ok\": %s}\n",
-                    N, s.max_records, s.max_delay_us, N / (us * 1e-6), N / (us * 1e-6) / oracle_rate, pct(0.5), pct(0.99),
+                    N, s.max_records, s.max_delay_us, s.batches, s.spin_us, N / (us * 1e-6), N / (us * 1e-6) / oracle_rate, pct(0.5), pct(0.99),
                     lat.empty() ? 0.0 : lat.back(), in_us / us, (got - base == N && bad == 0) ? "true" : "false");
         std::fflush(stdout);
     }

@@ -252,16 +252,21 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
 
     // BatchingParser: the cases repeated, fed in polls of 1-100 fragments (the reference's
     // per-poll limit), delivered in order with results equal to parse_message's, under small
-    // batches (many hand-offs, on_fragment waiting for the older batch), the byte limit, the
-    // deadline, an explicit flush and the destructor's flush
+    // batches (many hand-offs, more batches in flight than are kept), the byte limit, the
+    // deadline, an explicit flush and the destructor's flush, 2 to 64 batches kept, with and
+    // without spinning waits
     {
         const size_t N = 5000;
         struct Setting {
             size_t max_records, max_bytes;
             int delay_us;
+            size_t batches;
+            int spin_us;
         };
-        for (const Setting st : {Setting{7, 1u << 20, 1000000}, Setting{4096, 1u << 20, 200},
-                                 Setting{8192, 3000, 1000000}, Setting{1, 1u << 20, 0}}) {
+        for (const Setting st : {Setting{7, 1u << 20, 1000000, 4, 200}, Setting{4096, 1u << 20, 200, 4, 200},
+                                 Setting{8192, 3000, 1000000, 4, 200}, Setting{1, 1u << 20, 0, 4, 200},
+                                 Setting{5, 1u << 20, 1000000, 2, 0}, Setting{3, 1u << 20, 0, 8, 50},
+                                 Setting{64, 1u << 20, 1000000, 64, 200}}) {
             size_t got = 0;
             bool ok = true;
             {
@@ -269,6 +274,8 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
                 o.max_records = st.max_records;
                 o.max_bytes = st.max_bytes;
                 o.max_delay = std::chrono::microseconds(st.delay_us);
+                o.batches = st.batches;
+                o.spin = std::chrono::microseconds(st.spin_us);
                 BatchingParser bp([&](const ParseResult& r) { ok = ok && same(r, single[got++ % cases.size()]); }, o);
                 uint64_t seed = 12345;
                 size_t fed = 0;
@@ -290,8 +297,54 @@ static void surface_tests(const std::vector<std::string>& f5, const std::vector<
             }  // destructor: flush
             CHECK(ok && got == N);
             if (!(ok && got == N))
-                std::fprintf(stderr, "  BatchingParser max_records %zu: %zu of %zu delivered, ok %d\n", st.max_records,
-                             got, N, (int)ok);
+                std::fprintf(stderr, "  BatchingParser max_records %zu batches %zu: %zu of %zu delivered, ok %d\n",
+                             st.max_records, st.batches, got, N, (int)ok);
+        }
+        // a handler that throws: the exception leaves the poll / flush that delivered
+        // the record; the records after it come with the next calls, in order, none twice
+        for (const size_t batches : {size_t(2), size_t(4)}) {
+            const size_t M = 3000;
+            size_t got = 0, throws = 0;
+            bool ok = true;
+            BatchingParser::Options o;
+            o.max_records = 64;
+            o.max_delay = std::chrono::microseconds(0);
+            o.batches = batches;
+            BatchingParser bp(
+                [&](const ParseResult& r) {
+                    const size_t k = got++;
+                    ok = ok && same(r, single[k % cases.size()]);
+                    if (k % 997 == 500) throw std::runtime_error("handler failure");
+                },
+                o);
+            size_t fed = 0;
+            while (fed < M) {
+                for (size_t k = 0; k < 50 && fed < M; ++k, ++fed) {
+                    const Case& c = cases[fed % cases.size()];
+                    try {
+                        bp.on_fragment(c.rec.empty() ? nullptr : c.rec.data(), c.rec.size());
+                    } catch (const std::runtime_error&) {
+                        ++throws;
+                    }
+                }
+                try {
+                    (void)bp.poll();
+                } catch (const std::runtime_error&) {
+                    ++throws;
+                }
+            }
+            for (int t = 0; t < 10; ++t) {
+                try {
+                    (void)bp.flush();
+                    break;
+                } catch (const std::runtime_error&) {
+                    ++throws;
+                }
+            }
+            CHECK(ok && got == M && throws == 3 && bp.delivered() == M && bp.pending() == 0);
+            if (!(ok && got == M && throws == 3))
+                std::fprintf(stderr, "  BatchingParser throwing handler, batches %zu: %zu of %zu, %zu throws, ok %d\n",
+                             batches, got, M, throws, (int)ok);
         }
     }
 
