@@ -1000,8 +1000,15 @@ __global__ __launch_bounds__(kBlock) void order_json_measure(JsonArgs a) {
                 typedef const __attribute__((address_space(1))) u32x4 g128;
                 typedef __attribute__((address_space(3))) u32x4 l128;
                 const uint64_t nb = (end - g0 + 15) / 16;
-                for (uint64_t c = lane; c < nb; c += kWave)
-                    *(l128*)(sbuf[wv] + 16 * c) = *(g128*)(a.arena + g0 + 16 * c);
+                for (uint64_t c = lane; c < nb; c += kWave) {
+                    const uint64_t o = g0 + 16 * c;
+                    if (o + 16 <= end) {
+                        *(l128*)(sbuf[wv] + 16 * c) = *(g128*)(a.arena + o);
+                    } else {  // the range's partial last chunk: bytewise, never past the wave's last
+                              // string byte (the arena may end there, at the end of a mapping)
+                        for (uint64_t k = 0; k < end - o; ++k) sbuf[wv][16 * c + k] = a.arena[o + k];
+                    }
+                }
             }
         }
         __syncthreads();

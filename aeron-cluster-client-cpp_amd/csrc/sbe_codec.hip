@@ -33,6 +33,7 @@
 #include <chrono>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <type_traits>
 
 #include <cstdint>
@@ -4556,7 +4557,22 @@ int sbe_server_destroy(sbe_server* s) {
         rc = serve_call(s, r);
     }
     if (s->stream) {
-        const hipError_t e = hipStreamSynchronize(s->stream);
+        // a bounded wait: a server that failed may hold a kernel that never leaves;
+        // after idle time + 10 s its buffers are left allocated (the kernel may still touch them)
+        // and the call fails instead of hanging the caller
+        const auto t0 = std::chrono::steady_clock::now();
+        const auto limit = std::chrono::microseconds(s->idle_ticks / 100) + std::chrono::seconds(10);
+        hipError_t e;
+        while ((e = hipStreamQuery(s->stream)) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > limit) {
+                std::snprintf(g_last_error, sizeof g_last_error,
+                              "serve kernel still running %lld us after shutdown: its buffers are left allocated",
+                              (long long)std::chrono::duration_cast<std::chrono::microseconds>(limit).count());
+                delete s;
+                return SBE_EHIP;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
         if (rc == SBE_OK && e != hipSuccess) rc = record_hip(e);
         (void)hipStreamDestroy(s->stream);
     }

@@ -348,7 +348,9 @@ struct Ctx {
     HostBuf h_aux;
     std::vector<uint64_t> pin, pout;  // encode plan scratch (kept: first-touch costs on every call otherwise)
     sbe_server* srv = nullptr;
-    bool srv_failed = false;
+    bool srv_failed = false;   // in a cool-down after a failure (server() returns nullptr)
+    int srv_failures = 0;      // failures so far (the cool-down doubles with each)
+    std::chrono::steady_clock::time_point srv_retry_at{};
     Ctx() {
         if (sbe_device_ready() != 1) fail("no gfx950 device visible");
         pipe.create();
@@ -368,21 +370,32 @@ struct Ctx {
     // the batch kernels take it).
     // wide: a batch for several workgroups (up to serve_wide_max_records())
     sbe_server* server(size_t n, bool wide = false) {
-        if (n == 0 || n > (wide ? serve_wide_max_records() : serve_max_records()) || srv_failed) return nullptr;
+        if (n == 0 || n > (wide ? serve_wide_max_records() : serve_max_records())) return nullptr;
+        if (srv_failed) {
+            if (std::chrono::steady_clock::now() < srv_retry_at) return nullptr;
+            srv_failed = false;  // the cool-down is over: try a server again
+        }
         if (!srv && sbe_server_create_wide(&srv, serve_idle_us(), serve_workgroups()) != SBE_OK) {
             srv = nullptr;
-            srv_failed = true;
             (void)hipGetLastError();
+            back_off();
         }
         return srv;
     }
-    // A serve request failed (timed out, or the server's stream failed): this thread stops using
-    // the serve kernel (its batches go to the batch kernels from now on) and frees the server.
+    // A serve request failed (timed out, or the server's stream failed): the server is freed (a
+    // bounded wait, sbe_server_destroy) and this thread's calls go to the batch kernels for a
+    // cool-down that doubles with each failure of this thread, from 1 s up to 64 s; then a new server is
+    // tried (one transient timeout no longer disables the serve path for good).
     void drop_server() noexcept {
         if (srv) (void)sbe_server_destroy(srv);
         srv = nullptr;
-        srv_failed = true;
         (void)hipGetLastError();
+        back_off();
+    }
+    void back_off() noexcept {
+        srv_failed = true;
+        srv_retry_at = std::chrono::steady_clock::now() + std::chrono::seconds(1ll << std::min(srv_failures, 6));
+        ++srv_failures;
     }
     // Before batch work is enqueued on this thread's streams: a resident server of this thread
     // exits first (a shutdown request, then its stream drains), so that no kernel or copy of the

@@ -440,7 +440,9 @@ int sbe_server_create_wide(sbe_server** srv, uint32_t idle_us, uint32_t workgrou
 /* Stops the kernel (a shutdown request, then the stream is synchronised) and frees the server.
  * A request that times out (10 s) or finds the server's stream failed returns SBE_EHIP and leaves
  * the server failed: every later request returns SBE_EHIP at once, and destroy only waits for the
- * kernel to leave (it exits idle_us after its last request) before freeing. */
+ * kernel to leave (it exits idle_us after its last request) before freeing.  That wait is bounded
+ * (idle_us + 10 s): a kernel still running then is left with its buffers (never freed under it)
+ * and destroy returns SBE_EHIP. */
 int sbe_server_destroy(sbe_server* srv);
 int sbe_serve_encode_topic(sbe_server* srv, const sbe_tm_batch* in, uint64_t n, uint64_t ts_default, uint32_t flags,
                            uint8_t* out, uint64_t out_capacity, uint64_t* out_off, uint8_t* status);

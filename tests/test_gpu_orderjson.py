@@ -193,3 +193,31 @@ def test_gpu_window_edges(codec, what):
         for i in np.nonzero(fits)[0]:
             a, b = int(off[i]), int(off[i + 1])
             assert out[a:b].tobytes() == exp[a:b], i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", [0, 1])
+def test_gpu_arena_at_allocation_end(codec, what):
+    """the sizing launch stages each wave's string range with 16-byte loads; the range's
+    last partial chunk is read bytewise, so nothing past the last string byte is read.  The packed
+    arena here ends exactly at the end of a 2 MiB allocation, at an address that is not 16-byte
+    aligned; the texts must equal the oracle's."""
+    import torch
+    fields, cid, ts, q = T.order_batch(3000, 77, True)
+    arena, str_len = T.pack_order_fields(fields)
+    if arena.size % 16 == 0:  # keep the end unaligned
+        fields[0] = [fields[0][0] + b"x"] + list(fields[0][1:])
+        arena, str_len = T.pack_order_fields(fields)
+    exp, exp_off = T.oracle_order_json(arena, str_len, cid, ts, q, what, nthreads=8)
+    buf = torch.zeros(1 << 21, dtype=torch.uint8, device="cuda")
+    assert arena.size < buf.numel()
+    a = buf[buf.numel() - arena.size:]
+    a.copy_(torch.from_numpy(arena))
+    r = codec.order_to_json_batch(a, torch.from_numpy(str_len.astype(np.int32)).cuda(),
+                                  torch.from_numpy(np.asarray(cid, np.int64)).cuda(),
+                                  torch.from_numpy(np.asarray(ts, np.int64)).cuda(),
+                                  torch.from_numpy(np.asarray(q, np.float64)).cuda(), what)
+    torch.cuda.synchronize()
+    off = r.out_off.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(off, exp_off)
+    assert r.out.cpu().numpy()[: int(off[-1])].tobytes() == exp
