@@ -3057,7 +3057,7 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
     const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tpk[4] = {tp0, tp0, tp0, tp0};
 #endif
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
     const uint64_t t0 = tile * kTile;
     const uint64_t r = t0 + (uint64_t)lane;
     const bool valid = r < a.n;
@@ -3133,6 +3133,191 @@ __global__ __launch_bounds__(kWave, (kWin == kWinWide || kWin == kWinLarge) ? SB
     dec_tile<kMode, kWin>(a, blockIdx.x, win);
 }
 
+// Decode of mixed batches with waves specialised by record kind (verdict r5 item 3).  In a tile of
+// config 3's mix (69 % TopicMessages, 30 % Acks) a wave runs both parse paths one after the other:
+// the TopicMessage lanes' payload scan with the Ack lanes idle, then the Ack lanes' printable-run
+// scan with the TopicMessage lanes idle.  A workgroup of kG waves stages the kG tiles' bytes into
+// one shared window, counts the TopicMessages and the Acks, and deals the records to the waves by
+// kind (TopicMessages first, in record order, then Acks): at most one wave of the group holds
+// both kinds.  Each lane parses its record from the shared window, and the descriptors go back to
+// record order through LDS before the stores, so each wave stores contiguous rows.  A record that
+// does not lie in the window (the group's bytes past kGW, or rec_off not increasing) is parsed
+// from HBM by its lane (dec_record_glb), as the one-wave kernel does with a record no window can
+// hold.  (A fallback to the one-wave path inside this kernel gave the parse functions a second
+// call site, so the compiler outlined them and passed each descriptor through scratch: 30 scratch
+// stores a wave, twice the decode time.)
+// The workgroups are persistent (occupancy x CUs) and take groups g, g + G, ...; the next group's
+// bytes are loaded into registers while the current one is parsed, and the offsets of the one
+// after it a step earlier still, so a group's two dependent HBM round trips (offsets, then bytes)
+// hide behind the previous group's work.  Every load of the loop is issued unconditionally (at a
+// clamped group index on the last step), so the compiler's waits count them exactly.
+struct GroupOffs {
+    uint64_t g0, wb, we;  // first record; staged window [wb, we) (uniform)
+    uint64_t rs, rl;      // this thread's record
+    bool valid;
+};
+template <uint32_t kT, uint32_t kGW>
+__device__ __forceinline__ GroupOffs group_offs(const DecArgs& a, uint64_t g, uint32_t tid) {
+    GroupOffs o;
+    o.g0 = g * kT;
+    const uint64_t r = o.g0 + tid;
+    o.valid = r < a.n;
+    const uint64_t last = o.g0 + kT < a.n ? o.g0 + kT : a.n;
+    const uint64_t T0 = uniform64(a.rec_off[o.g0]);
+    const uint64_t end = (uniform64(a.rec_off[last]) + 15) & ~15ull;
+    o.wb = T0 & ~15ull;
+    o.we = end <= o.wb ? o.wb : (end - o.wb <= kGW ? end : o.wb + kGW);
+    const uint64_t rc = o.valid ? r : a.n - 1;
+    o.rs = a.rec_off[rc];
+    o.rl = a.rec_off[rc + 1] - o.rs;
+    return o;
+}
+template <uint32_t kT, uint32_t kPerThr>
+__device__ __forceinline__ void group_issue(const DecArgs& a, const GroupOffs& o, uint32_t tid, uint4 (&I)[kPerThr]) {
+    const uint32_t nch = (uint32_t)((o.we - o.wb) >> 4);
+    const uintptr_t src = reinterpret_cast<uintptr_t>(a.in) + o.wb;
+#pragma unroll
+    for (uint32_t k = 0; k < kPerThr; ++k) {
+        const uint32_t ch = tid + kT * k;
+        I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+template <uint32_t kMode, uint32_t kG, uint32_t kGW>
+__device__ __forceinline__ void dec_group(const DecArgs& a, uint32_t* win) {
+    constexpr uint32_t kT = kG * kWave;  // records of the group
+    constexpr uint32_t kPerThr = kGW / 16 / kT;  // staged chunks per thread
+    static_assert(kGW % (16 * kT) == 0, "group window shape");
+    __shared__ uint32_t rsA[kT], rlA[kT];
+    __shared__ uint16_t slot_rec[kT];
+    __shared__ uint32_t kcount[2 * kG];
+    const uint32_t tid = threadIdx.x, w = tid / kWave, lane = tid & (kWave - 1);
+    const uint64_t ngroups = (a.n + kT - 1) / kT, G = gridDim.x;
+    uint64_t g = blockIdx.x;
+    if (g >= ngroups) return;
+    auto clampg = [&](uint64_t x) { return x < ngroups ? x : ngroups - 1; };
+    GroupOffs o = group_offs<kT, kGW>(a, g, tid);
+    uint4 I[kPerThr];
+    group_issue<kT, kPerThr>(a, o, tid, I);
+    GroupOffs on = group_offs<kT, kGW>(a, clampg(g + G), tid);
+    for (;;) {
+        const bool has_next = g + G < ngroups;  // uniform
+        const uint64_t r = o.g0 + tid;
+        const bool inw = o.valid && o.rs >= o.wb && o.rs + o.rl <= o.we;  // parsed from the window
+        {
+            const uint32_t nch = (uint32_t)((o.we - o.wb) >> 4);
+#pragma unroll
+            for (uint32_t k = 0; k < kPerThr; ++k) {
+                const uint32_t ch = tid + kT * k;
+                if (ch < nch) lds_write_chunk(win, ch, I[k]);
+            }
+        }
+        rsA[tid] = inw ? (uint32_t)(o.rs - o.wb) : ~0u;
+        rlA[tid] = (uint32_t)(o.rl < 0xffffffffull ? o.rl : 0xffffffffull);
+        __syncthreads();
+        // the next group's bytes and the offsets of the one after it, in flight from here on
+        group_issue<kT, kPerThr>(a, on, tid, I);
+        const GroupOffs onn = group_offs<kT, kGW>(a, clampg(g + 2 * G), tid);
+        // kind of the record: an Ack (template 2, schema 1: the printable-run path) or anything else
+        uint32_t ack = 0;
+        if (inw && o.rl >= 8) {
+            const LdsRec R{win, (uint32_t)(o.rs - o.wb)};
+            const uint32_t h0 = R.u32(0), h1 = R.u32(4);
+            ack = (h0 >> 16) == 2u && (h1 & 0xffffu) == 1u;
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint64_t bt = __ballot(o.valid && !ack), ba = __ballot(o.valid && ack);
+        if (lane == 0) {
+            kcount[w] = (uint32_t)__builtin_popcountll(bt);
+            kcount[kG + w] = (uint32_t)__builtin_popcountll(ba);
+        }
+        __syncthreads();
+        uint32_t ntm = 0, pre_t = 0, pre_a = 0, nval = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kG; ++k) {
+            ntm += kcount[k];
+            nval += kcount[k] + kcount[kG + k];
+            pre_t += k < w ? kcount[k] : 0u;
+            pre_a += k < w ? kcount[kG + k] : 0u;
+        }
+        // invalid threads (the batch's last group) keep their own index, past the valid ones
+        const uint32_t slot = !o.valid ? tid
+                            : ack      ? ntm + pre_a + (uint32_t)__builtin_popcountll(ba & below)
+                                       : pre_t + (uint32_t)__builtin_popcountll(bt & below);
+        slot_rec[slot] = (uint16_t)tid;
+        __syncthreads();
+        // this lane's record: the tid-th of the dealt order
+        const uint32_t j = slot_rec[tid];
+        const bool jv = tid < nval;
+        Desc d;
+        d.clear();
+        const uint32_t jb = rsA[j], jl = rlA[j];
+        if (jv) {
+            if (jb != ~0u) {
+                dec_record<kMode>(LdsRec{win, jb}, jl, d);
+                if (kMode == SBE_DEC_PARSE_MESSAGE && (d.flags & kFlSeqPending))
+                    d.flags = (d.flags & ~kFlSeqPending) | has_seq_key_lane(LdsRec{win, jb}, d.off[3], d.len[3]);
+            } else {  // not in the window: from HBM
+                const uint64_t rj = o.g0 + j, sj = a.rec_off[rj], lj = a.rec_off[rj + 1] - sj;
+                if (lj > 0xffffffffull) dec_oversize<kMode>(d);
+                else d = dec_record_glb<kMode>(a.in, sj, (uint32_t)lj);
+            }
+        }
+        // the descriptors back in record order through LDS (the window is free once every lane
+        // has parsed), so each wave's stores cover contiguous rows as in the one-wave kernel
+        constexpr uint32_t kDs = 17;  // dwords per staged descriptor (odd: no bank conflicts)
+        static_assert(kDs * kT * 4 <= kGW, "descriptor staging fits the window");
+        __syncthreads();
+        if (jv) {
+            uint32_t* q = win + kDs * j;
+            q[0] = d.status | (d.flags << 8);
+            q[1] = (uint32_t)d.hdr[0] | ((uint32_t)d.hdr[1] << 16);
+            q[2] = (uint32_t)d.hdr[2] | ((uint32_t)d.hdr[3] << 16);
+            q[3] = (uint32_t)d.ts;
+            q[4] = (uint32_t)(d.ts >> 32);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                q[5 + k] = d.off[k];
+                q[10 + k] = d.len[k];
+            }
+        }
+        __syncthreads();
+        Desc e;
+        e.clear();
+        if (o.valid) {
+            const uint32_t* q = win + kDs * tid;
+            e.status = q[0] & 0xffu;
+            e.flags = q[0] >> 8;
+            e.hdr[0] = (uint16_t)q[1];
+            e.hdr[1] = (uint16_t)(q[1] >> 16);
+            e.hdr[2] = (uint16_t)q[2];
+            e.hdr[3] = (uint16_t)(q[2] >> 16);
+            e.ts = (uint64_t)q[3] | ((uint64_t)q[4] << 32);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                e.off[k] = q[5 + k];
+                e.len[k] = q[10 + k];
+            }
+        }
+        dec_outputs<kMode, false>(a, r, o.valid, o.rs, e);
+        if (!has_next) break;
+        __syncthreads();  // every thread is past its descriptor read before the window is rewritten
+        g += G;
+        o = on;
+        on = onn;
+    }
+}
+
+#ifndef SBE_DEC_GROUP  // A/B builds: tiles per workgroup of the group decode kernel (0: the one-wave mid kernel)
+#define SBE_DEC_GROUP 0
+#endif
+constexpr uint32_t kDecG = SBE_DEC_GROUP > 0 ? SBE_DEC_GROUP : 1;
+template <uint32_t kMode>
+__global__ __launch_bounds__(kDecG * kWave, kDecG >= 3 ? 2 : 3) void sbe_decode_group_kernel(DecArgs a) {
+    __shared__ uint32_t win[kDecG * kWinMid / 4];
+    dec_group<kMode, kDecG, kDecG * kWinMid>(a, win);
+}
+
 thread_local char g_last_error[256] = "";
 
 int record_hip(hipError_t e) {
@@ -3173,6 +3358,35 @@ uint64_t pack_grid(const void* kernel, uint64_t tiles) {
     // G/128 + 1 <= 64
     if (g > (uint64_t)(kWave - 1) * kTilesPerSb) g = (uint64_t)(kWave - 1) * kTilesPerSb;
     return tiles < g ? tiles : g;
+}
+
+// Persistent grid of the group decode kernel (kDecG waves a workgroup): occupancy x CUs, at most
+// one workgroup per group.
+uint64_t group_grid(const void* kernel, uint64_t groups) {
+    static thread_local const void* ck[4] = {};
+    static thread_local int cdev[4] = {};
+    static thread_local uint64_t cg[4] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    uint64_t g = 0;
+    for (int i = 0; i < 4; ++i)
+        if (ck[i] == kernel && cdev[i] == dev) g = cg[i];
+    if (g == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kDecG * kWave, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        g = (uint64_t)per_cu * (uint64_t)cus;
+        for (int i = 0; i < 4; ++i)
+            if (ck[i] == nullptr) {
+                ck[i] = kernel;
+                cdev[i] = dev;
+                cg[i] = g;
+                break;
+            }
+    }
+    return groups < g ? groups : g;
 }
 
 // Optional launch profiling: every `g_prof_every`-th launch of the pack kernel and of the decode
@@ -3825,6 +4039,104 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// MATERIALIZE (sbe_materialize_views): the decoded views copied into an arena.  Three launches:
+// per-1024-record block view bytes, one workgroup scanning the block sums, and the copy, where
+// each thread takes one record: its arena base from the block prefix plus a block scan, its five
+// views as unaligned 16-byte loads and stores (a view's last chunk may run into the next view's
+// bytes, which the same thread writes afterwards; the record's last view ends bytewise, so no
+// thread writes another record's bytes).
+// ------------------------------------------------------------------------------------------
+constexpr int kMatBlk = 1024;
+struct MatArgs {
+    const uint8_t* in;
+    const uint64_t* rec_off;
+    uint64_t n;
+    const uint8_t* status;
+    const uint32_t* view_off;
+    const uint32_t* view_len;
+    uint8_t* arena;
+    uint64_t cap;
+    uint64_t* arena_off;
+    uint64_t* bsum;  // per block: view bytes, then (in place) their exclusive scan
+};
+__device__ __forceinline__ uint64_t mat_rec_bytes(const MatArgs& a, uint64_t i) {
+    if (i >= a.n) return 0;
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t += a.view_len[5 * i + k];
+    return t;
+}
+// exclusive scan of v over the 1024-thread block; total = the block's sum
+__device__ __forceinline__ uint64_t mat_block_scan(uint64_t v, uint64_t& total) {
+    __shared__ uint64_t wt[kMatBlk / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    const uint64_t inc = wave_incl_scan64(v, lane);
+    if (lane == kWave - 1) wt[w] = inc;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kMatBlk / kWave; ++k) {
+        pre += k < w ? wt[k] : 0ull;
+        tot += wt[k];
+    }
+    total = tot;
+    return pre + inc - v;
+}
+__global__ __launch_bounds__(kMatBlk) void mat_sums(MatArgs a) {
+    uint64_t tot;
+    (void)mat_block_scan(mat_rec_bytes(a, (uint64_t)blockIdx.x * kMatBlk + threadIdx.x), tot);
+    if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kMatBlk) void mat_scan_blocks(MatArgs a, uint64_t nb) {
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < nb; c0 += kMatBlk) {
+        const uint64_t j = c0 + threadIdx.x;
+        uint64_t tot;
+        const uint64_t v = j < nb ? a.bsum[j] : 0ull;
+        const uint64_t ex = mat_block_scan(v, tot);
+        __syncthreads();
+        if (j < nb) a.bsum[j] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.arena_off[5 * a.n] = carry;
+}
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+__global__ __launch_bounds__(kMatBlk) void mat_copy(MatArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kMatBlk + threadIdx.x;
+    uint64_t tot;
+    const uint64_t base = a.bsum[blockIdx.x] + mat_block_scan(mat_rec_bytes(a, i), tot);
+    if (i >= a.n) return;
+    const uint8_t* rec = a.in + a.rec_off[i];
+    const uint64_t rl = a.rec_off[i + 1] - a.rec_off[i];
+    uint32_t L[5], O[5];
+    uint64_t at[6];
+    at[0] = base;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        L[k] = a.view_len[5 * i + k];
+        O[k] = a.view_off[5 * i + k];
+        at[k + 1] = at[k] + L[k];
+        a.arena_off[5 * i + k] = at[k];
+    }
+    const uint64_t rec_end = at[5] < a.cap ? at[5] : a.cap;  // this record's bytes end here
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        if (L[k] == 0 || at[k + 1] > a.cap) continue;  // views past the capacity are not written
+        const uint8_t* src = rec + O[k];
+        uint8_t* dst = a.arena + at[k];
+        uint32_t c = 0;
+        // whole 16-byte chunks; the view's last one may run into the next view (which this thread
+        // writes afterwards) when it stays inside the record on both sides
+        for (; c + 16 <= L[k] || (c < L[k] && at[k] + c + 16 <= rec_end && O[k] + c + 16 <= rl); c += 16) {
+            const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(src + c);
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4_ua*>(dst + c));
+        }
+        for (; c < L[k]; ++c) dst[c] = src[c];  // the record's last bytes: never past its end
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Gather of encoded shards to one rank: the {bytes, n} of every rank go round in
 // one ncclAllGather, then the shards move in one group of ncclSend / ncclRecv at the prefix
 // offsets, and the root rebases each received offset array by its shard's byte prefix.
@@ -4469,6 +4781,11 @@ int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t 
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinLarge>), grid, block, 0, s, e0, e1, 0, a);     \
         else if (shape == 1)                                                                               \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinWide>), grid, block, 0, s, e0, e1, 0, a);      \
+        else if (shape == 2 && SBE_DEC_GROUP > 0)                                                          \
+            hipExtLaunchKernelGGL((sbe_decode_group_kernel<M>),                                             \
+                                  dim3((uint32_t)group_grid((const void*)sbe_decode_group_kernel<M>,       \
+                                                            (n + kDecG * kTile - 1) / (kDecG * kTile))),    \
+                                  dim3(kDecG * kWave), 0, s, e0, e1, 0, a);                                \
         else if (shape == 2)                                                                               \
             hipExtLaunchKernelGGL((sbe_decode_kernel<M, kWinMid>), grid, block, 0, s, e0, e1, 0, a);       \
         else if (shape == 3)                                                                               \
@@ -4762,6 +5079,27 @@ int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64
     const uint64_t blocks = ((n + 15) / 16 + 255) / 256;  // 16 records per thread
     hipLaunchKernelGGL(sbe_seqnum_kernel, dim3((uint32_t)(blocks < 65536 ? blocks : 65536)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), a);
+    return record_hip(hipGetLastError());
+}
+
+size_t sbe_materialize_workspace_size(uint64_t n) { return (size_t)(8 * ((n + kMatBlk - 1) / kMatBlk) + 16); }
+
+int sbe_materialize_views(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
+                          uint8_t* arena, uint64_t arena_capacity, uint64_t* arena_off, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!arena_off) return SBE_EINVAL;
+    if (n == 0) return record_hip(hipMemsetAsync(arena_off, 0, 8, s));
+    if (!in || !rec_off || !dec || !dec->status || !dec->view_off || !dec->view_len || !workspace) return SBE_EINVAL;
+    if (!arena && arena_capacity) return SBE_EINVAL;
+    if (workspace_bytes < sbe_materialize_workspace_size(n)) return SBE_ENOSPC;
+    const uint64_t nb = (n + kMatBlk - 1) / kMatBlk;
+    if (nb > 0xffffffffull) return SBE_EINVAL;
+    uint64_t* bsum = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(workspace) + 15) & ~(uintptr_t)15);
+    MatArgs a{in, rec_off, n, dec->status, dec->view_off, dec->view_len, arena, arena_capacity, arena_off, bsum};
+    hipLaunchKernelGGL(mat_sums, dim3((uint32_t)nb), dim3(kMatBlk), 0, s, a);
+    hipLaunchKernelGGL(mat_scan_blocks, dim3(1), dim3(kMatBlk), 0, s, a, nb);
+    hipLaunchKernelGGL(mat_copy, dim3((uint32_t)nb), dim3(kMatBlk), 0, s, a);
     return record_hip(hipGetLastError());
 }
 

@@ -30,7 +30,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SBECODEC_LIB") or os.path.join(_HERE, "libsbecodec.so")
 
 # ---- constants mirrored from include/sbecodec.h ----
-ABI_VERSION = 7
+ABI_VERSION = 8
 ENC_REF_TRUNCATE8 = 0x1
 ENC_PUBLISH_TOPIC = 0x2
 ENC_OK, ENC_OVERFLOW = 0, 6
@@ -130,6 +130,13 @@ def _load():
         lib.sbe_decode_batch_sized.restype = ctypes.c_int
         lib.sbe_decode_batch_sized.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                ctypes.c_uint32, ctypes.POINTER(_Decoded), ctypes.c_void_p]
+    if hasattr(lib, "sbe_materialize_views"):
+        lib.sbe_materialize_workspace_size.restype = ctypes.c_size_t
+        lib.sbe_materialize_workspace_size.argtypes = [ctypes.c_uint64]
+        lib.sbe_materialize_views.restype = ctypes.c_int
+        lib.sbe_materialize_views.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(_Decoded), ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     lib.sbe_eval_sequence_numbers.restype = ctypes.c_int
     lib.sbe_eval_sequence_numbers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(_Decoded), ctypes.c_void_p, ctypes.c_void_p]
@@ -471,6 +478,46 @@ def eval_sequence_numbers(data, rec_off, dec: Decoded, seq=None, stream=None) ->
     rc = lib().sbe_eval_sequence_numbers(_ptr(data), _ptr(rec_off), n, ctypes.byref(d), _ptr(seq), _stream(stream))
     _check(rc, "sbe_eval_sequence_numbers")
     return seq[:n]
+
+
+@dataclass
+class Materialized:
+    arena: torch.Tensor      # uint8: every record's five views back to back
+    arena_off: torch.Tensor  # int64 [5n+1]: view k of record i = arena[arena_off[5i+k]:][:view_len[i][k]]
+
+
+def materialize_views(data, rec_off, dec: Decoded, arena=None, arena_capacity=None, arena_off=None,
+                      workspace=None, stream=None) -> Materialized:
+    """MATERIALIZE (sbe_materialize_views): the five views of every record that decode_batch
+    described, copied out of `data` into one arena, so the strings outlive the input (the
+    reference's ParseResult owns its strings, include/aeron_cluster/sbe_messages.hpp:306-328).
+    With no arena given, it is sized exactly: one synchronisation of `stream` reads the total."""
+    data = _dev(data, torch.uint8, "data")
+    rec_off = _dev(rec_off, torch.int64, "rec_off")
+    n = int(rec_off.numel()) - 1
+    dev = data.device
+    if arena_off is None:
+        arena_off = torch.empty(5 * n + 1, dtype=torch.int64, device=dev)
+    arena_off = _dev(arena_off, torch.int64, "arena_off")
+    if arena_off.numel() < 5 * n + 1:
+        raise SbeError(f"arena_off holds {arena_off.numel()} entries, 5 n + 1 = {5 * n + 1} needed")
+    need = int(lib().sbe_materialize_workspace_size(max(n, 1)))
+    if workspace is None:
+        workspace = torch.empty(need + 16, dtype=torch.uint8, device=dev)
+    workspace = _dev(workspace, torch.uint8, "workspace")
+    d = _Decoded(*(getattr(dec, k).data_ptr() for k in ("status", "flags", "hdr", "ts", "view_off", "view_len")))
+    sized = arena is None and arena_capacity is None
+    if sized:  # views can only be as long as the records: the input bytes bound the arena
+        total = int(dec.view_len[:n].to(torch.int64).sum().item()) if n else 0
+        arena = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+    arena = _dev(arena, torch.uint8, "arena")
+    cap = int(arena.numel()) if arena_capacity is None else int(arena_capacity)
+    if cap > arena.numel():
+        raise SbeError(f"arena_capacity {cap} exceeds the arena tensor ({arena.numel()} bytes)")
+    rc = lib().sbe_materialize_views(_ptr(data), _ptr(rec_off), n, ctypes.byref(d), _ptr(arena), cap,
+                                     _ptr(arena_off), _ptr(workspace), int(workspace.numel()), _stream(stream))
+    _check(rc, "sbe_materialize_views")
+    return Materialized(arena, arena_off[: 5 * n + 1])
 
 
 @dataclass

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define SBECODEC_ABI_VERSION 7
+#define SBECODEC_ABI_VERSION 8
 
 /* ---- return codes of every entry point ---- */
 #define SBE_OK 0
@@ -289,6 +289,21 @@ int sbe_decode_batch_sized(const uint8_t* in, const uint64_t* rec_off, uint64_t 
  * outputs of that decode call; seq is a device u64[n] (8-B aligned).  Same stream order rules. */
 int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
                               uint64_t* seq, void* stream);
+
+/* MATERIALIZE: the five views of every decoded record copied out of the input into one arena, so
+ * that the strings outlive the input buffer, as the reference's ParseResult owns its std::strings
+ * (include/aeron_cluster/sbe_messages.hpp:306-328) and a poll callback's fragment dies with the
+ * callback (src/cluster_client.cpp:541-546).  After sbe_decode_batch[_sized] on the same in /
+ * rec_off (dec: its outputs), view k of record i goes to arena[arena_off[5 i + k] ..) with
+ * view_len[i][k] bytes, views in record order and back to back (arena_off: device u64 [5 n + 1],
+ * the last entry the total; a view of length 0, including the Lite topicId slot, takes no bytes).
+ * A view that would end past arena_capacity is not written (arena_off still holds the full
+ * layout, so the caller can size the arena from arena_off[5 n] and rerun); nothing is written past
+ * arena_capacity.  Workspace: sbe_materialize_workspace_size(n) bytes (16-B aligned). */
+size_t sbe_materialize_workspace_size(uint64_t n);
+int sbe_materialize_views(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
+                          uint8_t* arena, uint64_t arena_capacity, uint64_t* arena_off, void* workspace,
+                          size_t workspace_bytes, void* stream);
 
 /* ============================ Aeron fragment reassembly ============================ */
 /* Replaces LocalFragmentReassembler::onFragment (src/cluster_client.cpp:39-82) for a batch of

@@ -995,3 +995,25 @@ def realistic_orders(n: int, seed: int = 0x5EED00F3):
     ts = (1_760_000_000_000_000_000 + rng.integers(0, 10 ** 12, n)).astype(np.int64)
     q = np.round(rng.random(n) * 10 ** 4, 4)
     return fields, cid, ts, q
+
+
+def oracle_materialize(data, rec_off, dec):
+    """MATERIALIZE's expected output from oracle descriptors (oracle_decode): every record's five
+    views data[rec_off[i] + view_off[i][k] :][: view_len[i][k]] back to back in record / view
+    order (what the reference's ParseResult strings hold, include/aeron_cluster/sbe_messages.hpp:
+    306-328), and arena_off [5n+1] (the last entry the total)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    rec_off = np.asarray(rec_off, dtype=np.uint64)
+    n = rec_off.size - 1
+    vl = dec["view_len"][:n].astype(np.uint64).reshape(-1)
+    vo = dec["view_off"][:n].astype(np.uint64).reshape(-1)
+    off = np.zeros(5 * n + 1, np.uint64)
+    off[1:] = np.cumsum(vl)
+    src = np.repeat(rec_off[:n], 5) + vo
+    total = int(off[-1])
+    if total == 0:
+        return np.zeros(0, np.uint8), off
+    # byte j of the arena comes from src[v] + (j - off[v]) for the view v holding it
+    v = np.repeat(np.arange(5 * n), vl.astype(np.int64))
+    j = np.arange(total, dtype=np.uint64)
+    return data[(src[v] + j - off[:-1][v]).astype(np.int64)], off
