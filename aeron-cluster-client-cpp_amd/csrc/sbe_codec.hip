@@ -2895,6 +2895,9 @@ __device__ __forceinline__ uint32_t dec_commit(uint32_t* win, uint64_t wb, uint6
 #pragma unroll
         for (int k = 0; k < dec_regs<kW>(); ++k) {
             if ((uint32_t)k < nrow) {
+                // (the key-slice compares as wave masks, v_cmp + s_or_b64 per dword instead of
+                // xors and v_min3, read config 4 decode 407.0 -> 439.6 us: the scalar ors issue
+                // from the same wave, profiles/r06_ab_cmp.log)
                 Suspect S;
                 S.add(I[k]);
                 sm |= S.any() ? 1u << k : 0u;
