@@ -38,7 +38,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 def test_host_side_entry_points(lib):
     lib.sbe_abi_version.restype = ctypes.c_int
-    assert lib.sbe_abi_version() == 7
+    assert lib.sbe_abi_version() == 8
     lib.sbe_encode_workspace_size.restype = ctypes.c_size_t
     lib.sbe_encode_workspace_size.argtypes = [ctypes.c_uint64]
     assert lib.sbe_encode_workspace_size(1_000_000) >= 16 * (1_000_000 // 256)
