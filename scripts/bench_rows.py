@@ -9,7 +9,10 @@ algorithmic bytes per launch (computed from the actual record sizes) and its fra
   order_json             1 M Orders → Order::to_json payload + publish_order headers JSON (two calls)
   reassemble             1 M Aeron fragments (90 % whole messages, the rest BEGIN..END groups),
                          BEGIN/END reassembly (all its launches, torch events around the call)
-Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...]  (GPU only)
+Rows whose buffers fit the 256 MB MALL a few times over rotate over --rotate (3) copies of their
+inputs and outputs (step k uses copy k mod R), as bench.py does, so no step finds its inputs in the
+cache a previous step left them in; config 4's 16.8 M-record batch (~6.5 GB) needs no rotation.
+Usage: python scripts/bench_rows.py [--steps K] [--rows a,b,...] [--rotate R]  (GPU only)
 """
 import argparse
 import json
@@ -50,6 +53,22 @@ def timed(fn, steps, warmup):
     return el / steps, (float(np.mean(pack)) if pack else None), (float(np.mean(deck)) if deck else None)
 
 
+ROT = 3  # --rotate
+
+
+class Rot:
+    """R copies of a row's device buffers; next() is the copy for the next step."""
+
+    def __init__(self, make):
+        self.sets = [make(k) for k in range(max(ROT, 1))]
+        self.k = 0
+
+    def next(self):
+        x = self.sets[self.k % len(self.sets)]
+        self.k += 1
+        return x
+
+
 CPU_THREADS = 16
 CPU_SECONDS = 3.0
 NO_CPU = False  # --no-cpu: skip the CPU baselines (profiling runs)
@@ -75,7 +94,8 @@ _cpu = None
 
 def line(row, n, step_s, kernels):
     global _cpu
-    out = {"row": row, "records": n, "records_per_s": n / step_s, "ms_per_step": step_s * 1e3, "kernels": {}}
+    out = {"row": row, "records": n, "records_per_s": n / step_s, "ms_per_step": step_s * 1e3,
+           "input_sets": 1 if row == "config4_var_roundtrip" else max(ROT, 1), "kernels": {}}
     if _cpu is not None:
         out["cpu_baseline"] = _cpu
         _cpu = None
@@ -97,11 +117,15 @@ def set_cpu(value, sample, cores=CPU_THREADS):
 def row_mixed(steps, warmup):
     n = 1_000_000
     data, off = T.mixed_records(n)
-    d, o = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
-    out = sbecodec.alloc_decoded(n, "cuda")
+    d0, o0 = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
+    R = Rot(lambda k: (d0.clone(), o0.clone(), sbecodec.alloc_decoded(n, "cuda")))
     nb = int(off[-1])
-    s, _, dk = timed(lambda: sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out, in_bytes=nb), steps,
-                     warmup)
+
+    def step():
+        d, o, out = R.next()
+        sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=out, in_bytes=nb)
+
+    s, _, dk = timed(step, steps, warmup)
     k = 200_000
     dk_, ok_ = data[: int(off[k])], off[: k + 1]
     set_cpu(cpu_rate(lambda: T.oracle_decode(dk_, ok_, T.DEC_PARSE, nthreads=CPU_THREADS), k),
@@ -140,14 +164,15 @@ def row_var(steps, warmup):
 def row_session(steps, warmup):
     n = 1_000_000
     arena, L, ts = T.fixed256_orders(n)
-    a, l, t = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32), dev(ts.view(np.int64), torch.int64)
-    ob = torch.empty(sbecodec.output_bound(n, arena.size), dtype=torch.uint8, device="cuda")
-    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    a0, l0, t0 = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32), dev(ts.view(np.int64), torch.int64)
     ws = sbecodec.alloc_workspace(n, "cuda")
-    dec = sbecodec.alloc_decoded(n, "cuda")
+    R = Rot(lambda k: (a0.clone(), l0.clone(), t0.clone(),
+                       torch.empty(sbecodec.output_bound(n, arena.size), dtype=torch.uint8, device="cuda"),
+                       torch.empty(n + 1, dtype=torch.int64, device="cuda"),
+                       torch.empty(n, dtype=torch.uint8, device="cuda"), sbecodec.alloc_decoded(n, "cuda")))
 
     def step():
+        a, l, t, ob, oo, st, dec = R.next()
         sbecodec.encode_session_batch(a, l, t, 7, 8, out=ob, out_off=oo, status=st, workspace=ws)
         sbecodec.decode_batch(ob, oo, sbecodec.DEC_PARSE_MESSAGE, out=dec, in_bytes=n * (32 + 248))
 
@@ -169,17 +194,18 @@ def row_lite(t_id, steps, warmup):
     n = 1_000_000
     nf = T.LITE_NF[t_id]
     arena, L, tid, seq = T.lite_records(n, t_id)
-    a, l = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32)
-    ti, sq = dev(tid.view(np.int32), torch.int32), dev(seq.view(np.int64), torch.int64)
+    a0, l0 = dev(arena, torch.uint8), dev(L.view(np.int32), torch.int32)
+    ti0, sq0 = dev(tid.view(np.int32), torch.int32), dev(seq.view(np.int64), torch.int64)
     cap = arena.size + (20 + 2 * nf) * n + 16
-    ob = torch.empty(cap, dtype=torch.uint8, device="cuda")
-    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    st = torch.empty(n, dtype=torch.uint8, device="cuda")
     ws = sbecodec.alloc_workspace(n, "cuda")
-    dec = sbecodec.alloc_decoded(n, "cuda")
     outb = arena.size + (20 + 2 * nf) * n
+    R = Rot(lambda k: (a0.clone(), l0.clone(), ti0.clone(), sq0.clone(),
+                       torch.empty(cap, dtype=torch.uint8, device="cuda"),
+                       torch.empty(n + 1, dtype=torch.int64, device="cuda"),
+                       torch.empty(n, dtype=torch.uint8, device="cuda"), sbecodec.alloc_decoded(n, "cuda")))
 
     def step():
+        a, l, ti, sq, ob, oo, st, dec = R.next()
         sbecodec.encode_lite_batch(t_id, a, l, ti, sq, out=ob, out_off=oo, status=st, workspace=ws)
         sbecodec.decode_batch(ob, oo, sbecodec.DEC_LITE, out=dec, in_bytes=outb)
 
@@ -200,11 +226,14 @@ def row_reassemble(steps, warmup):
     n = 1_000_000
     # 90 % whole messages, 10 % BEGIN..END groups of 2-5 fragments, no strays
     data, off, flags = T.fragment_stream(n, 11, p_single=0.9, maxlen=512, p_group=0.1)
-    d, o, f = dev(data, torch.uint8), dev(off.view(np.int64), torch.int64), dev(flags, torch.uint8)
-    out = torch.empty(max(data.size, 16), dtype=torch.uint8, device="cuda")
-    mo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    d0, o0, f0 = dev(data, torch.uint8), dev(off.view(np.int64), torch.int64), dev(flags, torch.uint8)
     ws = torch.empty(int(sbecodec.lib().sbe_reassemble_workspace_size(n)), dtype=torch.uint8, device="cuda")
-    fn = lambda: sbecodec.reassemble(d, o, f, out=out, msg_off=mo, workspace=ws)  # noqa: E731
+    R = Rot(lambda k: (d0.clone(), o0.clone(), f0.clone(), torch.empty(max(data.size, 16), dtype=torch.uint8, device="cuda"),
+                       torch.empty(n + 1, dtype=torch.int64, device="cuda")))
+
+    def fn():
+        d, o, f, out, mo = R.next()
+        sbecodec.reassemble(d, o, f, out=out, msg_off=mo, workspace=ws)
     for _ in range(warmup):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -231,14 +260,22 @@ def row_order_json(steps, warmup):
     n = 1_000_000
     fields, cid, ts, q = T.realistic_orders(n)
     arena, str_len = T.pack_order_fields(fields)
-    args = (dev(arena, torch.uint8), dev(str_len.astype(np.int32), torch.int32), dev(cid, torch.int64),
-            dev(ts, torch.int64), torch.from_numpy(q).cuda())
-    outs = {}
-    for what in (sbecodec.JSON_ORDER_PAYLOAD, sbecodec.JSON_PUBLISH_HEADERS):
-        r = sbecodec.order_to_json_batch(*args, what=what)
-        outs[what] = r
-    fn = lambda: [sbecodec.order_to_json_batch(*args, what=w, out=outs[w].out, out_off=outs[w].out_off,  # noqa: E731
-                                               status=outs[w].status) for w in outs]
+    args0 = (dev(arena, torch.uint8), dev(str_len.astype(np.int32), torch.int32), dev(cid, torch.int64),
+             dev(ts, torch.int64), torch.from_numpy(q).cuda())
+
+    def make(k):
+        args = tuple(x.clone() for x in args0)
+        outs = {w: sbecodec.order_to_json_batch(*args, what=w)
+                for w in (sbecodec.JSON_ORDER_PAYLOAD, sbecodec.JSON_PUBLISH_HEADERS)}
+        return args, outs
+
+    R = Rot(make)
+    outs = R.sets[0][1]
+
+    def fn():
+        args, os_ = R.next()
+        for w in os_:
+            sbecodec.order_to_json_batch(*args, what=w, out=os_[w].out, out_off=os_[w].out_off, status=os_[w].status)
     for _ in range(warmup):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -269,7 +306,10 @@ def main():
     ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
     ap.add_argument("--lib", help="library build to measure (A/B of variants; default: the product's)")
+    ap.add_argument("--rotate", type=int, default=3, help="copies of a row's buffers the steps rotate over")
     args = ap.parse_args()
+    global ROT
+    ROT = args.rotate
     if args.lib:
         sbecodec.use_library(os.path.abspath(args.lib))
     global NO_CPU
