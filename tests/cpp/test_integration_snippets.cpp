@@ -6,6 +6,7 @@
 // snippet's text unchanged.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -60,6 +61,19 @@ void snippet_parse_batch() {
 void snippet_batching_parser() {
     auto message_callback_ = [](const aeron_cluster::ParseResult&) {};
 #include "snip_batching_parser.inc"
+}
+
+void snippet_materialize() {
+    std::uint64_t n = 0, arena_capacity = 0;
+    const std::uint8_t* d_in = nullptr;
+    const std::uint64_t* d_rec_off = nullptr;
+    sbe_decoded dec{};
+    std::uint8_t* d_arena = nullptr;
+    std::uint64_t* d_arena_off = nullptr;
+    void* d_ws = nullptr;
+    hipStream_t stream = nullptr;
+#include "snip_materialize.inc"
+    (void)rc;
 }
 
 void snippet_gather() {
