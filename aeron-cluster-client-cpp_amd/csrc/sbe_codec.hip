@@ -282,10 +282,21 @@ struct Lay {
 #ifndef SBE_TM_RPT
 #define SBE_TM_RPT 32  // A/B builds only (scripts/abv.py)
 #endif
+// Session frames take 32-record tiles (two lanes a record) since the pack loop is chosen per launch:
+// their virtual tiles fill one 8 KiB window with ~29 frames, which two lanes a record compose in
+// one pass (session pack 131.8 -> 126.1 us on rotated inputs, profiles/r06_ab_rpt.log; with the
+// tile loop alone 64-record tiles had won, 156 -> 144 us, round 3).  OrderRequestLite keeps 64
+// (144.4 -> 155.3 us with 32).
+#ifndef SBE_TMS_RPT
+#define SBE_TMS_RPT 32
+#endif
+#ifndef SBE_L3_RPT
+#define SBE_L3_RPT 64  // A/B builds only
+#endif
 using LayTM = Lay<0, 16, 5, true, SBE_TM_RPT>;
-using LayTMS = Lay<32, 16, 5, true, 64>;
+using LayTMS = Lay<32, 16, 5, true, SBE_TMS_RPT>;
 using LayL2 = Lay<0, 12, 2, false, 64>;
-using LayL3 = Lay<0, 12, 3, false, 64>;
+using LayL3 = Lay<0, 12, 3, false, SBE_L3_RPT>;
 static_assert(LayTM::kOvh == SBE_TM_WIRE_OVERHEAD && LayTM::ovh(true) == SBE_TM_REF_OVERHEAD, "TM layout");
 static_assert(LayL2::kOvh == SBE_LITE_OVERHEAD(2) && LayTMS::kPre == SBE_SESSION_HDR_LEN, "layouts");
 // the layout's tile shape as local constants (functions templated on the layout)
