@@ -1145,8 +1145,11 @@ __device__ __forceinline__ void write_texts(const JsonArgs& a, lw8* win, uint32_
     }
 }
 
+#ifndef SBE_OJ_MINW  // A/B builds: minimum waves per SIMD the writing launch's registers must allow
+#define SBE_OJ_MINW 1
+#endif
 template <uint32_t kWhat>
-__global__ __launch_bounds__(kWWave) void order_json_write(JsonArgs a) {
+__global__ __launch_bounds__(kWWave, SBE_OJ_MINW) void order_json_write(JsonArgs a) {
     constexpr uint32_t kOpw = WShape<kWhat>::kOpw;
     static_assert(kBlock % kOpw == 0, "a writing tile lies inside one sizing block");
     __shared__ __attribute__((aligned(16))) uint8_t win[WShape<kWhat>::kWinB];

@@ -1078,9 +1078,29 @@ __device__ __forceinline__ void lds_dw5(lds_cu8* inb, int32_t i, uint32_t (&d)[5
     }
 }
 
+// SBE_CHUNK_UA (A/B builds): a chunk at any staged byte position as ONE unaligned ds_read_b128
+// (the LDS replays the misaligned access) instead of five dword reads and four v_alignbyte.
+// Fewer instructions, but the replays cost more: fixed-256 pack 94.7 -> 99.0 us, config 4 706.3
+// -> 709.3, session 125.6 -> 128.6, OrderRequestLite 144.6 -> 150.2 (profiles/r06_ab_ua.log).
+#ifndef SBE_CHUNK_UA
+#define SBE_CHUNK_UA 0
+#endif
+typedef uint32_t u32x4_ua1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) const u32x4_ua1 lds_cu32x4_ua;
+// the 16 bytes at staged byte u, u clamped to [-kInSlack, 4 * imax] (a clamped read only ever feeds
+// don't-care bytes; 4 * imax + 16 <= the dword form's last byte read)
+__device__ __forceinline__ u32x4 lds_chunk_ua(lds_cu8* inb, int32_t u, int32_t imax) {
+    const int32_t lo = -kInSlack, hi = 4 * imax;
+    u = u < lo ? lo : (u > hi ? hi : u);
+    const u32x4_ua1 x = *reinterpret_cast<lds_cu32x4_ua*>(inb + u);
+    u32x4 v;
+    v.x = x.x; v.y = x.y; v.z = x.z; v.w = x.w;
+    return v;
+}
 // the 16 bytes at staged-input position u (any alignment); the base is clamped into the array
 // (a clamped read only ever feeds don't-care bytes)
 __device__ __forceinline__ u32x4 chunk_lds(lds_cu8* inb, int32_t u, int32_t imax) {
+    if (SBE_CHUNK_UA) return lds_chunk_ua(inb, u, imax);
     int32_t i = u >> 2;
     i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax ? imax : i);
     const uint32_t sh = (uint32_t)u & 3u;
@@ -1249,19 +1269,31 @@ __device__ __forceinline__ void chunk_pass(lds_u8* wout, lds_cu8* inb, lds_i32* 
         }
         u[k] = p - E.sh0 - 2 * zone_of(E, p - E.rw);
     }
+#if SBE_CHUNK_UA
+    u32x4 w[kCpl];
+#else
     uint32_t d[kCpl][5];
+#endif
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
+#if SBE_CHUNK_UA
+        w[k] = lds_chunk_ua(inb, u[k], imax - 1);
+#else
         int32_t i = u[k] >> 2;
         i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax - 1 ? imax - 1 : i);
         lds_dw5(inb, i, d[k]);
+#endif
     }
     lds_u8* const wl = wout + lb + (lb >> 8) * kRowPad;  // padded rows never split a lane
 #pragma unroll
     for (int k = 0; k < kCpl; ++k) {
         if (k >= kk) break;
+#if SBE_CHUNK_UA
+        const u32x4 v = w[k];
+#else
         const u32x4 v = align4(d[k][0], d[k][1], d[k][2], d[k][3], d[k][4], (uint32_t)u[k] & 3u);
+#endif
         if (lb + 16 * k < wlen) *reinterpret_cast<lds_u32x4*>(wl + 16 * k) = v;
     }
 }
@@ -1628,20 +1660,32 @@ __device__ __forceinline__ bool compose_records(const EncArgs& ea, lds_u8* wout,
     auto group = [&](auto kGc, int32_t i0) {
         constexpr int kG = decltype(kGc)::value;
         int32_t u[kG];
+#if SBE_CHUNK_UA
+        u32x4 w[kG];
+#else
         uint32_t d[kG][5];
+#endif
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
             const int32_t X = 16 * (cb + i0 + k) - brw;
             const int32_t f = (X >= bz1) + (X >= bz2) + (X >= bz3) + (X >= bz4);
             u[k] = bsrc0 + X - 2 * f;
+#if SBE_CHUNK_UA
+            w[k] = lds_chunk_ua(inb, u[k], imax - 1);
+#else
             int32_t i = u[k] >> 2;
             i = i < -kInSlack / 4 ? -kInSlack / 4 : (i > imax - 1 ? imax - 1 : i);
             lds_dw5(inb, i, d[k]);
+#endif
         }
 #pragma unroll
         for (int k = 0; k < kG; ++k) {
             // the zone of the chunk's first byte; string starts inside it: zone_fixup
+#if SBE_CHUNK_UA
+            const u32x4 v = w[k];
+#else
             const u32x4 v = align4(d[k][0], d[k][1], d[k][2], d[k][3], d[k][4], (uint32_t)u[k] & 3u);
+#endif
             if (i0 + k < n_mine) {
                 const int32_t p = 16 * (cb + i0 + k);
                 *reinterpret_cast<lds_u32x4*>(wout + wout_addr(p)) = v;
