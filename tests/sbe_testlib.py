@@ -656,6 +656,40 @@ def var_orders(n: int, seed: int = 0x5EED0004):
     return arena, str_len, ts
 
 
+def vt_mixed(n: int, pattern: str, seed: int = 21):
+    """Batches the pack kernel runs on its virtual-tile loop (first superblock averages ~265 B
+    records, so a 32-record tile's output ends just past one 8 KiB window) with the records that change
+    window arithmetic mixed in: E109 records (no output bytes), 65534-byte and 70000-byte fields,
+    empty records, timestamp 0.  pattern: "sprinkled" (1% edge records at random), "zero_run" (a
+    run of 700 E109/empty records in the second superblock: tiles with no output), "long_run" (16
+    records of ~64 KB in a row, each spanning several windows)."""
+    rng = np.random.default_rng(seed)
+    L = np.zeros((n, 5), np.uint32)
+    L[:, 0] = rng.integers(3, 12, n)
+    L[:, 1] = rng.integers(8, 14, n)
+    L[:, 2] = 29
+    L[:, 3] = rng.integers(140, 171, n)
+    L[:, 4] = rng.integers(20, 40, n)
+    edges = np.array([[65535, 0, 0, 0, 0], [0, 0, 0, 65535, 0], [0, 0, 0, 0, 0], [65534, 3, 29, 1, 0],
+                      [70000, 1, 1, 1, 1], [1, 2, 3, 4, 5], [0, 0, 0, 65534, 65534]], np.uint32)
+    if pattern == "sprinkled":
+        idx = rng.choice(n, n // 100, replace=False)
+        L[idx] = edges[rng.integers(0, len(edges), idx.size)]
+    elif pattern == "zero_run":
+        lo = 4096 + 300
+        L[lo: lo + 700] = np.where((np.arange(700) % 3 == 0)[:, None], edges[2], edges[0])
+    elif pattern == "long_run":
+        lo = 4096 + 1000
+        L[lo: lo + 16, 3] = 65534
+        L[lo: lo + 16, 4] = rng.integers(0, 65535, 16)
+    else:
+        raise ValueError(pattern)
+    arena = rng.integers(0, 256, int(L.sum(dtype=np.int64)), dtype=np.uint8)
+    ts = rng.integers(1, 2**63, n, dtype=np.uint64)
+    ts[::11] = 0
+    return arena, L, ts
+
+
 def _s64(c: int) -> int:
     return c - (1 << 64) if c >= 1 << 63 else c
 

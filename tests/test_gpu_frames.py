@@ -70,6 +70,13 @@ def test_session_edges(codec):
         check_session(codec, arena, L, ts, 42, 43, flags=flags, ts_default=99)
 
 
+@pytest.mark.parametrize("pattern", ["sprinkled", "zero_run", "long_run"])
+def test_session_virtual_tiles_with_edges(codec, pattern):
+    arena, L, ts = T.vt_mixed(3 * 4096 + 77, pattern, seed=22)
+    for flags in (0, T.ENC_REF_TRUNCATE8):
+        check_session(codec, arena, L, ts, 5, -9, flags=flags, ts_default=77)
+
+
 def lite_gpu(codec, t, arena, L, tid, seq, str_off=None):
     nf = T.LITE_NF[t]
     a = to_dev(arena if arena.size else np.zeros(16, np.uint8), torch.uint8)

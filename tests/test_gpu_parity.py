@@ -146,6 +146,15 @@ def test_encode_edges(codec):
         check_encode(codec, arena, L, ts, flags=flags, ts_default=1_760_000_000_123)
 
 
+@pytest.mark.parametrize("flags", [0, T.ENC_REF_TRUNCATE8])
+@pytest.mark.parametrize("pattern", ["sprinkled", "zero_run", "long_run"])
+def test_encode_virtual_tiles_with_edges(codec, pattern, flags):
+    """The virtual-tile pack loop (chosen per launch from the first superblock's average tile, see
+    vt_pays in sbe_codec.hip) over E109 records, tiles with no output and records spanning windows."""
+    arena, L, ts = T.vt_mixed(3 * 4096 + 123, pattern)
+    check_encode(codec, arena, L, ts, flags=flags, ts_default=1_760_000_000_456)
+
+
 def field_length_records():
     """Every field length 0..80 in every field position, the other fields (7L + 13k) mod 81: 405
     records whose tiles mix empty, 1..3-byte and ~80-byte strings (the C++ host test builds the same
