@@ -2,7 +2,8 @@
 decode, every record's five views copied into one arena, so the strings outlive the input as the
 reference's ParseResult strings do (include/aeron_cluster/sbe_messages.hpp:306-328).  Bit-exact
 bytes and offsets vs the views of the oracle's own decode (tests/sbe_testlib.py oracle_materialize),
-in every decode mode, on mixed, fixed-256, Lite and edge records, with short capacities (nothing
+in every decode mode, on mixed, fixed-256, variable-length (views up to 65534 B), session-framed,
+Lite and edge records, with short capacities (nothing
 past the capacity is written) and an empty batch."""
 import numpy as np
 import pytest
@@ -42,6 +43,33 @@ def test_gpu_materialize_matches_oracle(codec, mode, work):
     got, got_off = run(codec, data, off, mode)
     assert np.array_equal(got_off, exp_off)
     assert got[: exp.size].tobytes() == exp.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("work", ["var_long", "session"])
+def test_gpu_materialize_long_views_and_frames(codec, work):
+    """Views of every length up to 65534 B (a thread copies its record's views in 16-byte steps; the
+    last step of a view may run into the next view of the same record, never past the record's
+    arena range) and session frames (views into the schema-111-wrapped record)."""
+    if work == "var_long":
+        arena, L, ts = T.var_orders(6000, seed=77)
+        L = L.copy()
+        rng = np.random.default_rng(5)
+        idx = rng.choice(len(L), 40, replace=False)
+        L[idx, 3] = rng.integers(1, 65535, idx.size)
+        L[idx[:5], 4] = 65534
+        L[idx[5:10]] = 0
+        arena = rng.integers(32, 127, int(L.sum(dtype=np.int64)), dtype=np.uint8)
+        data, off, _ = T.oracle_encode(arena, L, ts)
+    else:
+        arena, L, ts = T.var_orders(8000, seed=78)
+        data, off, _ = T.oracle_encode_session(arena, L, ts, 7, -3, None, T.ENC_REF_TRUNCATE8, 0)
+    for mode in (0, 1):
+        dec = T.oracle_decode(data, off, mode)
+        exp, exp_off = T.oracle_materialize(data, off, dec)
+        got, got_off = run(codec, data, off, mode)
+        assert np.array_equal(got_off, exp_off)
+        assert got[: exp.size].tobytes() == exp.tobytes()
 
 
 @pytest.mark.gpu
