@@ -4098,13 +4098,36 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
 
 // ------------------------------------------------------------------------------------------
 // MATERIALIZE (sbe_materialize_views): the decoded views copied into an arena.  Three launches:
-// per-1024-record block view bytes, one workgroup scanning the block sums, and the copy, where
-// each thread takes one record: its arena base from the block prefix plus a block scan, its five
-// views as unaligned 16-byte loads and stores (a view's last chunk may run into the next view's
-// bytes, which the same thread writes afterwards; the record's last view ends bytewise, so no
-// thread writes another record's bytes).
+// mat_sums (view bytes per 64-record tile and per 1024-record block), mat_scan_blocks (one
+// workgroup: the exclusive scan of the block sums, the arena total into arena_off[5 n]) and
+// mat_copy, one wave per tile.  A tile's views are one contiguous range of the arena (its base: the
+// block prefix plus the sums of the block's earlier tiles plus a wave scan).  Each lane stages its
+// record's views into an LDS window as 16-byte chunks, the record's chunks dealt in batches of
+// kMatBatch loads in flight at once (a view's last chunk is the 16 bytes ending at the view's end,
+// overlapping the chunk before it with the same bytes; a view under 16 bytes is written bytewise
+// from one 16-byte load that stays inside the record), then the wave stores the window with 16-byte
+// coalesced nontemporal stores and moves it on to the first record not yet written.  A record
+// larger than the window is copied by its own lane straight to the arena.  Measured (1 M fixed-256
+// records, all three launches; profiles/r06_ab_mat*.log): one thread a record copying straight to
+// the arena 0.823 ms (every store instruction wrote 64 scattered 16-byte pieces); the LDS window
+// with one dependent load a chunk 0.184 ms; batches of 1 / 4 / 8 chunk loads 0.221 / 0.169 / 0.170
+// ms (and 0.20 while the large-record path was out of line: its arrays went to scratch); 8 or 12
+// KiB windows, or registers for 4 waves per SIMD, 0.168-0.190 ms.
 // ------------------------------------------------------------------------------------------
 constexpr int kMatBlk = 1024;
+constexpr int kMatTile = kWave;                       // records per copy wave
+constexpr int kMatTpb = kMatBlk / kMatTile;           // tiles per block
+#ifndef SBE_MAT_WIN  // A/B builds
+#define SBE_MAT_WIN 16384
+#endif
+#ifndef SBE_MAT_MINW  // A/B builds: waves per SIMD the copy's registers must allow
+#define SBE_MAT_MINW 1
+#endif
+constexpr int32_t kMatWin = SBE_MAT_WIN;              // LDS window bytes of a copy wave
+#ifndef SBE_MAT_BATCH
+#define SBE_MAT_BATCH 4
+#endif
+constexpr int kMatBatch = SBE_MAT_BATCH;              // chunk loads of a lane in flight at once
 struct MatArgs {
     const uint8_t* in;
     const uint64_t* rec_off;
@@ -4116,6 +4139,7 @@ struct MatArgs {
     uint64_t cap;
     uint64_t* arena_off;
     uint64_t* bsum;  // per block: view bytes, then (in place) their exclusive scan
+    uint64_t* tsum;  // per tile: view bytes
 };
 __device__ __forceinline__ uint64_t mat_rec_bytes(const MatArgs& a, uint64_t i) {
     if (i >= a.n) return 0;
@@ -4141,8 +4165,12 @@ __device__ __forceinline__ uint64_t mat_block_scan(uint64_t v, uint64_t& total) 
     return pre + inc - v;
 }
 __global__ __launch_bounds__(kMatBlk) void mat_sums(MatArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * kMatBlk + threadIdx.x;
+    const uint64_t v = mat_rec_bytes(a, i);
+    const uint64_t t = wave_sum64(v);
+    if ((threadIdx.x & (kWave - 1)) == 0 && i < a.n) a.tsum[i / kMatTile] = t;
     uint64_t tot;
-    (void)mat_block_scan(mat_rec_bytes(a, (uint64_t)blockIdx.x * kMatBlk + threadIdx.x), tot);
+    (void)mat_block_scan(v, tot);
     if (threadIdx.x == 0) a.bsum[blockIdx.x] = tot;
 }
 __global__ __launch_bounds__(kMatBlk) void mat_scan_blocks(MatArgs a, uint64_t nb) {
@@ -4160,37 +4188,180 @@ __global__ __launch_bounds__(kMatBlk) void mat_scan_blocks(MatArgs a, uint64_t n
     if (threadIdx.x == 0) a.arena_off[5 * a.n] = carry;
 }
 typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
-__global__ __launch_bounds__(kMatBlk) void mat_copy(MatArgs a) {
-    const uint64_t i = (uint64_t)blockIdx.x * kMatBlk + threadIdx.x;
-    uint64_t tot;
-    const uint64_t base = a.bsum[blockIdx.x] + mat_block_scan(mat_rec_bytes(a, i), tot);
-    if (i >= a.n) return;
-    const uint8_t* rec = a.in + a.rec_off[i];
-    const uint64_t rl = a.rec_off[i + 1] - a.rec_off[i];
-    uint32_t L[5], O[5];
-    uint64_t at[6];
-    at[0] = base;
+typedef __attribute__((address_space(3))) u32x4_ua lds_u32x4_ua;
+typedef __attribute__((address_space(3))) uint8_t mat_lds8;
+// Views [0, k_end) of a record (arena offsets at[], lengths L[], record-relative sources O[]) from
+// rec straight to the arena at dst (= arena byte at[0]), one lane: whole 16-byte chunks, a view's
+// last chunk running into the next view (written afterwards) when the source stays inside the
+// record (rl bytes) and the destination before lim; the last view's tail bytewise.  The path of
+// records larger than an LDS window.
+__device__ __forceinline__ void mat_views_direct(uint8_t* dst, const uint8_t* rec, uint64_t rl, const uint64_t (&at)[6],
+                                                 const uint32_t (&L)[5], const uint32_t (&O)[5], int k_end, uint64_t lim) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        L[k] = a.view_len[5 * i + k];
-        O[k] = a.view_off[5 * i + k];
-        at[k + 1] = at[k] + L[k];
-        a.arena_off[5 * i + k] = at[k];
-    }
-    const uint64_t rec_end = at[5] < a.cap ? at[5] : a.cap;  // this record's bytes end here
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        if (L[k] == 0 || at[k + 1] > a.cap) continue;  // views past the capacity are not written
+        if (k >= k_end || L[k] == 0) continue;
         const uint8_t* src = rec + O[k];
-        uint8_t* dst = a.arena + at[k];
+        uint8_t* d = dst + (at[k] - at[0]);
         uint32_t c = 0;
-        // whole 16-byte chunks; the view's last one may run into the next view (which this thread
-        // writes afterwards) when it stays inside the record on both sides
-        for (; c + 16 <= L[k] || (c < L[k] && at[k] + c + 16 <= rec_end && O[k] + c + 16 <= rl); c += 16) {
+        for (; c + 16 <= L[k] || (c < L[k] && at[k] + c + 16 <= lim && O[k] + c + 16 <= rl); c += 16) {
             const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(src + c);
-            __builtin_nontemporal_store(v, reinterpret_cast<u32x4_ua*>(dst + c));
+            __builtin_nontemporal_store(v, reinterpret_cast<u32x4_ua*>(d + c));
         }
-        for (; c < L[k]; ++c) dst[c] = src[c];  // the record's last bytes: never past its end
+        for (; c < L[k]; ++c) d[c] = src[c];
+    }
+}
+// byte o (0..15) of a 16-byte block, by 64-bit shifts (no private array)
+__device__ __forceinline__ uint8_t mat_byte(const u32x4_ua& v, uint32_t o) {
+    const uint64_t h = (o & 8) ? ((uint64_t)v.w << 32 | v.z) : ((uint64_t)v.y << 32 | v.x);
+    return (uint8_t)(h >> (8 * (o & 7)));
+}
+__device__ __forceinline__ uint64_t mat_wave_min(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t t = __shfl_xor(v, d, kWave);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t mat_wave_max(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t t = __shfl_xor(v, d, kWave);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+// Views [0, k_end) of a record into the LDS window at w (= arena byte at[0]): chunk q of the record
+// (views in order, ceil(L / 16) chunks a view, chunk j of a view at min(16 j, L - 16)), kMatBatch
+// loads issued before their LDS stores.  A view under 16 bytes: one 16-byte load inside the record
+// (from the view's start, or ending at its end) and its bytes stored one by one.
+__device__ __forceinline__ void mat_views_lds(mat_lds8* w, const uint8_t* rec, uint64_t rl, const uint64_t (&at)[6],
+                                              const uint32_t (&L)[5], const uint32_t (&O)[5], int k_end) {
+    uint32_t cc[6];  // first chunk of each view
+    cc[0] = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) cc[k + 1] = cc[k] + (k < k_end ? (L[k] + 15) >> 4 : 0u);
+    const uint32_t nq = cc[5];
+    for (uint32_t q0 = 0; q0 < nq; q0 += kMatBatch) {
+        u32x4_ua v[kMatBatch];
+        uint32_t dof[kMatBatch], bo[kMatBatch], bm[kMatBatch];
+#pragma unroll
+        for (int b = 0; b < kMatBatch; ++b) {
+            const uint32_t q = q0 + b;
+            // the view holding chunk q (views past k_end have no chunks)
+            uint32_t Lk = L[0], Ok = O[0], ck = 0;
+            uint64_t ak = at[0];
+#pragma unroll
+            for (int k = 1; k < 5; ++k)
+                if (q >= cc[k]) {
+                    Lk = L[k];
+                    Ok = O[k];
+                    ck = cc[k];
+                    ak = at[k];
+                }
+            const uint32_t j = q - ck;
+            uint32_t s;   // source offset in the record of the 16 loaded bytes
+            uint32_t d;   // window offset of the first byte stored
+            bo[b] = 0;    // first loaded byte stored
+            bm[b] = 16;   // bytes stored (16: one 16-byte store)
+            if (Lk >= 16) {
+                const uint32_t p = 16 * j < Lk - 16 ? 16 * j : Lk - 16;
+                s = Ok + p;
+                d = (uint32_t)(ak - at[0]) + p;
+            } else {  // a short view: its bytes from one load inside the record
+                const bool fwd = (uint64_t)Ok + 16 <= rl;
+                s = fwd ? Ok : (Ok + Lk >= 16 ? Ok + Lk - 16 : 0u);
+                bo[b] = fwd ? 0u : (Ok + Lk >= 16 ? 16u - Lk : Ok);
+                bm[b] = Lk;
+                d = (uint32_t)(ak - at[0]);
+                if (rl < 16) {  // a record under 16 bytes: no load fits inside it; bytewise below
+                    bm[b] = 0x100u | Lk;
+                    bo[b] = Ok;
+                }
+            }
+            dof[b] = d;
+            if (q < nq && bm[b] <= 16) v[b] = *reinterpret_cast<const u32x4_ua*>(rec + s);
+        }
+#pragma unroll
+        for (int b = 0; b < kMatBatch; ++b) {
+            if (q0 + b >= nq) break;
+            if (bm[b] == 16) {
+                *reinterpret_cast<lds_u32x4_ua*>(w + dof[b]) = v[b];
+            } else if (bm[b] < 16) {
+                for (uint32_t t = 0; t < bm[b]; ++t) w[dof[b] + t] = mat_byte(v[b], bo[b] + t);
+            } else {
+                for (uint32_t t = 0; t < (bm[b] & 0xffu); ++t) w[dof[b] + t] = rec[bo[b] + t];
+            }
+        }
+    }
+}
+__global__ __launch_bounds__(kWave, SBE_MAT_MINW) void mat_copy(MatArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kMatWin];
+    const int lane = threadIdx.x;
+    const uint64_t t = blockIdx.x, i = t * kMatTile + (uint64_t)lane;
+    const bool live = i < a.n;
+    uint32_t L[5] = {0, 0, 0, 0, 0}, O[5] = {0, 0, 0, 0, 0};
+    uint64_t r0 = 0, r1 = 0, bytes = 0;
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            L[k] = a.view_len[5 * i + k];
+            O[k] = a.view_off[5 * i + k];
+            bytes += L[k];
+        }
+        r0 = a.rec_off[i];
+        r1 = a.rec_off[i + 1];
+    }
+    // base: the block's prefix, the block's tiles before this one, the wave's scan
+    const uint64_t b = t / kMatTpb, t0 = b * kMatTpb;
+    const uint64_t pre = (uint64_t)lane < t - t0 ? a.tsum[t0 + (uint64_t)lane] : 0ull;
+    const uint64_t o = a.bsum[b] + wave_sum64(pre) + wave_incl_scan64(bytes, lane) - bytes;
+    uint64_t at[6];
+    at[0] = o;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) at[k + 1] = at[k] + L[k];
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) a.arena_off[5 * i + k] = at[k];
+    }
+    // views written: those ending within the capacity (a prefix: at[] is non-decreasing)
+    int k_end = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) k_end += (live && at[k + 1] <= a.cap) ? 1 : 0;
+    uint64_t fit = o;  // end of this record's written bytes
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        if (k < k_end) fit = at[k + 1];
+    const uint8_t* rec = a.in + r0;
+    const uint64_t rl = r1 - r0;
+    bool done = fit == o;
+    if (!done && fit - o > (uint64_t)(kMatWin - 16)) {  // larger than any window: straight to the arena
+        mat_views_direct(a.arena + o, rec, rl, at, L, O, k_end, fit);
+        done = true;
+    }
+    uint64_t start = mat_wave_min(done ? ~0ull : o);
+    while (start != ~0ull) {  // uniform
+        const uint64_t wbase = start - (uint64_t)((reinterpret_cast<uintptr_t>(a.arena) + start) & 15u);
+        uint64_t my_end = 0;
+        if (!done && fit - wbase <= (uint64_t)kMatWin) {
+            mat_views_lds((mat_lds8*)win + (o - wbase), rec, rl, at, L, O, k_end);
+            done = true;
+            my_end = fit;
+        }
+        const uint64_t cend = mat_wave_max(my_end);
+        __syncthreads();
+        const uint64_t nch = (cend - wbase + 15) / 16;
+        for (uint64_t c = (uint64_t)lane; c < nch; c += kWave) {
+            const uint64_t x0 = wbase + 16 * c;  // arena + x0 is 16-byte aligned
+            if (x0 >= start && x0 + 16 <= cend) {
+                const u32x4 v = *(const __attribute__((address_space(3))) u32x4*)(win + 16 * c);
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(a.arena + x0));
+            } else {
+                for (uint64_t x = x0 < start ? start : x0; x < x0 + 16 && x < cend; ++x) a.arena[x] = win[x - wbase];
+            }
+        }
+        __syncthreads();
+        start = mat_wave_min(done ? ~0ull : o);
     }
 }
 
@@ -5140,7 +5311,9 @@ int sbe_eval_sequence_numbers(const uint8_t* in, const uint64_t* rec_off, uint64
     return record_hip(hipGetLastError());
 }
 
-size_t sbe_materialize_workspace_size(uint64_t n) { return (size_t)(8 * ((n + kMatBlk - 1) / kMatBlk) + 16); }
+size_t sbe_materialize_workspace_size(uint64_t n) {
+    return (size_t)(8 * ((n + kMatBlk - 1) / kMatBlk) + 8 * ((n + kMatTile - 1) / kMatTile) + 32);
+}
 
 int sbe_materialize_views(const uint8_t* in, const uint64_t* rec_off, uint64_t n, const sbe_decoded* dec,
                           uint8_t* arena, uint64_t arena_capacity, uint64_t* arena_off, void* workspace,
@@ -5151,13 +5324,14 @@ int sbe_materialize_views(const uint8_t* in, const uint64_t* rec_off, uint64_t n
     if (!in || !rec_off || !dec || !dec->status || !dec->view_off || !dec->view_len || !workspace) return SBE_EINVAL;
     if (!arena && arena_capacity) return SBE_EINVAL;
     if (workspace_bytes < sbe_materialize_workspace_size(n)) return SBE_ENOSPC;
-    const uint64_t nb = (n + kMatBlk - 1) / kMatBlk;
-    if (nb > 0xffffffffull) return SBE_EINVAL;
+    const uint64_t nb = (n + kMatBlk - 1) / kMatBlk;      // mat_sums blocks
+    const uint64_t nt = (n + kMatTile - 1) / kMatTile;    // copy waves
+    if (nt > 0xffffffffull) return SBE_EINVAL;
     uint64_t* bsum = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(workspace) + 15) & ~(uintptr_t)15);
-    MatArgs a{in, rec_off, n, dec->status, dec->view_off, dec->view_len, arena, arena_capacity, arena_off, bsum};
+    MatArgs a{in, rec_off, n, dec->status, dec->view_off, dec->view_len, arena, arena_capacity, arena_off, bsum, bsum + nb};
     hipLaunchKernelGGL(mat_sums, dim3((uint32_t)nb), dim3(kMatBlk), 0, s, a);
     hipLaunchKernelGGL(mat_scan_blocks, dim3(1), dim3(kMatBlk), 0, s, a, nb);
-    hipLaunchKernelGGL(mat_copy, dim3((uint32_t)nb), dim3(kMatBlk), 0, s, a);
+    hipLaunchKernelGGL(mat_copy, dim3((uint32_t)nt), dim3(kWave), 0, s, a);
     return record_hip(hipGetLastError());
 }
 

@@ -9,6 +9,8 @@ algorithmic bytes per launch (computed from the actual record sizes) and its fra
   order_json             1 M Orders → Order::to_json payload + publish_order headers JSON (two calls)
   reassemble             1 M Aeron fragments (90 % whole messages, the rest BEGIN..END groups),
                          BEGIN/END reassembly (all its launches, torch events around the call)
+  materialize            1 M fixed-256 records' parse_message views copied into one arena
+                         (sbe_materialize_views, all its launches, torch events around the call)
 Rows whose buffers fit the 256 MB MALL a few times over rotate over --rotate (3) copies of their
 inputs and outputs (step k uses copy k mod R), as bench.py does, so no step finds its inputs in the
 cache a previous step left them in; config 4's 16.8 M-record batch (~6.5 GB) needs no rotation.
@@ -299,11 +301,52 @@ def row_order_json(steps, warmup):
     line("order_json", n, ms * 1e-3, {"sbe_order_to_json_batch x2 (payload + headers)": (ms, nbytes)})
 
 
+def row_materialize(steps, warmup):
+    """MATERIALIZE (sbe_materialize_views) after a parse_message decode of 1 M fixed-256 records:
+    every record's views copied into one arena (Σlen read and written, plus the
+    descriptors' offsets and lengths and rec_off read and 40 B of arena offsets written a record)."""
+    n = 1_000_000
+    arena, L, ts = T.fixed256_orders(n)
+    data, off, _ = T.oracle_encode(arena, L, ts)
+    d0, o0 = dev(data, torch.uint8), dev(off.astype(np.uint64), torch.int64)
+    ws = torch.empty(int(sbecodec.lib().sbe_materialize_workspace_size(n)) + 16, dtype=torch.uint8, device="cuda")
+
+    def make(k):
+        d, o = d0.clone(), o0.clone()
+        dec = sbecodec.decode_batch(d, o, sbecodec.DEC_PARSE_MESSAGE, out=sbecodec.alloc_decoded(n, "cuda"),
+                                    in_bytes=data.size)
+        return d, o, dec, torch.empty(data.size, dtype=torch.uint8, device="cuda"), \
+            torch.empty(5 * n + 1, dtype=torch.int64, device="cuda")
+    R = Rot(make)
+    torch.cuda.synchronize()
+    vbytes = int(R.sets[0][2].view_len[:n].to(torch.int64).sum().item())
+
+    def fn():
+        d, o, dec, ar, ao = R.next()
+        sbecodec.materialize_views(d, o, dec, arena=ar, arena_capacity=ar.numel(), arena_off=ao, workspace=ws)
+    for _ in range(warmup):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = 2 * vbytes + (40 + 8 + 40) * n
+    k = 200_000
+    dk = T.oracle_decode(data[: int(off[k])], off[: k + 1], T.DEC_PARSE, nthreads=CPU_THREADS)
+    set_cpu(cpu_rate(lambda: T.oracle_materialize(data[: int(off[k])], off[: k + 1], dk), k),
+            f"{k} records of the same batch, the oracle's view copy (numpy gather), 1 thread", cores=1)
+    line("materialize", n, ms * 1e-3, {"sbe_materialize_views (all launches)": (ms, nbytes)})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json")
+    ap.add_argument("--rows", default="mixed,var,session,lite301,lite201,reassemble,order_json,materialize")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
     ap.add_argument("--lib", help="library build to measure (A/B of variants; default: the product's)")
     ap.add_argument("--rotate", type=int, default=3, help="copies of a row's buffers the steps rotate over")
@@ -326,6 +369,8 @@ def main():
             row_reassemble(args.steps, args.warmup)
         elif r == "order_json":
             row_order_json(args.steps, args.warmup)
+        elif r == "materialize":
+            row_materialize(args.steps, args.warmup)
         elif r.startswith("lite"):
             row_lite(int(r[4:]), args.steps, args.warmup)
         torch.cuda.empty_cache()
