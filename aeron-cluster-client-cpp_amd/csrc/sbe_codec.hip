@@ -4112,7 +4112,8 @@ __global__ __launch_bounds__(256) void frag_copy(FragArgs a) {
 // the arena 0.823 ms (every store instruction wrote 64 scattered 16-byte pieces); the LDS window
 // with one dependent load a chunk 0.184 ms; batches of 1 / 4 / 8 chunk loads 0.221 / 0.169 / 0.170
 // ms (and 0.20 while the large-record path was out of line: its arrays went to scratch); 8 or 12
-// KiB windows, or registers for 4 waves per SIMD, 0.168-0.190 ms.
+// KiB windows, or registers for 4 waves per SIMD, 0.168-0.190 ms; the tile's input staged in a
+// second 16 KiB of LDS by coalesced loads first, 0.207 ms (5 workgroups per CU instead of 10).
 // ------------------------------------------------------------------------------------------
 constexpr int kMatBlk = 1024;
 constexpr int kMatTile = kWave;                       // records per copy wave
