@@ -19,8 +19,9 @@
 //  decode  (MessageParser::parse_message :513-551 / MessageHandler::on_egress
 //           include/aeron_cluster/message_handler.hpp:35-68 + decode_ack src/ack_decoder.cpp:29-105 /
 //           the Lite flyweights), one launch, one wave per 64-record tile:
-//    1. the tile's bytes are staged window by window (16 KiB windows; 12 KiB for batches of records
-//       over 256 B on average, 15 KiB up to 204 B, 8 KiB up to 112 B: sbe_decode_batch_sized) into
+//    1. the tile's bytes are staged window by window (16 KiB windows; 20 KiB for batches of records
+//       of 257-320 B on average, 13 KiB above, 15 KiB up to 204 B, 8 KiB up to 112 B:
+//       sbe_decode_batch_sized) into
 //       an XOR-swizzled LDS window with 16-byte loads; the second
 //       window's loads are issued before the first one is parsed
 //    2. each lane parses its record from LDS (template-ID dispatch per lane) and writes the
@@ -47,13 +48,17 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kTile = 64;                 // records per workgroup (one per lane)
 // LDS window bytes of the decode kernel: kWin for records up to 256 B on average (a 64-record
-// tile in one window), kWinWide for longer ones (more workgroups per CU; they take two or more
-// windows either way).  sbe_decode_batch_sized picks by the batch's average record size.
+// tile in one window), kWinWide for 257-320 B (a 64-record tile of 280-B session frames, 17.9 KB,
+// whole in one 20 KiB window: 8 workgroups per CU, where 12 KiB windows allowed 13 but took two
+// windows a tile; session-frame decode 71.8-73.7 -> 64.2-65.1 us, 300-B records 1890 -> 1846 us,
+// 320-B 1844 -> 1791 us at 4 M; 18 KiB read 64.1 us on the frames but 2300 / 2396 us on the 300 /
+// 320-B records, which it cannot hold whole; profiles/r06_ab_decsess{,2}.log, r06_ab_declarge.log).
+// sbe_decode_batch_sized picks by the batch's average record size.
 #ifndef SBE_DEC_WIN
 #define SBE_DEC_WIN 16384
 #endif
 #ifndef SBE_DEC_WIN_WIDE
-#define SBE_DEC_WIN_WIDE 12288
+#define SBE_DEC_WIN_WIDE 20480
 #endif
 constexpr uint32_t kWin = SBE_DEC_WIN;
 constexpr uint32_t kWinWide = SBE_DEC_WIN_WIDE;
@@ -78,8 +83,9 @@ constexpr uint64_t kWideAvg = 256;  // average record bytes above which the kWin
 constexpr uint32_t kWinMid = SBE_DEC_WIN_MID, kWinSmall = 8192;
 // Batches of records over kLargeAvg bytes on average (config 4: 387 B) take a 13 KiB window: a
 // 64-record tile of ~24.8 KB then fits two windows (12 KiB windows hold ~24.2 KB in two, so most
-// tiles paid a third).  Config 4 decode 422.4 -> 405.8 us at 4 M records; session frames (280 B)
-// stay on 12 KiB, where 13 KiB read 69.5 -> 72.0 us (profiles/r05_ab_decwide.log).
+// tiles paid a third).  Config 4 decode 422.4 -> 405.8 us at 4 M records (profiles/r05_ab_decwide.log).
+// Windows holding most config-4 tiles whole (25 / 27 KiB, 6 workgroups per CU) read 685.7 / 632.5
+// against 405.3 us (profiles/r06_ab_declarge.log).
 #ifndef SBE_DEC_WIN_LARGE  // A/B builds only
 #define SBE_DEC_WIN_LARGE 13312
 #endif
@@ -3186,7 +3192,8 @@ __device__ __forceinline__ void dec_tile(const DecArgs& a, uint64_t tile, uint32
 #define SBE_DEC_MINW_WIDE SBE_DEC_MINW
 #endif
 template <uint32_t kMode, uint32_t kWin>
-__global__ __launch_bounds__(kWave, (kWin == kWinWide || kWin == kWinLarge) ? SBE_DEC_MINW_WIDE : SBE_DEC_MINW) void sbe_decode_kernel(DecArgs a) {
+// the 20 KiB window's LDS allows 8 workgroups per CU, 2 waves per SIMD: its registers are sized for that
+__global__ __launch_bounds__(kWave, kWin == kWinWide && kWinWide > 16384 ? 2 : ((kWin == kWinWide || kWin == kWinLarge) ? SBE_DEC_MINW_WIDE : SBE_DEC_MINW)) void sbe_decode_kernel(DecArgs a) {
     __shared__ uint32_t win[kWin / 4];
     dec_tile<kMode, kWin>(a, blockIdx.x, win);
 }

@@ -32,9 +32,9 @@ def gpu_encode(codec, arena, str_len, ts, str_off=None, flags=0, ts_default=0):
 
 
 # the decode kernel shapes (LDS windows of a 64-record tile, chosen by sbe_decode_batch_sized from
-# the average record size in_bytes / n): 16 KiB (in_bytes 0: unknown), 13 KiB (over 320 B), 12 KiB
+# the average record size in_bytes / n): 16 KiB (in_bytes 0: unknown), 13 KiB (over 320 B), 20 KiB
 # (257..320 B), 15 KiB (113..204 B), 8 KiB (up to 112 B).  Values: in_bytes for a batch of n records.
-SHAPES = {"w16k": lambda n: 0, "w13k": lambda n: 1 << 62, "w12k": lambda n: 300 * n, "w15k": lambda n: 150 * n,
+SHAPES = {"w16k": lambda n: 0, "w13k": lambda n: 1 << 62, "w20k": lambda n: 300 * n, "w15k": lambda n: 150 * n,
           "w8k": lambda n: 1}
 
 
