@@ -2923,6 +2923,13 @@ __device__ __noinline__ Desc dec_record_glb(const uint8_t* in, uint64_t rs, uint
 // (bit k: chunk lane + 64 k holds a key-slice dword or a backslash byte), classified from the
 // staging registers (tiles with records over kSeqLaneRec bytes: `wide`), so the "_sequence_number"
 // scan needs no LDS pass of its own.
+// The decode's staging loads are nontemporal (the records are read once): against the default cache
+// policy, rotated inputs, fixed-256 55.4 / 57.2 us, config 3 58.5 / 59.6, session frames 63.4 /
+// 65.6, OrderRequestLite 66.5 / 71.0; one set re-read, fixed-256 56.3 / 58.4, config 4 410.9 / 430.9
+// (profiles/r06_ab_decntl_{rot,warm}.log)
+#ifndef SBE_DEC_NTL  // A/B builds: 0 = the decode's staging loads with the default cache policy
+#define SBE_DEC_NTL 1
+#endif
 template <uint32_t kW>
 __device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_t we, int lane,
                                           uint4 (&I)[dec_regs<kW>()]) {
@@ -2931,7 +2938,8 @@ __device__ __forceinline__ void dec_issue(const DecArgs& a, uint64_t wb, uint64_
 #pragma unroll
     for (int k = 0; k < dec_regs<kW>(); ++k) {
         const uint32_t ch = lane + kWave * k;
-        I[k] = ch < nch ? gload128_nt(src + 16ull * ch) : make_uint4(0, 0, 0, 0);
+        I[k] = ch < nch ? (SBE_DEC_NTL ? gload128_nt(src + 16ull * ch) : gload128(src + 16ull * ch))
+                        : make_uint4(0, 0, 0, 0);
     }
 }
 
