@@ -3929,8 +3929,12 @@ constexpr int kFcU = SBE_FC_U;
 #endif
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4_a1 g_u32x4_a1;
-#ifndef SBE_FC_NTL  // A/B builds: 1 = the copy's source loads nontemporal
-#define SBE_FC_NTL 0
+// The copy's source loads are nontemporal (each fragment is read once): on rotated inputs the row
+// read 157.0 / 157.0 / 156.9 -> 154.9 / 155.8 / 154.2 us over three alternations
+// (profiles/r06_ab_fc_rot.log; round 5, re-reading one batch every step, had them slower, 149.7 ->
+// 163.4 us); 2 / 8 chunks a lane a step 160.4-161.1 / 157.7-159.4 us.
+#ifndef SBE_FC_NTL  // A/B builds: 0 = default-policy source loads
+#define SBE_FC_NTL 1
 #endif
 __device__ __forceinline__ uint4 gload128_ua(uintptr_t addr) {  // any byte address (one global_load_dwordx4)
 #if SBE_FC_NTL
