@@ -4255,6 +4255,11 @@ __device__ __forceinline__ uint64_t mat_wave_max(uint64_t v) {
 // (views in order, ceil(L / 16) chunks a view, chunk j of a view at min(16 j, L - 16)), kMatBatch
 // loads issued before their LDS stores.  A view under 16 bytes: one 16-byte load inside the record
 // (from the view's start, or ending at its end) and its bytes stored one by one.
+// (nontemporal view loads: 0.165 -> 0.244 ms, profiles/r06_ab_matntl.log: a record's later chunks
+// re-read the lines its first loads brought in)
+#ifndef SBE_MAT_NTL  // A/B builds: 1 = the views' loads nontemporal
+#define SBE_MAT_NTL 0
+#endif
 __device__ __forceinline__ void mat_views_lds(mat_lds8* w, const uint8_t* rec, uint64_t rl, const uint64_t (&at)[6],
                                               const uint32_t (&L)[5], const uint32_t (&O)[5], int k_end) {
     uint32_t cc[6];  // first chunk of each view
@@ -4300,7 +4305,9 @@ __device__ __forceinline__ void mat_views_lds(mat_lds8* w, const uint8_t* rec, u
                 }
             }
             dof[b] = d;
-            if (q < nq && bm[b] <= 16) v[b] = *reinterpret_cast<const u32x4_ua*>(rec + s);
+            if (q < nq && bm[b] <= 16)
+                v[b] = SBE_MAT_NTL ? __builtin_nontemporal_load(reinterpret_cast<const u32x4_ua*>(rec + s))
+                                   : *reinterpret_cast<const u32x4_ua*>(rec + s);
         }
 #pragma unroll
         for (int b = 0; b < kMatBatch; ++b) {
